@@ -1,0 +1,96 @@
+"""ctypes binding of libiddgcn_hip.so (C-ABI declared in include/iddgcn.h).
+
+The product path has no CPU fallback: if the shared library is missing or was
+built for another ABI version, :func:`lib` raises immediately.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
+ABI_VERSION = 1
+
+ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
+
+vp = ctypes.c_void_p
+ci = ctypes.c_int
+cll = ctypes.c_longlong
+cf = ctypes.c_float
+
+
+class RowGemmArgs(ctypes.Structure):
+    """Mirror of iddgcn_rowgemm_t."""
+    _fields_ = [
+        ("M", ci), ("D", ci),
+        ("A", vp), ("a_idx", vp),
+        ("B", vp), ("b_trans", ci),
+        ("C", vp), ("accumulate", ci),
+        ("R", ci),
+        ("coef", vp), ("coef_idx", vp),
+        ("V", vp), ("v_idx", vp),
+        ("v_rel_stride", cll), ("v_row_stride", cll),
+        ("act", ci), ("aux", vp),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "iddgcn_abi_version": (ci, []),
+    "iddgcn_spmm_csr_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, ci]),
+    "iddgcn_rowgemm_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
+    "iddgcn_gemm_tn_blocks": (ci, [cll, ci]),
+    "iddgcn_gemm_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
+    "iddgcn_gemm_tn_narrow_blocks": (ci, [cll]),
+    "iddgcn_gemm_tn_narrow_f32": (ci, [vp, cll, ci, ci, vp, vp, vp, ci, vp, vp, ci]),
+    "iddgcn_alpha_fwd_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp]),
+    "iddgcn_combine_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cll, vp]),
+    "iddgcn_distmult_blocks": (ci, [cll]),
+    "iddgcn_distmult_bce_f32": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, ci]),
+    "iddgcn_seg_gather_reduce_f32": (ci, [vp, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "iddgcn_tail_seg_reduce_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, cll, vp, cll, vp, vp]),
+    "iddgcn_head_bwd_node_f32": (ci, [vp, ci, ci, ci, vp, vp, cll, vp, vp, vp, vp, vp, vp, cll, vp, vp]),
+    "iddgcn_reduce_slabs_f32": (ci, [vp, ci, cll, vp, vp, ci, cf]),
+    "iddgcn_adam_f32": (ci, [vp, cll, vp, vp, vp, vp, cf, cf, cf, cf, ci]),
+}
+
+_lib = None
+
+
+class IddgcnError(RuntimeError):
+    pass
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def load(path=LIB_PATH):
+    """Load the library and bind every symbol of include/iddgcn.h (no GPU call)."""
+    if not os.path.exists(path):
+        raise IddgcnError(
+            f"libiddgcn_hip.so not found at {path}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950). "
+            "There is no CPU fallback for the IDDGCN hot path.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.iddgcn_abi_version()
+    if v != ABI_VERSION:
+        raise IddgcnError(f"libiddgcn_hip ABI version {v}, expected {ABI_VERSION}")
+    return lib
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = load()
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        kind = {-1: "unsupported feature width D", -2: "unsupported relation count R",
+                -3: "invalid argument"}.get(rc, f"HIP error {rc}")
+        raise IddgcnError(f"{what} failed: {kind}")

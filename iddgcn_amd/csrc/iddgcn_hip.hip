@@ -1,0 +1,941 @@
+// libiddgcn_hip — MI355X (gfx950 / CDNA4) kernels for IDDGCN's multi-relational
+// graph convolution, forward and backward, behind the C-ABI of include/iddgcn.h.
+//
+// Design notes (DESIGN.md has the full version):
+//  * 64-lane wavefronts.  Row-wise memory-bound kernels map one row of D fp32 to
+//    D/4 lanes (one float4 = 16 B per lane), so a wave moves 1 KiB per instruction.
+//  * Dense D x D projections run on the exact-f32 MFMA v_mfma_f32_32x32x2_f32
+//    (157 TFLOP/s chip peak, bitwise an fmaf chain).  The D x D weight is kept in
+//    registers for the life of a persistent workgroup (one 32-column slab per
+//    wave, D/2 VGPRs), the streamed rows go HBM -> LDS (padded rows, conflict-free
+//    ds_read_b128 of 4 k-steps at once, k permuted identically on both operands).
+//  * No float atomics anywhere: scatters are deterministic segmented gathers over
+//    precomputed CSR-style permutations, and cross-block sums go through slabs
+//    reduced in block order.  Results are bitwise reproducible run to run.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/iddgcn.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define MAX_R 8
+#define EPS_BCE 1e-7f
+
+namespace {
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int m = LPR / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+inline int launch_status() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+inline bool dim_ok(int d) { return d == 32 || d == 64 || d == 128 || d == 256; }
+
+// ---------------------------------------------------------------------------
+// CSR SpMM: one row per group of D/4 lanes, sequential sum in CSR order.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void spmm_csr_kernel(int n_seg, int n_rows, const int* __restrict__ ptr,
+                                                       const int* __restrict__ col, const float* __restrict__ vals,
+                                                       const float* __restrict__ X, float* __restrict__ Y,
+                                                       int accumulate) {
+    constexpr int LPR = D / 4;
+    const long long grow = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
+    if (grow >= (long long)n_seg * n_rows) return;
+    const int s = (int)(grow / n_rows);
+    const int n = (int)(grow % n_rows);
+    const int* p = ptr + (long long)s * (n_rows + 1);
+    const int beg = p[n], end = p[n + 1];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int k = beg;
+    // two rows in flight, summed strictly in CSR order
+    for (; k + 1 < end; k += 2) {
+        const int c0 = col[k], c1 = col[k + 1];
+        f32x4 x0 = ld4(X + (long long)c0 * D + sub * 4);
+        f32x4 x1 = ld4(X + (long long)c1 * D + sub * 4);
+        if (vals) {
+            x0 *= vals[k];
+            x1 *= vals[k + 1];
+        }
+        acc += x0;
+        acc += x1;
+    }
+    if (k < end) {
+        f32x4 x0 = ld4(X + (long long)col[k] * D + sub * 4);
+        if (vals) x0 *= vals[k];
+        acc += x0;
+    }
+    float* y = Y + grow * D + sub * 4;
+    if (accumulate) acc += ld4(y);
+    st4(y, acc);
+}
+
+// ---------------------------------------------------------------------------
+// Row GEMM with fused epilogue on v_mfma_f32_32x32x2_f32.
+//   wave w: column slab cs = w % CS (32 output columns), row group rg = w / CS.
+//   B slab resident in VGPRs: breg[s] = B[kk(s,h)][c0+i],  kk(s,h) = 8(s/4) + 4h + s%4,
+//   A fragment for 4 consecutive k-steps = one ds_read_b128 of A_lds[row i][8q+4h..+3].
+// ---------------------------------------------------------------------------
+template <int D>
+struct RG {
+    static constexpr int CS = D / 32;
+    static constexpr int NW = CS >= 4 ? CS : 4;
+    static constexpr int RGS = NW / CS;
+    static constexpr int TR = RGS * 32;
+    static constexpr int LDA = D + 4;
+};
+
+struct RowGemmP {
+    int M;
+    const float* A; const int* a_idx;
+    const float* B; int b_trans;
+    float* C; int accumulate;
+    int R;
+    const float* coef; const int* coef_idx;
+    const float* V; const int* v_idx;
+    long long v_rel_stride, v_row_stride;
+    int act; const float* aux;
+    int tiles_per_block;
+};
+
+template <int D>
+__global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmP p) {
+    using C = RG<D>;
+    __shared__ __attribute__((aligned(16))) float As[C::TR * C::LDA];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int cs = wave % C::CS;
+    const int rg = wave / C::CS;
+    const int i = lane & 31, h = lane >> 5;
+    const int c0 = cs * 32;
+
+    float breg[D / 2];
+#pragma unroll
+    for (int s = 0; s < D / 2; ++s) {
+        const int kk = 8 * (s >> 2) + 4 * h + (s & 3);
+        breg[s] = p.b_trans ? p.B[(c0 + i) * D + kk] : p.B[kk * D + c0 + i];
+    }
+
+    const long long ntiles = ((long long)p.M + C::TR - 1) / C::TR;
+    const long long t_beg = (long long)blockIdx.x * p.tiles_per_block;
+    long long t_end = t_beg + p.tiles_per_block;
+    if (t_end > ntiles) t_end = ntiles;
+
+    for (long long tile = t_beg; tile < t_end; ++tile) {
+        const long long row0 = tile * C::TR;
+        __syncthreads();
+        constexpr int F4R = D / 4;
+        constexpr int TOT = C::TR * F4R;
+#pragma unroll
+        for (int it = 0; it < TOT / (C::NW * 64); ++it) {
+            const int idx = it * C::NW * 64 + threadIdx.x;
+            const int r = idx / F4R, c4 = idx % F4R;
+            const long long e = row0 + r;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (e < p.M) {
+                const long long src = p.a_idx ? (long long)p.a_idx[e] : e;
+                v = ld4(p.A + src * D + c4 * 4);
+            }
+            st4(As + r * C::LDA + c4 * 4, v);
+        }
+        __syncthreads();
+
+        f32x16 acc;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+        const float* arow = As + (rg * 32 + i) * C::LDA + 4 * h;
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            const f32x4 a4 = ld4(arow + 8 * q);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[0], breg[4 * q + 0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[1], breg[4 * q + 1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[2], breg[4 * q + 2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[3], breg[4 * q + 3], acc, 0, 0, 0);
+        }
+
+        const int c = c0 + i;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const long long e = row0 + rg * 32 + row;
+            if (e >= p.M) continue;
+            float v = acc[reg];
+            float* cp = p.C + e * D + c;
+            if (p.accumulate) v += *cp;
+            if (p.R > 0) {
+                const long long ci = p.coef_idx ? (long long)p.coef_idx[e] : e;
+                const long long vi = p.v_idx ? (long long)p.v_idx[e] : e;
+                const float* vb = p.V + vi * p.v_row_stride + c;
+                for (int r = 0; r < p.R; ++r) v += p.coef[ci * p.R + r] * vb[r * p.v_rel_stride];
+            }
+            if (p.act == IDDGCN_ACT_SIGMOID) {
+                v = sigmoidf_(v);
+            } else if (p.act == IDDGCN_ACT_DSIGMOID) {
+                const float x = p.aux[e * D + c];
+                v = v * (x * (1.0f - x));
+            }
+            *cp = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// TN reduction GEMM  C = A^T B  over many rows, partial per workgroup.
+//   wave w: output row tile ct = w % CT (32 rows of C), k-group g = w / CT.
+//   A^T fragment: lane (i,h), step s -> A_tile[2s+h][32ct+i]; B: B_tile[2s+h][32cj+i].
+// ---------------------------------------------------------------------------
+template <int D>
+struct TN {
+    static constexpr int CT = D / 32;
+    static constexpr int NW = CT >= 4 ? CT : 4;
+    static constexpr int G = NW / CT;
+    static constexpr int TK = 32;
+    static constexpr int TILE = TK * D;                   // floats per operand tile
+    static constexpr int RED = (G > 1) ? (NW * CT * 16 * 64) : 0;
+    static constexpr int LDS = (2 * TILE > RED) ? 2 * TILE : RED;
+};
+
+template <int D>
+__global__ __launch_bounds__(TN<D>::NW * 64) void gemm_tn_kernel(long long M, long long rows_per_block,
+                                                                  const float* __restrict__ A,
+                                                                  const float* __restrict__ B,
+                                                                  float* __restrict__ slab) {
+    using C = TN<D>;
+    __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+    float* As = lds;
+    float* Bs = lds + C::TILE;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ct = wave % C::CT, g = wave / C::CT;
+    const int i = lane & 31, h = lane >> 5;
+
+    f32x16 acc[C::CT];
+#pragma unroll
+    for (int cj = 0; cj < C::CT; ++cj)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[cj][j] = 0.f;
+
+    const long long r_beg = (long long)blockIdx.x * rows_per_block;
+    long long r_end = r_beg + rows_per_block;
+    if (r_end > M) r_end = M;
+
+    for (long long row0 = r_beg; row0 < r_end; row0 += C::TK) {
+        __syncthreads();
+        constexpr int F4R = D / 4;
+        constexpr int TOT = C::TK * F4R;
+#pragma unroll
+        for (int it = 0; it < TOT / (C::NW * 64); ++it) {
+            const int idx = it * C::NW * 64 + threadIdx.x;
+            const int r = idx / F4R, c4 = idx % F4R;
+            const long long e = row0 + r;
+            f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+            if (e < r_end) {
+                a = ld4(A + e * D + c4 * 4);
+                b = ld4(B + e * D + c4 * 4);
+            }
+            st4(As + r * D + c4 * 4, a);
+            st4(Bs + r * D + c4 * 4, b);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < C::TK / 2; ++s) {
+            if ((s % C::G) != g) continue;
+            const float a = As[(2 * s + h) * D + 32 * ct + i];
+#pragma unroll
+            for (int cj = 0; cj < C::CT; ++cj) {
+                const float b = Bs[(2 * s + h) * D + 32 * cj + i];
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[cj], 0, 0, 0);
+            }
+        }
+    }
+
+    if (C::G > 1) {
+        __syncthreads();
+        // groups 1..G-1 park their accumulators in LDS, group 0 adds them in group order
+        if (g > 0) {
+#pragma unroll
+            for (int cj = 0; cj < C::CT; ++cj)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) lds[((wave * C::CT + cj) * 16 + j) * 64 + lane] = acc[cj][j];
+        }
+        __syncthreads();
+        if (g == 0) {
+            for (int gg = 1; gg < C::G; ++gg) {
+                const int w2 = gg * C::CT + ct;
+#pragma unroll
+                for (int cj = 0; cj < C::CT; ++cj)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) acc[cj][j] += lds[((w2 * C::CT + cj) * 16 + j) * 64 + lane];
+            }
+        }
+    }
+    if (g == 0) {
+        float* out = slab + (long long)blockIdx.x * D * D;
+#pragma unroll
+        for (int cj = 0; cj < C::CT; ++cj)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int row = 32 * ct + (j & 3) + 8 * (j >> 2) + 4 * h;
+                out[row * D + 32 * cj + i] = acc[cj][j];
+            }
+    }
+}
+
+// out[D][R] partial of A^T dz and colsum(dz) per block; slab row layout [(D+1)][R]
+template <int D>
+__global__ __launch_bounds__(D) void gemm_tn_narrow_kernel(long long M, long long rows_per_block, int R,
+                                                           const float* __restrict__ A,
+                                                           const float* __restrict__ dz,
+                                                           float* __restrict__ slab) {
+    const int d = threadIdx.x;
+    float acc[MAX_R], accb[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) acc[r] = accb[r] = 0.f;
+    const long long r_beg = (long long)blockIdx.x * rows_per_block;
+    long long r_end = r_beg + rows_per_block;
+    if (r_end > M) r_end = M;
+    for (long long e = r_beg; e < r_end; ++e) {
+        const float a = A[e * D + d];
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+            if (r < R) {
+                const float z = dz[e * R + r];
+                acc[r] += a * z;
+                accb[r] += z;
+            }
+    }
+    float* out = slab + (long long)blockIdx.x * (D + 1) * R;
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) {
+            out[d * R + r] = acc[r];
+            if (d == 0) out[D * R + r] = accb[r];
+        }
+}
+
+// ---------------------------------------------------------------------------
+// alpha: z = x·Wa + ba ; s = softmax(z) ; w = sigmoid(s)
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void alpha_kernel(int M, int R, const float* __restrict__ X,
+                                                    const int* __restrict__ x_idx, const float* __restrict__ Wa,
+                                                    const float* __restrict__ ba, float* __restrict__ S_out,
+                                                    float* __restrict__ W_out) {
+    constexpr int LPR = D / 4;
+    const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
+    const bool live = row < M;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        const long long src = x_idx ? (long long)x_idx[row] : row;
+        x = ld4(X + src * D + sub * 4);
+    }
+    float z[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) {
+        float part = 0.f;
+        if (r < R) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) part += x[j] * Wa[(sub * 4 + j) * R + r];
+        }
+        z[r] = group_sum<LPR>(part);
+    }
+    if (!live || sub != 0) return;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) {
+            z[r] += ba[r];
+            mx = fmaxf(mx, z[r]);
+        }
+    float sum = 0.f;
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) {
+            z[r] = expf(z[r] - mx);
+            sum += z[r];
+        }
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) {
+            const float s = z[r] / sum;
+            S_out[row * R + r] = s;
+            W_out[row * R + r] = sigmoidf_(s);
+        }
+}
+
+// ---------------------------------------------------------------------------
+// combine (no GEMM): out = sigmoid(Y[yi] + sum_r coef[ci][r] * V_r[vi])
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void combine_kernel(int M, int R, const float* __restrict__ Y,
+                                                      const int* __restrict__ y_idx, const float* __restrict__ coef,
+                                                      const int* __restrict__ coef_idx, const float* __restrict__ V,
+                                                      const int* __restrict__ v_idx, long long v_rel_stride,
+                                                      float* __restrict__ out) {
+    constexpr int LPR = D / 4;
+    const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
+    if (e >= M) return;
+    const long long yi = y_idx ? (long long)y_idx[e] : e;
+    const long long ci = coef_idx ? (long long)coef_idx[e] : e;
+    const long long vi = v_idx ? (long long)v_idx[e] : e;
+    f32x4 v = ld4(Y + yi * D + sub * 4);
+    for (int r = 0; r < R; ++r) {
+        const float w = coef[ci * R + r];
+        const f32x4 pv = ld4(V + r * v_rel_stride + vi * D + sub * 4);
+        v += w * pv;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = sigmoidf_(v[j]);
+    st4(out + e * D + sub * 4, v);
+}
+
+// ---------------------------------------------------------------------------
+// DistMult + Keras BCE + backward seed.  256-thread blocks, grid-stride over rows;
+// per-lane-group register partials for drel and loss, block-ordered reduction.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const float* __restrict__ Xh,
+                                                       const int* __restrict__ h_idx, const float* __restrict__ Xt,
+                                                       const int* __restrict__ t_idx, const int* __restrict__ r_idx,
+                                                       const float* __restrict__ rel, const float* __restrict__ y,
+                                                       float scale, float* __restrict__ p_out,
+                                                       float* __restrict__ ds_out, float* __restrict__ do_out,
+                                                       float* __restrict__ drel_slab, float* __restrict__ loss_slab) {
+    constexpr int LPR = D / 4;
+    constexpr int GROUPS = 256 / LPR;  // row groups per block
+    __shared__ __attribute__((aligned(16))) float red[GROUPS * MAX_R * D];
+    __shared__ float lred[GROUPS];
+    const int grp = threadIdx.x / LPR;
+    const int sub = threadIdx.x % LPR;
+    const bool train = (y != nullptr);
+    f32x4 dr[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) dr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float lacc = 0.f;
+
+    for (long long e = (long long)blockIdx.x * GROUPS + grp; e < T; e += (long long)gridDim.x * GROUPS) {
+        const int hr = h_idx[e];
+        const int rr = r_idx[e];
+        const long long ti = t_idx ? (long long)t_idx[e] : e;
+        const f32x4 a = ld4(Xh + (long long)hr * D + sub * 4);
+        const f32x4 b = ld4(Xt + ti * D + sub * 4);
+        const f32x4 rho = ld4(rel + (long long)rr * D + sub * 4);
+        const f32x4 prod = a * rho * b;
+        const float s = group_sum<LPR>(prod[0] + prod[1] + prod[2] + prod[3]);
+        const float p = sigmoidf_(s);
+        if (p_out && sub == 0) p_out[e] = p;
+        if (!train) continue;
+        const float yy = y[e];
+        const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
+        const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
+        const float g = pass ? scale * (-(yy / (pc + EPS_BCE)) + (1.0f - yy) / (1.0f - pc + EPS_BCE)) : 0.f;
+        const float ds = g * p * (1.0f - p);
+        if (sub == 0) {
+            ds_out[e] = ds;
+            lacc += -(yy * logf(pc + EPS_BCE) + (1.0f - yy) * logf(1.0f - pc + EPS_BCE));
+        }
+        f32x4 dx = (ds * rho) * a;
+        dx = dx * (b * (1.0f - b));
+        st4(do_out + e * D + sub * 4, dx);
+        const f32x4 dre = ds * (a * b);
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+            if (r == rr) dr[r] += dre;
+    }
+    if (!train) return;
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) st4(red + (grp * MAX_R + r) * D + sub * 4, dr[r]);
+    if (sub == 0) lred[grp] = lacc;
+    __syncthreads();
+    for (int x = threadIdx.x; x < R * D; x += 256) {
+        const int r = x / D, c = x % D;
+        float s = 0.f;
+        for (int gq = 0; gq < GROUPS; ++gq) s += red[(gq * MAX_R + r) * D + c];
+        drel_slab[(long long)blockIdx.x * R * D + x] = s;
+    }
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int gq = 0; gq < GROUPS; ++gq) s += lred[gq];
+        loss_slab[blockIdx.x] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// segmented gather-reduce (head side): out[n] = dsig * sum coef[e] rel[r_e] rows[e]
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void seg_gather_reduce_kernel(int n_nodes, const int* __restrict__ seg_ptr,
+                                                                const int* __restrict__ perm,
+                                                                const float* __restrict__ coef,
+                                                                const int* __restrict__ r_idx,
+                                                                const float* __restrict__ rel,
+                                                                const float* __restrict__ rows,
+                                                                const float* __restrict__ X, float* __restrict__ out) {
+    constexpr int LPR = D / 4;
+    const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
+    if (n >= n_nodes) return;
+    const int beg = seg_ptr[n], end = seg_ptr[n + 1];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = beg; k < end; ++k) {
+        const long long e = perm ? (long long)perm[k] : (long long)k;
+        f32x4 v = ld4(rows + e * D + sub * 4);
+        if (coef) v *= coef[e];
+        if (rel) v *= ld4(rel + (long long)r_idx[e] * D + sub * 4);
+        acc += v;
+    }
+    if (X) {
+        const f32x4 x = ld4(X + n * D + sub * 4);
+        acc = acc * (x * (1.0f - x));
+    }
+    st4(out + n * D + sub * 4, acc);
+}
+
+// ---------------------------------------------------------------------------
+// tail-side layer backward over tail-sorted contiguous segments
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, int R, const int* __restrict__ seg_ptr,
+                                                              const int* __restrict__ h_idx,
+                                                              const float* __restrict__ W,
+                                                              const float* __restrict__ dO,
+                                                              const float* __restrict__ P, long long p_rel_stride,
+                                                              float* __restrict__ dP, long long dp_rel_stride,
+                                                              float* __restrict__ dsum, float* __restrict__ dWedge) {
+    constexpr int LPR = D / 4;
+    const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
+    const bool live = n < n_nodes;
+    const int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
+    f32x4 pr[MAX_R], acc[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) {
+        acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        pr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (live && r < R) pr[r] = ld4(P + r * p_rel_stride + n * D + sub * 4);
+    }
+    f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+    // every lane of a group iterates the same segment; groups of one wave may differ,
+    // so the shuffles below run under a wave-uniform trip count.
+    int len = end - beg;
+    int maxlen = len;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, m, 64));
+    for (int k = 0; k < maxlen; ++k) {
+        const bool act = k < len;
+        const long long e = (long long)beg + k;
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+        int hh = 0;
+        if (act) {
+            d = ld4(dO + e * D + sub * 4);
+            hh = h_idx[e];
+        }
+        s4 += d;
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r) {
+            if (r < R) {
+                const float w = act ? W[(long long)hh * R + r] : 0.f;
+                acc[r] += w * d;
+                const f32x4 q = d * pr[r];
+                const float dw = group_sum<LPR>(q[0] + q[1] + q[2] + q[3]);
+                if (act && sub == 0) dWedge[e * R + r] = dw;
+            }
+        }
+    }
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) st4(dP + r * dp_rel_stride + n * D + sub * 4, acc[r]);
+    if (dsum) st4(dsum + n * D + sub * 4, s4);
+}
+
+// ---------------------------------------------------------------------------
+// head-chain node backward (one layer)
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, const float* __restrict__ dO,
+                                                            const float* __restrict__ P, long long p_rel_stride,
+                                                            const float* __restrict__ Ssm,
+                                                            const float* __restrict__ W,
+                                                            const int* __restrict__ hseg_ptr,
+                                                            const int* __restrict__ hperm,
+                                                            const float* __restrict__ dWedge,
+                                                            float* __restrict__ dP, long long dp_rel_stride,
+                                                            float* __restrict__ dsum, float* __restrict__ dz) {
+    constexpr int LPR = D / 4;
+    const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
+    const bool live = n < n_nodes;
+    f32x4 d = {0.f, 0.f, 0.f, 0.f};
+    if (live) d = ld4(dO + n * D + sub * 4);
+    if (live && dsum) {
+        float* sp = dsum + n * D + sub * 4;
+        st4(sp, ld4(sp) + d);
+    }
+    const int beg = (live && hseg_ptr) ? hseg_ptr[n] : 0;
+    const int end = (live && hseg_ptr) ? hseg_ptr[n + 1] : 0;
+    float dw[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) {
+        float part = 0.f;
+        if (r < R) {
+            if (live) {
+                const f32x4 q = d * ld4(P + r * p_rel_stride + n * D + sub * 4);
+                part = q[0] + q[1] + q[2] + q[3];
+            }
+            // edge contributions: lane sub takes k = beg+sub, beg+sub+LPR, ...
+            float ep = 0.f;
+            for (int k = beg + sub; k < end; k += LPR) ep += dWedge[(long long)hperm[k] * R + r];
+            part += ep;
+        }
+        dw[r] = group_sum<LPR>(part);
+    }
+    if (!live) return;
+    float s[MAX_R], w[MAX_R], dsv[MAX_R];
+    float dot = 0.f;
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) {
+            s[r] = Ssm[n * R + r];
+            w[r] = W[n * R + r];
+            dsv[r] = dw[r] * w[r] * (1.0f - w[r]);
+            dot += dsv[r] * s[r];
+        }
+    if (sub == 0) {
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+            if (r < R) dz[n * R + r] = (dsv[r] - dot) * s[r];
+    }
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) {
+            float* pp = dP + r * dp_rel_stride + n * D + sub * 4;
+            st4(pp, ld4(pp) + w[r] * d);
+        }
+}
+
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(int n_slabs, long long n, const float* __restrict__ slab,
+                                                           float* __restrict__ out, int accumulate, float scale) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int b = 0; b < n_slabs; ++b) s += slab[(long long)b * n + i];
+    s *= scale;
+    out[i] = accumulate ? out[i] + s : s;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(long long n, float* __restrict__ var, float* __restrict__ m,
+                                                   float* __restrict__ v, const float* __restrict__ g, float alpha,
+                                                   float b1, float b2, float eps, int sparse_form) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float gi = g[i];
+    float mi = m[i], vi = v[i];
+    if (sparse_form) {
+        mi = mi * b1 + gi * (1.0f - b1);
+        vi = vi * b2 + (gi * gi) * (1.0f - b2);
+    } else {
+        mi = mi + (gi - mi) * (1.0f - b1);
+        vi = vi + (gi * gi - vi) * (1.0f - b2);
+    }
+    m[i] = mi;
+    v[i] = vi;
+    var[i] = var[i] - (mi * alpha) / (sqrtf(vi) + eps);
+}
+
+inline unsigned grid_for(long long rows, int lpr) {
+    const long long threads = rows * lpr;
+    return (unsigned)((threads + 255) / 256);
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int iddgcn_abi_version(void) { return IDDGCN_ABI_VERSION; }
+
+int iddgcn_spmm_csr_f32(void* stream, int n_seg, int n_rows, int d, const int* row_ptr, const int* col,
+                        const float* vals, const float* X, float* Y, int accumulate) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (n_seg < 0 || n_rows < 0 || !row_ptr || !X || !Y) return IDDGCN_E_BAD_ARG;
+    const long long rows = (long long)n_seg * n_rows;
+    if (rows == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = grid_for(rows, d / 4);
+#define SPMM(DD) hipLaunchKernelGGL(spmm_csr_kernel<DD>, dim3(grid), dim3(256), 0, st, n_seg, n_rows, row_ptr, col, vals, X, Y, accumulate)
+    switch (d) {
+        case 32: SPMM(32); break;
+        case 64: SPMM(64); break;
+        case 128: SPMM(128); break;
+        default: SPMM(256); break;
+    }
+#undef SPMM
+    return launch_status();
+}
+
+int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
+    if (!a) return IDDGCN_E_BAD_ARG;
+    if (!dim_ok(a->D)) return IDDGCN_E_BAD_DIM;
+    if (a->R < 0 || a->R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (a->M < 0 || !a->A || !a->B || !a->C) return IDDGCN_E_BAD_ARG;
+    if (a->R > 0 && (!a->coef || !a->V)) return IDDGCN_E_BAD_ARG;
+    if (a->act == IDDGCN_ACT_DSIGMOID && !a->aux) return IDDGCN_E_BAD_ARG;
+    if (a->M == 0) return 0;
+    RowGemmP p;
+    p.M = a->M; p.A = a->A; p.a_idx = a->a_idx; p.B = a->B; p.b_trans = a->b_trans;
+    p.C = a->C; p.accumulate = a->accumulate; p.R = a->R; p.coef = a->coef; p.coef_idx = a->coef_idx;
+    p.V = a->V; p.v_idx = a->v_idx; p.v_rel_stride = a->v_rel_stride; p.v_row_stride = a->v_row_stride;
+    p.act = a->act; p.aux = a->aux;
+    hipStream_t st = (hipStream_t)stream;
+#define RGEMM(DD, MAXB)                                                                         \
+    {                                                                                           \
+        const long long nt = ((long long)p.M + RG<DD>::TR - 1) / RG<DD>::TR;                    \
+        long long nb = nt < (MAXB) ? nt : (MAXB);                                               \
+        p.tiles_per_block = (int)((nt + nb - 1) / nb);                                          \
+        nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;                                  \
+        hipLaunchKernelGGL(rowgemm_kernel<DD>, dim3((unsigned)nb), dim3(RG<DD>::NW * 64), 0, st, p); \
+    }
+    switch (a->D) {
+        case 32: RGEMM(32, 2048); break;
+        case 64: RGEMM(64, 2048); break;
+        case 128: RGEMM(128, 1024); break;
+        default: RGEMM(256, 256); break;
+    }
+#undef RGEMM
+    return launch_status();
+}
+
+int iddgcn_gemm_tn_blocks(long long M, int d) {
+    const long long tiles = (M + 31) / 32;
+    const long long cap = (d >= 256) ? 256 : 1024;
+    long long nb = tiles < cap ? tiles : cap;
+    return (int)(nb < 1 ? 1 : nb);
+}
+
+int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const float* B, float* slab, int n_blocks,
+                       float* C, int accumulate) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (M < 0 || n_blocks < 1 || !A || !B || !slab || !C) return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    long long rpb = (M + n_blocks - 1) / n_blocks;
+    rpb = ((rpb + 31) / 32) * 32;
+    if (rpb < 32) rpb = 32;
+#define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
+    switch (d) {
+        case 32: TNK(32); break;
+        case 64: TNK(64); break;
+        case 128: TNK(128); break;
+        default: TNK(256); break;
+    }
+#undef TNK
+    int rc = launch_status();
+    if (rc) return rc;
+    const long long n = (long long)d * d;
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_blocks, n, slab, C,
+                       accumulate, 1.0f);
+    return launch_status();
+}
+
+int iddgcn_gemm_tn_narrow_blocks(long long M) {
+    long long nb = (M + 127) / 128;
+    if (nb > 1024) nb = 1024;
+    return (int)(nb < 1 ? 1 : nb);
+}
+
+int iddgcn_gemm_tn_narrow_f32(void* stream, long long M, int d, int R, const float* A, const float* dz, float* slab,
+                              int n_blocks, float* dWa, float* dba, int accumulate) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (M < 0 || n_blocks < 1 || !A || !dz || !slab || !dWa || !dba) return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const long long rpb = (M + n_blocks - 1) / n_blocks;
+#define NK(DD) hipLaunchKernelGGL(gemm_tn_narrow_kernel<DD>, dim3(n_blocks), dim3(DD), 0, st, M, rpb, R, A, dz, slab)
+    switch (d) {
+        case 32: NK(32); break;
+        case 64: NK(64); break;
+        case 128: NK(128); break;
+        default: NK(256); break;
+    }
+#undef NK
+    int rc = launch_status();
+    if (rc) return rc;
+    // slab rows are [(D+1)*R]; reduce the weight part and the bias part separately
+    const long long nw = (long long)d * R;
+    const long long stride = (long long)(d + 1) * R;
+    // reduce with stride: reuse reduce_slabs on a strided view by reducing the whole row then copying
+    // (n_blocks x (D+1)R is tiny), writing into dWa / dba through two launches.
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, st, n_blocks, stride,
+                       slab, slab + (long long)n_blocks * stride, 0, 1.0f);
+    rc = launch_status();
+    if (rc) return rc;
+    const float* red = slab + (long long)n_blocks * stride;
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, 1, nw, red, dWa,
+                       accumulate, 1.0f);
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(1), dim3(256), 0, st, 1, (long long)R, red + nw, dba, accumulate,
+                       1.0f);
+    return launch_status();
+}
+
+int iddgcn_alpha_fwd_f32(void* stream, int M, int d, int R, const float* X, const int* x_idx, const float* Wa,
+                         const float* ba, float* S_out, float* W_out) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (M < 0 || !X || !Wa || !ba || !S_out || !W_out) return IDDGCN_E_BAD_ARG;
+    if (M == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = grid_for(M, d / 4);
+#define AK(DD) hipLaunchKernelGGL(alpha_kernel<DD>, dim3(grid), dim3(256), 0, st, M, R, X, x_idx, Wa, ba, S_out, W_out)
+    switch (d) {
+        case 32: AK(32); break;
+        case 64: AK(64); break;
+        case 128: AK(128); break;
+        default: AK(256); break;
+    }
+#undef AK
+    return launch_status();
+}
+
+int iddgcn_combine_f32(void* stream, int M, int d, int R, const float* Y, const int* y_idx, const float* coef,
+                       const int* coef_idx, const float* V, const int* v_idx, long long v_rel_stride, float* out) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (R < 0 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (M < 0 || !Y || !out || (R > 0 && (!coef || !V))) return IDDGCN_E_BAD_ARG;
+    if (M == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = grid_for(M, d / 4);
+#define CK(DD) hipLaunchKernelGGL(combine_kernel<DD>, dim3(grid), dim3(256), 0, st, M, R, Y, y_idx, coef, coef_idx, V, v_idx, v_rel_stride, out)
+    switch (d) {
+        case 32: CK(32); break;
+        case 64: CK(64); break;
+        case 128: CK(128); break;
+        default: CK(256); break;
+    }
+#undef CK
+    return launch_status();
+}
+
+int iddgcn_distmult_blocks(long long T) {
+    long long nb = (T + 255) / 256;
+    if (nb > 2048) nb = 2048;
+    return (int)(nb < 1 ? 1 : nb);
+}
+
+int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R, const float* Xh, const int* h_idx,
+                            const float* Xt, const int* t_idx, const int* r_idx, const float* rel, const float* y,
+                            float scale, float* p_out, float* ds_out, float* do_out, float* drel_slab,
+                            float* loss_slab, int n_blocks) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (T < 0 || n_blocks < 1 || !Xh || !h_idx || !Xt || !r_idx || !rel) return IDDGCN_E_BAD_ARG;
+    if (y && (!ds_out || !do_out || !drel_slab || !loss_slab)) return IDDGCN_E_BAD_ARG;
+    if (T == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+#define DK(DD) hipLaunchKernelGGL(distmult_kernel<DD>, dim3(n_blocks), dim3(256), 0, st, T, R, Xh, h_idx, Xt, t_idx, r_idx, rel, y, scale, p_out, ds_out, do_out, drel_slab, loss_slab)
+    switch (d) {
+        case 32: DK(32); break;
+        case 64: DK(64); break;
+        case 128: DK(128); break;
+        default: DK(256); break;
+    }
+#undef DK
+    return launch_status();
+}
+
+int iddgcn_seg_gather_reduce_f32(void* stream, int n_nodes, int d, const int* seg_ptr, const int* perm,
+                                 const float* coef, const int* r_idx, const float* rel, const float* rows,
+                                 const float* X, float* out) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (n_nodes < 0 || !seg_ptr || !rows || !out || (rel && !r_idx)) return IDDGCN_E_BAD_ARG;
+    if (n_nodes == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = grid_for(n_nodes, d / 4);
+#define GK(DD) hipLaunchKernelGGL(seg_gather_reduce_kernel<DD>, dim3(grid), dim3(256), 0, st, n_nodes, seg_ptr, perm, coef, r_idx, rel, rows, X, out)
+    switch (d) {
+        case 32: GK(32); break;
+        case 64: GK(64); break;
+        case 128: GK(128); break;
+        default: GK(256); break;
+    }
+#undef GK
+    return launch_status();
+}
+
+int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* h_idx,
+                               const float* W, const float* dO, const float* P, long long p_rel_stride, float* dP,
+                               long long dp_rel_stride, float* dsum, float* dWedge) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (n_nodes < 0 || !seg_ptr || !h_idx || !W || !dO || !P || !dP || !dWedge) return IDDGCN_E_BAD_ARG;
+    if (n_nodes == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = grid_for(n_nodes, d / 4);
+#define TK(DD) hipLaunchKernelGGL(tail_seg_reduce_kernel<DD>, dim3(grid), dim3(256), 0, st, n_nodes, R, seg_ptr, h_idx, W, dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge)
+    switch (d) {
+        case 32: TK(32); break;
+        case 64: TK(64); break;
+        case 128: TK(128); break;
+        default: TK(256); break;
+    }
+#undef TK
+    return launch_status();
+}
+
+int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const float* dO, const float* P,
+                             long long p_rel_stride, const float* Ssm, const float* W, const int* hseg_ptr,
+                             const int* hperm, const float* dWedge, float* dP, long long dp_rel_stride, float* dsum,
+                             float* dz) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (n_nodes < 0 || !dO || !P || !Ssm || !W || !dP || !dz) return IDDGCN_E_BAD_ARG;
+    if (hseg_ptr && (!hperm || !dWedge)) return IDDGCN_E_BAD_ARG;
+    if (n_nodes == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = grid_for(n_nodes, d / 4);
+#define HK(DD) hipLaunchKernelGGL(head_bwd_node_kernel<DD>, dim3(grid), dim3(256), 0, st, n_nodes, R, dO, P, p_rel_stride, Ssm, W, hseg_ptr, hperm, dWedge, dP, dp_rel_stride, dsum, dz)
+    switch (d) {
+        case 32: HK(32); break;
+        case 64: HK(64); break;
+        case 128: HK(128); break;
+        default: HK(256); break;
+    }
+#undef HK
+    return launch_status();
+}
+
+int iddgcn_reduce_slabs_f32(void* stream, int n_slabs, long long n, const float* slab, float* out, int accumulate,
+                            float scale) {
+    if (n_slabs < 1 || n < 0 || !slab || !out) return IDDGCN_E_BAD_ARG;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       n_slabs, n, slab, out, accumulate, scale);
+    return launch_status();
+}
+
+int iddgcn_adam_f32(void* stream, long long n, float* var, float* m, float* v, const float* g, float alpha, float b1,
+                    float b2, float eps, int sparse_form) {
+    if (n < 0 || !var || !m || !v || !g) return IDDGCN_E_BAD_ARG;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, var, m, v,
+                       g, alpha, b1, b2, eps, sparse_form);
+    return launch_status();
+}
+
+}  // extern "C"

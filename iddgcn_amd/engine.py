@@ -1,0 +1,289 @@
+"""Step engine: the whole IDDGCN training / inference step as HIP launches.
+
+Formulation.  The reference evaluates every layer per
+scored edge (IDDGCN.py:60-79).  Three exact identities move most of it to the
+node level (N rows instead of T = B_pos + B_neg rows):
+
+  1. ``AE_r = A_r·E`` does not depend on the layer input (the layer is always
+     fed ``all_e``, IDDGCN.py:243/256/269) -> one SpMM per relation per step;
+  2. ``AE_r[idx]·K_r == (AE_r·K_r)[idx]`` -> ``P_r^l = AE_r·K_r^l`` per node;
+  3. the head chain ``x_h^l`` (and the dynamic weights ``w^l``, computed from
+     the head only, IDDGCN.py:66) depend on the head entity alone -> computed
+     once per node as ``X^l``.
+
+What stays per edge is the tail chain: layer 1 is a pure gather-combine of
+node tables, layers 2-3 need ``x_t^{l-1}·S^l`` (MFMA) fused with the gather of
+``P_r^l[t]`` scaled by ``w^l[h]`` and the sigmoid.  The backward mirrors this:
+edge-level MFMA GEMMs for ``dx·S^T`` and ``dS``, deterministic segmented
+reductions for every scatter, node-level MFMA GEMMs for the rest.
+
+Parameters live in ONE flat fp32 buffer (and so do their gradients), so Adam
+is two launches and data-parallel training needs one all-reduce per step.
+"""
+import contextlib
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import ops
+from .graph import DeviceAdjacency, ScoredEdges
+
+NUM_LAYERS = 3
+
+
+def param_layout(N, R, D):
+    """(name, shape, sparse_form) in flat-buffer order.  E and rel use the
+    Keras sparse-Adam form (their TF gradients are IndexedSlices)."""
+    lay = [("E", (N, D), True), ("rel", (R, D), True)]
+    for l in range(1, NUM_LAYERS + 1):
+        lay += [(f"K{l}", (R, D, D), False), (f"S{l}", (D, D), False),
+                (f"Wa{l}", (D, R), False), (f"ba{l}", (R,), False)]
+    return lay
+
+
+class FlatParams:
+    """A flat fp32 buffer with named views (parameters or their gradients)."""
+
+    def __init__(self, N, R, D, device):
+        self.N, self.R, self.D = N, R, D
+        self.layout = param_layout(N, R, D)
+        total = sum(int(np.prod(s)) for _, s, _ in self.layout)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=device)
+        self.views, off = {}, 0
+        self.n_sparse = 0
+        for name, shape, sparse in self.layout:
+            n = int(np.prod(shape))
+            self.views[name] = self.flat[off:off + n].view(shape)
+            if sparse:
+                self.n_sparse = off + n
+            off += n
+
+    def __getitem__(self, k):
+        return self.views[k]
+
+    def load(self, d):
+        for name, shape, _ in self.layout:
+            if name in d:
+                src = torch.as_tensor(np.asarray(d[name], dtype=np.float32).reshape(shape))
+                self.views[name].copy_(src)
+
+    def to_numpy(self):
+        return {k: v.detach().cpu().numpy().copy() for k, v in self.views.items()}
+
+
+class KerasAdam:
+    """Keras 2.7 Adam (lr=1e-3, b1=.9, b2=.999, eps=1e-7) over a FlatParams."""
+
+    def __init__(self, params, learning_rate=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+        self.lr, self.b1, self.b2, self.eps = learning_rate, beta_1, beta_2, epsilon
+        self.m = torch.zeros_like(params.flat)
+        self.v = torch.zeros_like(params.flat)
+        self.iterations = 0
+
+    def apply(self, params, grads):
+        self.iterations += 1
+        f = np.float32
+        t = f(self.iterations)
+        b1p, b2p = f(self.b1) ** t, f(self.b2) ** t          # computed in fp32 as TF does
+        alpha = f(self.lr) * np.sqrt(f(1) - b2p) / (f(1) - b1p)
+        ns = params.n_sparse
+        ops.adam(params.flat[:ns], self.m[:ns], self.v[:ns], grads.flat[:ns], alpha, self.b1, self.b2, self.eps, 1)
+        ops.adam(params.flat[ns:], self.m[ns:], self.v[ns:], grads.flat[ns:], alpha, self.b1, self.b2, self.eps, 0)
+
+
+class Workspace:
+    """Every device buffer one step needs, sized for (N, R, D, T)."""
+
+    def __init__(self, N, R, D, T, device, train=True):
+        f = dict(dtype=torch.float32, device=device)
+        e = lambda *s: torch.empty(*s, **f)  # noqa: E731
+        self.AE = e(R, N, D)
+        self.P = e(NUM_LAYERS, R, N, D)
+        self.ES1 = e(N, D)
+        self.X = e(NUM_LAYERS, N, D)            # head chain X^1..X^3
+        self.Ssm = e(NUM_LAYERS, N, R)
+        self.W = e(NUM_LAYERS, N, R)
+        self.xt = e(NUM_LAYERS, T, D)           # tail chain x^1..x^3
+        self.p = e(T)
+        self.nb_dm = ops.distmult_blocks(T)
+        self.train = train
+        if not train:
+            return
+        self.ds = e(T)
+        self.dE_a = e(T, D)                     # edge-level grads, ping-pong
+        self.dE_b = e(T, D)
+        self.dWedge = e(T, R)
+        self.dOn_a = e(N, D)                    # node-level grads, ping-pong
+        self.dOn_b = e(N, D)
+        self.dP = e(R, N, D)
+        self.dAE = e(R, N, D)
+        self.dES = e(N, D)
+        self.dz = e(N, R)
+        self.WaT = e(R, D)
+        self.drel_slab = e(self.nb_dm * R * D)
+        self.loss_slab = e(self.nb_dm)
+        self.loss = e(1)
+        tn = max(ops.tn_blocks(T, D), ops.tn_blocks(N, D))
+        self.tn_slab = e(tn * D * D)
+        self.narrow_slab = e((ops.tn_narrow_blocks(N) + 1) * (D + 1) * R)
+
+
+class Engine:
+    """Runs forward / backward / Adam for one (graph, scored-edge batch)."""
+
+    def __init__(self, num_entities, num_relations, dim, device=None):
+        if dim not in (32, 64, 128, 256):
+            raise L.IddgcnError("embedding dim must be one of 32, 64, 128, 256")
+        if not 1 <= num_relations <= 8:
+            raise L.IddgcnError("num_relations must be in [1, 8]")
+        self.N, self.R, self.D = num_entities, num_relations, dim
+        self.device = torch.device("cuda") if device is None else torch.device(device)
+        if self.device.type != "cuda":
+            raise L.IddgcnError("IDDGCN engine runs on the GPU only (no CPU fallback)")
+        L.lib()  # fail loudly now if the HIP library is missing
+        self._ws = {}
+        self.probe = None      # {name: [(start_event, end_event), ...]} when timing kernels
+
+    @contextlib.contextmanager
+    def _mark(self, name):
+        """Bracket one launch with HIP events on the current stream (bench.py roofline)."""
+        if self.probe is None:
+            yield
+            return
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        yield
+        b.record()
+        self.probe.setdefault(name, []).append((a, b))
+
+    # -- setup --------------------------------------------------------------
+    def adjacency(self, adj_mats):
+        return DeviceAdjacency(adj_mats, self.N, self.device)
+
+    def edges(self, triples, labels=None):
+        return ScoredEdges(triples, labels, self.N, self.R, self.device)
+
+    def workspace(self, T, train):
+        key = (T, train)
+        if key not in self._ws:
+            self._ws = {k: v for k, v in self._ws.items() if k[1] != train}  # keep one per mode
+            self._ws[key] = Workspace(self.N, self.R, self.D, T, self.device, train)
+        return self._ws[key]
+
+    # -- forward ------------------------------------------------------------
+    def forward(self, P, adj, ed, ws, train):
+        N, R, D, T = self.N, self.R, self.D, ed.T
+        E = P["E"]
+        # AE_r = A_r·E, all relations in one launch (IDDGCN.py:69-70)
+        ops.spmm_csr(adj.fwd_ptr, adj.fwd_col, adj.fwd_val, E, ws.AE, R, N)
+        # P_r^l = AE_r·K_r^l (node-level form of IDDGCN.py:71-72,76-77)
+        for l in range(NUM_LAYERS):
+            K = P[f"K{l + 1}"]
+            for r in range(R):
+                ops.rowgemm(ws.AE[r], K[r], ws.P[l, r])
+        # layer 1: x·S1 is node-level for both sides (inputs are E[h], E[t])
+        ops.rowgemm(E, P["S1"], ws.ES1)
+        ops.alpha_fwd(E, P["Wa1"], P["ba1"], ws.Ssm[0], ws.W[0])
+        ops.combine(ws.ES1, ws.W[0], ws.P[0], ws.X[0])
+        ops.combine(ws.ES1, ws.W[0], ws.P[0], ws.xt[0], y_idx=ed.t, coef_idx=ed.h, v_idx=ed.t)
+        # layers 2, 3
+        for l in (1, 2):
+            S = P[f"S{l + 1}"]
+            ops.alpha_fwd(ws.X[l - 1], P[f"Wa{l + 1}"], P[f"ba{l + 1}"], ws.Ssm[l], ws.W[l])
+            ops.rowgemm(ws.X[l - 1], S, ws.X[l], coef=ws.W[l], V=ws.P[l], v_rel_stride=N * D,
+                        act=L.ACT_SIGMOID)
+            with self._mark("tail_fwd_gemm"):
+                ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.W[l], coef_idx=ed.h, V=ws.P[l], v_idx=ed.t,
+                            v_rel_stride=N * D, act=L.ACT_SIGMOID)
+        # DistMult (+ BCE and backward seed when training)
+        if train:
+            scale = 1.0 / (float(self._t_global or T) * float(N))
+            ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], y=ed.y, scale=scale, p_out=ws.p,
+                             ds_out=ws.ds, do_out=ws.dE_a, drel_slab=ws.drel_slab, loss_slab=ws.loss_slab)
+        else:
+            ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], p_out=ws.p)
+
+    _t_global = None
+
+    # -- backward -----------------------------------------------------------
+    def backward(self, P, G, adj, ed, ws):
+        N, R, D = self.N, self.R, self.D
+        # head-side seed: dO^3[n] = X3(1-X3) * sum_{h_e=n} ds_e rel[r_e] * x3_e
+        dOn, dOn_next = ws.dOn_a, ws.dOn_b
+        ops.seg_gather_reduce(ed.hptr, ws.xt[2], dOn, perm=ed.hperm, coef=ws.ds, r_idx=ed.r, rel=P["rel"],
+                              X=ws.X[2])
+        do, do_next = ws.dE_a, ws.dE_b          # do^3 written by distmult
+        for l in (2, 1, 0):                     # layer index l -> reference layer l+1
+            Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
+            # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part
+            ops.tail_seg_reduce(ed.tptr, ed.h, Wl, do, Pl, ws.dP, ws.dWedge, dsum=ws.dES if l == 0 else None)
+            if l > 0:
+                # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x)
+                with self._mark("tail_dS_tn"):
+                    ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab)
+                with self._mark("tail_bwd_gemm"):
+                    ops.rowgemm(do, Sl, do_next, b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1])
+            # head side (node level)
+            ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
+                              dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)
+            Xin = ws.X[l - 1] if l > 0 else P["E"]
+            ws.WaT.copy_(P[f"Wa{l + 1}"].t())
+            ops.gemm_tn_narrow(Xin, ws.dz, G[f"Wa{l + 1}"], G[f"ba{l + 1}"], ws.narrow_slab)
+            if l > 0:
+                ops.gemm_tn(Xin, dOn, G[f"S{l + 1}"], ws.tn_slab, accumulate=True)
+                ops.rowgemm(dOn, Sl, dOn_next, b_trans=True, coef=ws.dz, V=ws.WaT, v_rel_stride=D,
+                            v_row_stride=0, act=L.ACT_DSIGMOID, aux=Xin)
+            else:
+                ops.gemm_tn(P["E"], ws.dES, G["S1"], ws.tn_slab)
+                # dE (head input of layer 1 + x·S1 inputs of both sides)
+                ops.rowgemm(ws.dES, Sl, G["E"], b_trans=True, coef=ws.dz, V=ws.WaT, v_rel_stride=D,
+                            v_row_stride=0)
+            # relation kernels: dK_r = AE_r^T dP_r ; dAE_r += dP_r K_r^T
+            K, dK = P[f"K{l + 1}"], G[f"K{l + 1}"]
+            for r in range(R):
+                ops.gemm_tn(ws.AE[r], ws.dP[r], dK[r], ws.tn_slab)
+                ops.rowgemm(ws.dP[r], K[r], ws.dAE[r], b_trans=True, accumulate=(l != 2))
+            dOn, dOn_next = dOn_next, dOn
+            do, do_next = do_next, do
+        # dE += sum_r A_r^T dAE_r  (gradient through all_e -> sparse_dense_matmul)
+        ops.spmm_csr(adj.bwd_ptr, adj.bwd_col, adj.bwd_val, ws.dAE.view(R * N, D), G["E"].view(1, N, D), 1, N,
+                     accumulate=True)
+        # DistMult rel grad and the loss
+        ops.reduce_slabs(ws.drel_slab, ws.nb_dm, G["rel"])
+        ops.reduce_slabs(ws.loss_slab, ws.nb_dm, ws.loss)
+
+    # -- public steps ---------------------------------------------------------
+    def train_step(self, params, grads, opt, adj, ed, t_global=None, allreduce=None):
+        """One full-batch step (IDDGCN.py:123-178).  Returns the device scalar
+        sum of per-edge BCE terms of this rank (divide by T for the mean)."""
+        ws = self.workspace(ed.T, True)
+        self._t_global = t_global
+        self.forward(params, adj, ed, ws, True)
+        self.backward(params, grads, adj, ed, ws)
+        if allreduce is not None:
+            allreduce(grads.flat, ws.loss)
+        opt.apply(params, grads)
+        return ws.loss
+
+    def predict(self, params, adj, ed):
+        ws = self.workspace(ed.T, False)
+        self.forward(params, adj, ed, ws, False)
+        return ed.unsort(ws.p)
+
+    def loss_and_grads(self, params, grads, adj, ed, t_global=None):
+        ws = self.workspace(ed.T, True)
+        self._t_global = t_global
+        self.forward(params, adj, ed, ws, True)
+        self.backward(params, grads, adj, ed, ws)
+        return ws.loss, ed.unsort(ws.p)
+
+
+def step_flops(N, R, D, T, M):
+    """Algorithmic work of one training step (W_gemm)."""
+    return 12 * D * D * T + 18 * (R + 1) * N * D * D + 4 * M * D
+
+
+def step_bytes(N, R, D, T, M, L=NUM_LAYERS):
+    """Algorithmic HBM bytes of one training step (Q_hbm, fp32)."""
+    return 40 * T * D + 8 * L * R * T * D + 24 * T + 16 * M + 16 * L * (R + 1) * N * D

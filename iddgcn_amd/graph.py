@@ -1,0 +1,163 @@
+"""Host-side graph build: per-relation adjacency and scored-edge layouts.
+
+* ``get_adj_mats`` mirrors ``utils1.get_adj_mats`` (utils1.py:420-451): per
+  relation, the sorted unique (obj, sbj) pairs with value 1.0, or the single
+  placeholder (0,0)=0.0 for an empty relation, shaped (1, N, N) like the
+  reference's reshaped ``tf.SparseTensor``.  The edge order is row-major
+  sorted — exactly the order ``np.unique`` + ``tf.sparse.reorder`` produce —
+  and it is the CSR order the SpMM kernel sums in.
+* ``DeviceAdjacency`` holds, on the GPU, the batched CSR of every A_r (forward
+  ``A_r·E``) and the batched CSR of every A_r^T (backward ``A_r^T·dAE_r``).
+* ``ScoredEdges`` lays the scored triples (positives ++ negatives) out in HBM
+  sorted by tail, so the tail-side gathers/scatters of every layer walk
+  contiguous segments, and adds a head-sorted permutation for the head-side
+  reductions.  All indices are validated here (int32, in range) so no kernel
+  ever sees an out-of-range index.
+"""
+import numpy as np
+import torch
+
+from ._lib import IddgcnError
+
+INT32_MAX = 2 ** 31 - 1
+
+
+class SparseAdj:
+    """Host stand-in for the reference's (1, N, N) ``tf.SparseTensor``."""
+
+    def __init__(self, indices, values, num_entities):
+        self.indices = indices            # (nnz, 3) int64: [0, row, col]
+        self.values = values              # (nnz,) float32
+        self.dense_shape = (1, num_entities, num_entities)
+
+    @property
+    def rows(self):
+        return self.indices[:, 1]
+
+    @property
+    def cols(self):
+        return self.indices[:, 2]
+
+    @property
+    def nnz(self):
+        return int(self.values.shape[0])
+
+
+def _as_triples(data):
+    if isinstance(data, torch.Tensor):
+        data = data.cpu().numpy()
+    data = np.asarray(data)
+    if data.ndim == 3 and data.shape[0] == 1:
+        data = data[0]
+    if data.ndim != 2 or data.shape[1] != 3:
+        raise IddgcnError(f"triples must be (B, 3), got {data.shape}")
+    return data.astype(np.int64)
+
+
+def get_adj_mats(data, num_entities, num_relations):
+    """utils1.get_adj_mats (utils1.py:420-451) without TensorFlow."""
+    data = _as_triples(data)
+    if data.size and (data[:, [0, 2]].min() < 0 or data[:, [0, 2]].max() >= num_entities):
+        raise IddgcnError("entity index out of range [0, num_entities)")
+    mats = []
+    for r in range(num_relations):
+        sel = data[data[:, 1] == r]
+        if sel.shape[0] == 0:
+            rc = np.zeros((1, 2), dtype=np.int64)
+            val = np.zeros((1,), dtype=np.float32)
+        else:
+            # lexicographic (row, col) unique == np.unique(axis=0) == tf.sparse.reorder order
+            key = sel[:, 0] * np.int64(num_entities) + sel[:, 2]
+            key = np.unique(key)
+            rc = np.stack([key // num_entities, key % num_entities], 1)
+            val = np.ones((rc.shape[0],), dtype=np.float32)
+        idx = np.concatenate([np.zeros((rc.shape[0], 1), dtype=np.int64), rc], 1)
+        mats.append(SparseAdj(idx, val, num_entities))
+    return mats
+
+
+def _csr(rows, cols, n):
+    order = np.lexsort((cols, rows))
+    rows, cols = rows[order], cols[order]
+    ptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(ptr, rows + 1, 1)
+    return np.cumsum(ptr), cols, order
+
+
+class DeviceAdjacency:
+    """Batched CSR of every A_r (forward) and one merged CSR of all A_r^T (backward)."""
+
+    def __init__(self, adj_mats, num_entities, device):
+        N = num_entities
+        self.num_entities = N
+        self.num_relations = len(adj_mats)
+        fptr, fcol, fval = [], [], []
+        bc, bm, bv = [], [], []
+        off_f = 0
+        any_val = False
+        self.nnz = []
+        for r, a in enumerate(adj_mats):
+            rows = np.asarray(a.rows, dtype=np.int64)
+            cols = np.asarray(a.cols, dtype=np.int64)
+            vals = np.asarray(a.values, dtype=np.float32)
+            if rows.size and (rows.min() < 0 or rows.max() >= N or cols.min() < 0 or cols.max() >= N):
+                raise IddgcnError("adjacency index out of range")
+            any_val |= bool(np.any(vals != 1.0))
+            p, c, o = _csr(rows, cols, N)
+            fptr.append(p + off_f)
+            fcol.append(c)
+            fval.append(vals[o])
+            off_f += c.size
+            bc.append(cols)
+            bm.append(rows + r * N)
+            bv.append(vals)
+            self.nnz.append(int(rows.size))
+        if off_f > INT32_MAX or N * len(adj_mats) > INT32_MAX:
+            raise IddgcnError("adjacency too large for int32 offsets")
+        # Backward: dE[c] += sum_r sum_{m: (m,c) in A_r} dAE[r][m].  One merged CSR of
+        # [A_0^T | A_1^T | ...] over N rows whose column ids index the concatenated
+        # dAE (R*N rows); inside a row entries run relation-major, then by m.
+        bc, bm, bv = np.concatenate(bc), np.concatenate(bm), np.concatenate(bv)
+        bptr, bcol, border = _csr(bc, bm, N)
+        t = lambda x, dt: torch.as_tensor(np.ascontiguousarray(x).astype(dt), device=device)  # noqa: E731
+        self.fwd_ptr, self.fwd_col = t(np.concatenate(fptr), np.int32), t(np.concatenate(fcol), np.int32)
+        self.bwd_ptr, self.bwd_col = t(bptr, np.int32), t(bcol, np.int32)
+        # values are all 1.0 unless a placeholder (0,0)=0 exists: pass them only then
+        self.fwd_val = t(np.concatenate(fval), np.float32) if any_val else None
+        self.bwd_val = t(bv[border], np.float32) if any_val else None
+        self.total_nnz = off_f
+
+
+class ScoredEdges:
+    """Scored triples (B, 3) laid out tail-sorted on the GPU.
+
+    ``order[k]`` is the caller's row index of sorted position k; predictions
+    are returned in the caller's order.
+    """
+
+    def __init__(self, triples, labels, num_entities, num_relations, device):
+        tr = _as_triples(triples)
+        T = tr.shape[0]
+        if T > INT32_MAX:
+            raise IddgcnError("too many scored edges for int32 indexing")
+        h, r, t = tr[:, 0], tr[:, 1], tr[:, 2]
+        if T and (min(h.min(), t.min()) < 0 or max(h.max(), t.max()) >= num_entities):
+            raise IddgcnError("scored entity index out of range [0, num_entities)")
+        if T and (r.min() < 0 or r.max() >= num_relations):
+            raise IddgcnError("scored relation index out of range [0, num_relations)")
+        order = np.argsort(t, kind="stable")
+        self.order = order
+        hs, rs, ts = h[order], r[order], t[order]
+        tptr = np.searchsorted(ts, np.arange(num_entities + 1), side="left")
+        hperm = np.argsort(hs, kind="stable")
+        hptr = np.searchsorted(hs[hperm], np.arange(num_entities + 1), side="left")
+        g = lambda x, dt: torch.as_tensor(np.ascontiguousarray(x).astype(dt), device=device)  # noqa: E731
+        self.T = T
+        self.h, self.r, self.t = g(hs, np.int32), g(rs, np.int32), g(ts, np.int32)
+        self.tptr, self.hperm, self.hptr = g(tptr, np.int32), g(hperm, np.int32), g(hptr, np.int32)
+        self.y = None if labels is None else g(np.asarray(labels, dtype=np.float32)[order], np.float32)
+        self.inv = g(np.argsort(order, kind="stable"), np.int64)
+
+    def unsort(self, x):
+        """Sorted-order per-edge tensor -> caller's order."""
+        return x[self.inv]

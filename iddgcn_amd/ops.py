@@ -1,0 +1,215 @@
+"""Thin torch-facing wrappers over the C-ABI (one call = one library entry point).
+
+torch is used only as the device-memory / stream provider: every wrapper takes
+CUDA(HIP) tensors, validates shapes/dtypes on the host (so a bad shape never
+reaches a kernel), and passes raw pointers plus torch's current stream.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+_F32 = torch.float32
+_I32 = torch.int32
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _req(t, dtype, shape=None, name="tensor"):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise L.IddgcnError(f"{name} must be a GPU tensor (no CPU fallback)")
+    if t.dtype != dtype:
+        raise L.IddgcnError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise L.IddgcnError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise L.IddgcnError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+
+
+def _idx_ok(idx, n_rows, bound, name):
+    if idx is None:
+        return
+    _req(idx, _I32, (n_rows,), name)
+
+
+def spmm_csr(row_ptr, col, vals, X, Y, n_seg, n_rows, accumulate=False):
+    D = X.shape[1]
+    _req(row_ptr, _I32, (n_seg * (n_rows + 1),), "row_ptr")
+    _req(col, _I32, None, "col")
+    _req(vals, _F32, None, "vals")
+    _req(X, _F32, None, "X")
+    _req(Y, _F32, (n_seg, n_rows, D), "Y")
+    L.check(L.lib().iddgcn_spmm_csr_f32(_stream(), n_seg, n_rows, D, _ptr(row_ptr), _ptr(col), _ptr(vals),
+                                        _ptr(X), _ptr(Y), int(accumulate)), "spmm_csr")
+
+
+def rowgemm(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, coef_idx=None, V=None,
+            v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None):
+    D = B.shape[0]
+    M = C.shape[0] if M is None else M
+    R = 0 if coef is None else coef.shape[-1]
+    _req(A, _F32, None, "A")
+    _req(B, _F32, (D, D), "B")
+    _req(C, _F32, (M, D), "C")
+    if A.dim() != 2 or A.shape[1] != D:
+        raise L.IddgcnError(f"A must be (rows, {D})")
+    if a_idx is None and A.shape[0] < M:
+        raise L.IddgcnError("A has fewer rows than C")
+    _idx_ok(a_idx, M, A.shape[0], "a_idx")
+    if R:
+        _req(coef, _F32, None, "coef")
+        _req(V, _F32, None, "V")
+        _idx_ok(coef_idx, M, coef.shape[0], "coef_idx")
+        _idx_ok(v_idx, M, None, "v_idx")
+    if act == L.ACT_DSIGMOID:
+        _req(aux, _F32, (M, D), "aux")
+    args = L.RowGemmArgs(
+        M=M, D=D, A=_ptr(A), a_idx=_ptr(a_idx), B=_ptr(B), b_trans=int(b_trans), C=_ptr(C),
+        accumulate=int(accumulate), R=R, coef=_ptr(coef), coef_idx=_ptr(coef_idx), V=_ptr(V),
+        v_idx=_ptr(v_idx), v_rel_stride=int(v_rel_stride),
+        v_row_stride=int(D if v_row_stride is None else v_row_stride), act=int(act), aux=_ptr(aux))
+    L.check(L.lib().iddgcn_rowgemm_f32(_stream(), ctypes.byref(args)), "rowgemm")
+
+
+def tn_blocks(M, D):
+    return int(L.lib().iddgcn_gemm_tn_blocks(int(M), int(D)))
+
+
+def gemm_tn(A, B, C, slab, accumulate=False):
+    M, D = A.shape
+    _req(A, _F32, (M, D), "A")
+    _req(B, _F32, (M, D), "B")
+    _req(C, _F32, (D, D), "C")
+    nb = tn_blocks(M, D)
+    if slab.numel() < nb * D * D:
+        raise L.IddgcnError("gemm_tn slab too small")
+    L.check(L.lib().iddgcn_gemm_tn_f32(_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C),
+                                       int(accumulate)), "gemm_tn")
+
+
+def tn_narrow_blocks(M):
+    return int(L.lib().iddgcn_gemm_tn_narrow_blocks(int(M)))
+
+
+def gemm_tn_narrow(A, dz, dWa, dba, slab, accumulate=False):
+    M, D = A.shape
+    R = dz.shape[1]
+    _req(dz, _F32, (M, R), "dz")
+    _req(dWa, _F32, (D, R), "dWa")
+    _req(dba, _F32, (R,), "dba")
+    nb = tn_narrow_blocks(M)
+    if slab.numel() < (nb + 1) * (D + 1) * R:
+        raise L.IddgcnError("gemm_tn_narrow slab too small")
+    L.check(L.lib().iddgcn_gemm_tn_narrow_f32(_stream(), M, D, R, _ptr(A), _ptr(dz), _ptr(slab), nb, _ptr(dWa),
+                                              _ptr(dba), int(accumulate)), "gemm_tn_narrow")
+
+
+def alpha_fwd(X, Wa, ba, S_out, W_out, x_idx=None, M=None):
+    D, R = Wa.shape
+    M = S_out.shape[0] if M is None else M
+    _req(X, _F32, None, "X")
+    _req(Wa, _F32, (D, R), "W_alpha")
+    _req(ba, _F32, (R,), "b_alpha")
+    _req(S_out, _F32, (M, R), "S_out")
+    _req(W_out, _F32, (M, R), "W_out")
+    _idx_ok(x_idx, M, X.shape[0], "x_idx")
+    L.check(L.lib().iddgcn_alpha_fwd_f32(_stream(), M, D, R, _ptr(X), _ptr(x_idx), _ptr(Wa), _ptr(ba),
+                                         _ptr(S_out), _ptr(W_out)), "alpha_fwd")
+
+
+def combine(Y, coef, V, out, *, y_idx=None, coef_idx=None, v_idx=None, v_rel_stride=None):
+    M, D = out.shape
+    R = coef.shape[-1]
+    _req(Y, _F32, None, "Y")
+    _req(coef, _F32, None, "coef")
+    _req(V, _F32, None, "V")
+    _req(out, _F32, (M, D), "out")
+    for n, ix in (("y_idx", y_idx), ("coef_idx", coef_idx), ("v_idx", v_idx)):
+        _idx_ok(ix, M, None, n)
+    vrs = V.shape[1] * D if v_rel_stride is None else v_rel_stride
+    L.check(L.lib().iddgcn_combine_f32(_stream(), M, D, R, _ptr(Y), _ptr(y_idx), _ptr(coef), _ptr(coef_idx),
+                                       _ptr(V), _ptr(v_idx), int(vrs), _ptr(out)), "combine")
+
+
+def distmult_blocks(T):
+    return int(L.lib().iddgcn_distmult_blocks(int(T)))
+
+
+def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_out=None, ds_out=None,
+                 do_out=None, drel_slab=None, loss_slab=None):
+    T = h_idx.shape[0]
+    R, D = rel.shape
+    _req(h_idx, _I32, (T,), "h_idx")
+    _req(r_idx, _I32, (T,), "r_idx")
+    _req(Xh, _F32, None, "Xh")
+    _req(Xt, _F32, None, "Xt")
+    _req(rel, _F32, (R, D), "rel")
+    _req(y, _F32, (T,), "y")
+    _req(p_out, _F32, (T,), "p_out")
+    nb = distmult_blocks(T)
+    if y is not None:
+        _req(ds_out, _F32, (T,), "ds_out")
+        _req(do_out, _F32, (T, D), "do_out")
+        if drel_slab.numel() < nb * R * D or loss_slab.numel() < nb:
+            raise L.IddgcnError("distmult slabs too small")
+    L.check(L.lib().iddgcn_distmult_bce_f32(_stream(), T, D, R, _ptr(Xh), _ptr(h_idx), _ptr(Xt), _ptr(t_idx),
+                                            _ptr(r_idx), _ptr(rel), _ptr(y), float(scale), _ptr(p_out),
+                                            _ptr(ds_out), _ptr(do_out), _ptr(drel_slab), _ptr(loss_slab), nb),
+            "distmult_bce")
+    return nb
+
+
+def seg_gather_reduce(seg_ptr, rows, out, *, perm=None, coef=None, r_idx=None, rel=None, X=None):
+    n_nodes, D = out.shape
+    _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")
+    _req(out, _F32, (n_nodes, D), "out")
+    L.check(L.lib().iddgcn_seg_gather_reduce_f32(_stream(), n_nodes, D, _ptr(seg_ptr), _ptr(perm), _ptr(coef),
+                                                 _ptr(r_idx), _ptr(rel), _ptr(rows), _ptr(X), _ptr(out)),
+            "seg_gather_reduce")
+
+
+def tail_seg_reduce(seg_ptr, h_idx, W, dO, P, dP, dWedge, dsum=None):
+    R, n_nodes, D = P.shape
+    _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")
+    _req(P, _F32, (R, n_nodes, D), "P")
+    _req(dP, _F32, (R, n_nodes, D), "dP")
+    _req(dsum, _F32, (n_nodes, D), "dsum")
+    L.check(L.lib().iddgcn_tail_seg_reduce_f32(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(h_idx), _ptr(W),
+                                               _ptr(dO), _ptr(P), n_nodes * D, _ptr(dP), n_nodes * D, _ptr(dsum),
+                                               _ptr(dWedge)), "tail_seg_reduce")
+
+
+def head_bwd_node(dO, P, Ssm, W, dP, dz, *, hseg_ptr=None, hperm=None, dWedge=None, dsum=None):
+    R, n_nodes, D = P.shape
+    _req(dO, _F32, (n_nodes, D), "dO")
+    _req(Ssm, _F32, (n_nodes, R), "Ssm")
+    _req(W, _F32, (n_nodes, R), "W")
+    _req(dz, _F32, (n_nodes, R), "dz")
+    _req(dsum, _F32, (n_nodes, D), "dsum")
+    L.check(L.lib().iddgcn_head_bwd_node_f32(_stream(), n_nodes, D, R, _ptr(dO), _ptr(P), n_nodes * D, _ptr(Ssm),
+                                             _ptr(W), _ptr(hseg_ptr), _ptr(hperm), _ptr(dWedge), _ptr(dP),
+                                             n_nodes * D, _ptr(dsum), _ptr(dz)), "head_bwd_node")
+
+
+def reduce_slabs(slab, n_slabs, out, accumulate=False, scale=1.0):
+    n = out.numel()
+    L.check(L.lib().iddgcn_reduce_slabs_f32(_stream(), n_slabs, n, _ptr(slab), _ptr(out), int(accumulate),
+                                            float(scale)), "reduce_slabs")
+
+
+def adam(var, m, v, g, alpha, b1, b2, eps, sparse_form):
+    n = var.numel()
+    for t, nm in ((m, "m"), (v, "v"), (g, "g")):
+        if t.numel() != n:
+            raise L.IddgcnError(f"adam: {nm} size mismatch")
+    L.check(L.lib().iddgcn_adam_f32(_stream(), n, _ptr(var), _ptr(m), _ptr(v), _ptr(g), float(alpha), float(b1),
+                                    float(b2), float(eps), int(sparse_form)), "adam")

@@ -1,0 +1,159 @@
+/*
+ * iddgcn.h — C-ABI of libiddgcn_hip.so, the MI355X (gfx950) hot path of
+ * IDDGCN's directed multi-relational graph convolution (forward + backward).
+ *
+ * The reference (AhauBioinformatics/IDDGCN) is pure Python on TensorFlow 2.7;
+ * it has no FFI.  Each entry point below replaces the TF ops that one Keras
+ * call site lowers to (file:line in /root/reference/prediction/IDDGCN.py or
+ * utils1.py); the Python host layer (iddgcn_amd/) binds them with ctypes and
+ * keeps the Keras-shaped surface (IDDGCN_Layer, DistMult, get_IDDGCN_Model,
+ * fit/predict) — see INTEGRATION.md.
+ *
+ * Conventions (all entry points):
+ *   - pointers are DEVICE pointers to contiguous row-major fp32 (indices int32);
+ *   - the caller allocates every output and workspace; the library never
+ *     allocates or frees device memory and never synchronises the stream;
+ *   - `stream` is a hipStream_t passed as void*; NULL = default stream;
+ *   - return 0 on success, a positive hipError_t on a launch error, or a
+ *     negative IDDGCN_E* code on invalid arguments (nothing is launched then);
+ *   - feature width D must be one of 32, 64, 128, 256; relations R <= 8.
+ */
+#ifndef IDDGCN_H_
+#define IDDGCN_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IDDGCN_ABI_VERSION 1
+
+#define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
+#define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
+#define IDDGCN_E_BAD_ARG   (-3)   /* null required pointer / negative size */
+
+/* activation applied by the row-GEMM epilogue */
+#define IDDGCN_ACT_NONE     0
+#define IDDGCN_ACT_SIGMOID  1
+#define IDDGCN_ACT_DSIGMOID 2     /* v *= aux * (1 - aux)   (sigmoid backward) */
+
+int iddgcn_abi_version(void);
+
+/* Y[s][n][:] = (accumulate ? Y[s][n][:] : 0) + sum_{k=ptr[s*(n_rows+1)+n]}^{..+1} (vals ? vals[k] : 1) * X[col[k]][:]
+ * for s in [0, n_seg).  One CSR per relation, row_ptr holds absolute offsets into col/vals.
+ * Replaces tf.sparse.sparse_dense_matmul (IDDGCN.py:69-70) and, fed the CSC (= CSR of A^T),
+ * its gradient w.r.t. the dense operand (TF SparseTensorDenseMatMul adjoint_a).  Per-row sums
+ * are sequential in CSR order, the order TF's CPU kernel walks the sorted COO. */
+int iddgcn_spmm_csr_f32(void* stream, int n_seg, int n_rows, int d,
+                        const int* row_ptr, const int* col, const float* vals,
+                        const float* X, float* Y, int accumulate);
+
+/* Row GEMM on f32 MFMA with a fused epilogue.  For e in [0, M), c in [0, D):
+ *   v  = sum_k A[a_idx ? a_idx[e] : e][k] * (b_trans ? B[c][k] : B[k][c])
+ *   v += accumulate ? C[e][c] : 0
+ *   v += sum_{r<R} coef[(coef_idx ? coef_idx[e] : e)*R + r]
+ *                  * V[r*v_rel_stride + (v_idx ? v_idx[e] : e)*v_row_stride + c]
+ *   C[e][c] = act(v)   (NONE | SIGMOID | DSIGMOID with aux[e][c])
+ * Replaces IDDGCN.py:62-63 + 71-79 (x·S, + sigmoid(alpha_r)·(AE_r[idx]·K_r), sigmoid)
+ * with P_r = AE_r·K_r precomputed at node level, and the matching backward GEMMs. */
+typedef struct {
+    int M, D;
+    const float* A; const int* a_idx;
+    const float* B; int b_trans;
+    float* C; int accumulate;
+    int R;
+    const float* coef; const int* coef_idx;
+    const float* V; const int* v_idx;
+    long long v_rel_stride, v_row_stride;
+    int act; const float* aux;
+} iddgcn_rowgemm_t;
+int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
+
+/* C[D][D] (+)= A^T · B over M rows (A, B are M x D).  Two stages: each of n_blocks
+ * workgroups writes a D x D partial into `slab` (n_blocks*D*D floats), then the
+ * partials are summed in block order (deterministic).  n_blocks from
+ * iddgcn_gemm_tn_blocks().  Weight gradients dS, dK_r (tape.gradient, IDDGCN.py:172). */
+int iddgcn_gemm_tn_blocks(long long M, int d);
+int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const float* B,
+                       float* slab, int n_blocks, float* C, int accumulate);
+
+/* out[D][R] (+)= A^T·dz and out_b[R] (+)= colsum(dz) over M rows (dW_alpha, db_alpha).
+ * slab holds (n_blocks+1)*(D+1)*R floats; n_blocks from iddgcn_gemm_tn_narrow_blocks(). */
+int iddgcn_gemm_tn_narrow_blocks(long long M);
+int iddgcn_gemm_tn_narrow_f32(void* stream, long long M, int d, int R, const float* A,
+                              const float* dz, float* slab, int n_blocks,
+                              float* dWa, float* dba, int accumulate);
+
+/* Dynamic relation weights (IDDGCN.py:66,75): z = X[x_idx? x_idx[n]:n]·Wa + ba,
+ * s = softmax(z), w = sigmoid(s).  Writes S_out[M][R] (softmax, kept for backward)
+ * and W_out[M][R]. */
+int iddgcn_alpha_fwd_f32(void* stream, int M, int d, int R, const float* X, const int* x_idx,
+                         const float* Wa, const float* ba, float* S_out, float* W_out);
+
+/* Gather-combine without GEMM (layer 1, x·S pre-projected at node level):
+ *   out[e][c] = sigmoid(Y[y_idx? y_idx[e]:e][c]
+ *                       + sum_r coef[(coef_idx? coef_idx[e]:e)*R+r] * V[r*v_rel_stride + (v_idx? v_idx[e]:e)*D + c]) */
+int iddgcn_combine_f32(void* stream, int M, int d, int R,
+                       const float* Y, const int* y_idx,
+                       const float* coef, const int* coef_idx,
+                       const float* V, const int* v_idx, long long v_rel_stride, float* out);
+
+/* DistMult decoder (IDDGCN.py:103-109) fused with Keras BCE (IDDGCN.py:161-168)
+ * and the seed of the backward.  For each scored edge e:
+ *   a = Xh[h_idx[e]], b = Xt[t_idx ? t_idx[e] : e], rho = rel[r_idx[e]]
+ *   p = sigmoid(sum a*rho*b)                    -> p_out[e] (if p_out)
+ * If y != NULL (training):
+ *   loss_e = -(y log(clip(p)+eps) + (1-y) log(1-clip(p)+eps)), eps = 1e-7
+ *   g = scale * dloss_e/dp (0 where p is clipped), ds = g p (1-p)
+ *   ds_out[e] = ds;  do_out[e] = ds*rho*a * b*(1-b)
+ *   drel_slab[blk][r][:] += ds*a*b ; loss_slab[blk] += loss_e
+ * n_blocks from iddgcn_distmult_blocks(); slabs hold n_blocks*R*D and n_blocks floats. */
+int iddgcn_distmult_blocks(long long T);
+int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R,
+                            const float* Xh, const int* h_idx, const float* Xt, const int* t_idx,
+                            const int* r_idx, const float* rel, const float* y, float scale,
+                            float* p_out, float* ds_out, float* do_out,
+                            float* drel_slab, float* loss_slab, int n_blocks);
+
+/* Deterministic segmented gather-reduce (replaces the UnsortedSegmentSum of
+ * embedding_lookup's gradient): for node n,
+ *   out[n][c] = (dsig ? X[n][c](1-X[n][c]) : 1)
+ *               * sum_{k=seg_ptr[n]}^{seg_ptr[n+1]-1} coef[e] * (rel ? rel[r_idx[e]][c] : 1) * rows[e][c],
+ *   e = perm[k] (perm NULL -> e = k).  Sums run in perm order. */
+int iddgcn_seg_gather_reduce_f32(void* stream, int n_nodes, int d, const int* seg_ptr, const int* perm,
+                                 const float* coef, const int* r_idx, const float* rel,
+                                 const float* rows, const float* X, float* out);
+
+/* Tail-side backward of one layer over edges sorted by tail (contiguous segments):
+ *   dP[r][n][:]   = sum_{e in seg(n)} W[h_idx[e]][r] * dO[e][:]        (gradient of P_r[t])
+ *   dsum[n][:]    = sum_{e in seg(n)} dO[e][:]                          (if dsum; layer-1 x·S input)
+ *   dWedge[e][r]  = <dO[e], P[r][n]>                                    (gradient of sigmoid(alpha_r)) */
+int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const int* seg_ptr,
+                               const int* h_idx, const float* W, const float* dO, const float* P,
+                               long long p_rel_stride, float* dP, long long dp_rel_stride,
+                               float* dsum, float* dWedge);
+
+/* Node-level (head chain) backward of one layer, node n:
+ *   dsum[n] += dO[n]                                   (if dsum)
+ *   dW_r     = <dO[n], P[r][n]> + sum_{k in hseg(n)} dWedge[hperm[k]][r]
+ *   ds_r     = dW_r w_r (1-w_r);  dz[n][j] = s_j (ds_j - sum_r ds_r s_r)   (softmax-sigmoid backward)
+ *   dP[r][n] += w_r * dO[n]                                                   */
+int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const float* dO,
+                             const float* P, long long p_rel_stride, const float* Ssm, const float* W,
+                             const int* hseg_ptr, const int* hperm, const float* dWedge,
+                             float* dP, long long dp_rel_stride, float* dsum, float* dz);
+
+/* out[i] = (accumulate ? out[i] : 0) + scale * sum_{b<n_slabs} slab[b*n + i]  (block order) */
+int iddgcn_reduce_slabs_f32(void* stream, int n_slabs, long long n, const float* slab,
+                            float* out, int accumulate, float scale);
+
+/* Keras-2.7 Adam, one tensor (IDDGCN.py:174,392).  sparse_form=0: TF ApplyAdam
+ *   m += (g-m)(1-b1); v += (g^2-v)(1-b2); var -= alpha m/(sqrt(v)+eps)
+ * sparse_form=1 (_resource_apply_sparse, embeddings): m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2.
+ * alpha = lr sqrt(1-b2^t)/(1-b1^t) is computed by the caller. */
+int iddgcn_adam_f32(void* stream, long long n, float* var, float* m, float* v, const float* g,
+                    float alpha, float b1, float b2, float eps, int sparse_form);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IDDGCN_H_ */

@@ -1,0 +1,292 @@
+"""Per-kernel numerics on the GPU, each against a plain torch reference of the same op.
+
+Tolerances: fp32 kernels vs an fp64 torch reference, |err| <= 2e-5 * (1 + |ref|)
+scaled by the reduction length where sums are long.  Index/permutation work is exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from iddgcn_amd import _lib as L
+from iddgcn_amd import ops
+
+pytestmark = pytest.mark.gpu
+DIMS = [32, 64, 128, 256]
+
+
+def rnd(*s, dev, scale=1.0, gen=None):
+    return (torch.randn(*s, generator=gen, dtype=torch.float64) * scale).to(dev)
+
+
+def close(got, ref, tol):
+    got = got.double()
+    err = (got - ref).abs().max().item()
+    lim = tol * (1.0 + ref.abs().max().item())
+    assert err <= lim, f"max err {err} > {lim}"
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_spmm_csr(D, cuda):
+    g = torch.Generator().manual_seed(D)
+    N, R, nnz = 517, 3, 4000
+    rows = torch.randint(0, N, (R, nnz), generator=g)
+    cols = torch.randint(0, N, (R, nnz), generator=g)
+    X = rnd(N, D, dev=cuda, gen=g)
+    ptrs, colsl, ref = [], [], torch.zeros(R, N, D, dtype=torch.float64, device=cuda)
+    off = 0
+    for r in range(R):
+        key = torch.unique(rows[r] * N + cols[r])
+        rr, cc = key // N, key % N
+        ptr = torch.zeros(N + 1, dtype=torch.int64)
+        ptr[1:] = torch.cumsum(torch.bincount(rr, minlength=N), 0)
+        ptrs.append(ptr + off)
+        colsl.append(cc)
+        off += cc.numel()
+        ref[r].index_add_(0, rr.to(cuda), X[cc.to(cuda)])
+    ptr = torch.cat(ptrs).to(torch.int32).to(cuda)
+    col = torch.cat(colsl).to(torch.int32).to(cuda)
+    Y = torch.empty(R, N, D, device=cuda)
+    ops.spmm_csr(ptr, col, None, X.float(), Y, R, N)
+    close(Y, ref, 1e-5)
+    vals = torch.rand(off, generator=g).to(cuda)
+    Y2 = Y.clone()
+    ops.spmm_csr(ptr, col, vals, X.float(), Y2, R, N, accumulate=True)
+    ref2 = ref.clone()
+    start = 0
+    for r in range(R):
+        n = colsl[r].numel()
+        rr = torch.repeat_interleave(torch.arange(N), torch.diff(ptrs[r]))
+        ref2[r].index_add_(0, rr.to(cuda), X[colsl[r].to(cuda)] * vals[start:start + n, None].double())
+        start += n
+    close(Y2, ref2, 1e-5)
+
+
+@pytest.mark.parametrize("D", DIMS)
+@pytest.mark.parametrize("trans", [False, True])
+def test_rowgemm_plain(D, trans, cuda):
+    g = torch.Generator().manual_seed(7 * D + trans)
+    M = 1000 + D // 32        # not a multiple of any tile height
+    A, B = rnd(M, D, dev=cuda, gen=g), rnd(D, D, dev=cuda, gen=g)
+    C = torch.empty(M, D, device=cuda)
+    ops.rowgemm(A.float(), B.float(), C, b_trans=trans)
+    ref = A @ (B.t() if trans else B)
+    close(C, ref, 2e-5 * np.sqrt(D))
+    # MFMA path is exact f32: bitwise deterministic run to run
+    C2 = torch.empty_like(C)
+    ops.rowgemm(A.float(), B.float(), C2, b_trans=trans)
+    assert torch.equal(C, C2)
+
+
+@pytest.mark.parametrize("D", [64, 256])
+def test_rowgemm_asymmetric_identity(D, cuda):
+    """A = I (first D rows) with an asymmetric B catches a transposed C-write."""
+    M = 3 * D
+    A = torch.zeros(M, D, device=cuda)
+    A[:D] = torch.eye(D, device=cuda)
+    B = torch.arange(D * D, dtype=torch.float32, device=cuda).view(D, D) / (D * D)
+    C = torch.empty(M, D, device=cuda)
+    ops.rowgemm(A, B, C)
+    assert torch.equal(C[:D], B)
+    assert torch.equal(C[D:], torch.zeros_like(C[D:]))
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_rowgemm_combine_epilogue(D, cuda):
+    """C = sigmoid(A[a_idx]·S + sum_r W[h,r] * P_r[t]) — the tail-layer forward."""
+    g = torch.Generator().manual_seed(11 + D)
+    N, M, R = 300, 2049, 3
+    X = rnd(N, D, dev=cuda, gen=g, scale=0.2)
+    S = rnd(D, D, dev=cuda, gen=g, scale=D ** -0.5)
+    W = torch.rand(N, R, generator=g, dtype=torch.float64).to(cuda)
+    P = rnd(R, N, D, dev=cuda, gen=g)
+    a_idx = torch.randint(0, N, (M,), generator=g).to(cuda)
+    h = torch.randint(0, N, (M,), generator=g).to(cuda)
+    t = torch.randint(0, N, (M,), generator=g).to(cuda)
+    C = torch.empty(M, D, device=cuda)
+    ops.rowgemm(X.float(), S.float(), C, a_idx=a_idx.int(), coef=W.float(), coef_idx=h.int(), V=P.float(),
+                v_idx=t.int(), v_rel_stride=N * D, act=L.ACT_SIGMOID)
+    pre = X[a_idx] @ S
+    for r in range(R):
+        pre = pre + W[h, r:r + 1] * P[r][t]
+    close(C, torch.sigmoid(pre), 2e-5)
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_rowgemm_rank_update_dsigmoid_accumulate(D, cuda):
+    """C = (C + dO·S^T + dz·Wa^T) * X(1-X) — the node-level head backward."""
+    g = torch.Generator().manual_seed(13 + D)
+    M, R = 777, 4
+    dO, S = rnd(M, D, dev=cuda, gen=g), rnd(D, D, dev=cuda, gen=g)
+    dz, Wa = rnd(M, R, dev=cuda, gen=g), rnd(D, R, dev=cuda, gen=g)
+    X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
+    C0 = rnd(M, D, dev=cuda, gen=g)
+    C = C0.float().clone()
+    WaT = Wa.t().contiguous().float()
+    ops.rowgemm(dO.float(), S.float(), C, b_trans=True, accumulate=True, coef=dz.float(), V=WaT, v_rel_stride=D,
+                v_row_stride=0, act=L.ACT_DSIGMOID, aux=X.float())
+    ref = (C0 + dO @ S.t() + dz @ Wa.t()) * X * (1 - X)
+    close(C, ref, 3e-5 * np.sqrt(D))
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_gemm_tn(D, cuda):
+    g = torch.Generator().manual_seed(17 + D)
+    M = 5003
+    A, B = rnd(M, D, dev=cuda, gen=g), rnd(M, D, dev=cuda, gen=g)
+    C = rnd(D, D, dev=cuda, gen=g).float()
+    C0 = C.double().clone()
+    slab = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
+    ops.gemm_tn(A.float(), B.float(), C, slab, accumulate=True)
+    close(C, C0 + A.t() @ B, 2e-6 * np.sqrt(M))
+    C1 = torch.empty(D, D, device=cuda)
+    ops.gemm_tn(A.float(), B.float(), C1, slab)
+    C2 = torch.empty(D, D, device=cuda)
+    ops.gemm_tn(A.float(), B.float(), C2, slab)
+    assert torch.equal(C1, C2)              # slab reduction in block order: deterministic
+
+
+@pytest.mark.parametrize("D", [32, 256])
+def test_gemm_tn_narrow(D, cuda):
+    g = torch.Generator().manual_seed(19 + D)
+    M, R = 9001, 3
+    A, dz = rnd(M, D, dev=cuda, gen=g), rnd(M, R, dev=cuda, gen=g)
+    dWa, dba = torch.empty(D, R, device=cuda), torch.empty(R, device=cuda)
+    slab = torch.empty((ops.tn_narrow_blocks(M) + 1) * (D + 1) * R, device=cuda)
+    ops.gemm_tn_narrow(A.float(), dz.float(), dWa, dba, slab)
+    close(dWa, A.t() @ dz, 2e-6 * np.sqrt(M))
+    close(dba, dz.sum(0), 2e-6 * np.sqrt(M))
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_alpha(D, cuda):
+    g = torch.Generator().manual_seed(23 + D)
+    M, R = 999, 4
+    X, Wa, ba = rnd(M, D, dev=cuda, gen=g), rnd(D, R, dev=cuda, gen=g, scale=0.2), rnd(R, dev=cuda, gen=g)
+    S, W = torch.empty(M, R, device=cuda), torch.empty(M, R, device=cuda)
+    ops.alpha_fwd(X.float(), Wa.float(), ba.float(), S, W)
+    s = torch.softmax(X @ Wa + ba, -1)
+    close(S, s, 1e-5)
+    close(W, torch.sigmoid(s), 1e-5)
+    idx = torch.randint(0, M, (50,), generator=g).to(cuda)
+    S2, W2 = torch.empty(50, R, device=cuda), torch.empty(50, R, device=cuda)
+    ops.alpha_fwd(X.float(), Wa.float(), ba.float(), S2, W2, x_idx=idx.int())
+    assert torch.equal(S2, S[idx]) and torch.equal(W2, W[idx])
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_combine(D, cuda):
+    g = torch.Generator().manual_seed(29 + D)
+    N, M, R = 200, 3001, 2
+    Y, P = rnd(N, D, dev=cuda, gen=g), rnd(R, N, D, dev=cuda, gen=g)
+    W = torch.rand(N, R, generator=g, dtype=torch.float64).to(cuda)
+    h = torch.randint(0, N, (M,), generator=g).to(cuda)
+    t = torch.randint(0, N, (M,), generator=g).to(cuda)
+    out = torch.empty(M, D, device=cuda)
+    ops.combine(Y.float(), W.float(), P.float(), out, y_idx=t.int(), coef_idx=h.int(), v_idx=t.int())
+    ref = Y[t] + sum(W[h, r:r + 1] * P[r][t] for r in range(R))
+    close(out, torch.sigmoid(ref), 1e-5)
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_distmult_bce_matches_autograd(D, cuda):
+    g = torch.Generator().manual_seed(31 + D)
+    N, T, R = 400, 5000, 3
+    Xh = torch.rand(N, D, generator=g, dtype=torch.float64).to(cuda)
+    Xt = torch.rand(T, D, generator=g, dtype=torch.float64).to(cuda)
+    rel = rnd(R, D, dev=cuda, gen=g, scale=0.3)
+    h = torch.randint(0, N, (T,), generator=g).to(cuda)
+    r = torch.randint(0, R, (T,), generator=g).to(cuda)
+    y = (torch.rand(T, generator=g) < 0.5).double().to(cuda)
+    scale = 1.0 / (T * N)
+    nb = ops.distmult_blocks(T)
+    p, ds, do = torch.empty(T, device=cuda), torch.empty(T, device=cuda), torch.empty(T, D, device=cuda)
+    drel_slab, loss_slab = torch.empty(nb * R * D, device=cuda), torch.empty(nb, device=cuda)
+    ops.distmult_bce(Xh.float(), h.int(), Xt.float(), r.int(), rel.float(), y=y.float(), scale=scale, p_out=p,
+                     ds_out=ds, do_out=do, drel_slab=drel_slab, loss_slab=loss_slab)
+    drel, loss = torch.empty(R, D, device=cuda), torch.empty(1, device=cuda)
+    ops.reduce_slabs(drel_slab, nb, drel)
+    ops.reduce_slabs(loss_slab, nb, loss)
+    # torch reference: Keras BCE with eps clip, x 1/N, gradient w.r.t. rel and the tail pre-activation
+    xt = Xt.clone().requires_grad_(True)
+    relv = rel.clone().requires_grad_(True)
+    s = (Xh[h] * relv[r] * xt).sum(-1)
+    pr = torch.sigmoid(s)
+    eps = 1e-7
+    pc = pr.clamp(eps, 1 - eps)
+    bce = -(y * torch.log(pc + eps) + (1 - y) * torch.log(1 - pc + eps))
+    (bce.mean() / N).backward()
+    close(p, pr.detach(), 1e-6)
+    assert abs(loss.item() / T - bce.mean().item()) < 1e-5
+    close(drel, relv.grad, 1e-4)
+    close(do, xt.grad * Xt * (1 - Xt), 1e-4)
+    # predict-only mode writes p and nothing else
+    p2 = torch.empty(T, device=cuda)
+    ops.distmult_bce(Xh.float(), h.int(), Xt.float(), r.int(), rel.float(), p_out=p2)
+    assert torch.equal(p, p2)
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_segment_reductions(D, cuda):
+    """seg_gather_reduce / tail_seg_reduce / head_bwd_node against index_add references."""
+    g = torch.Generator().manual_seed(37 + D)
+    N, T, R = 257, 6000, 3
+    t = torch.sort(torch.randint(0, N, (T,), generator=g)).values
+    h = torch.randint(0, N, (T,), generator=g)
+    tptr = torch.searchsorted(t, torch.arange(N + 1), right=False).to(torch.int32).to(cuda)
+    hperm = torch.argsort(h, stable=True)
+    hptr = torch.searchsorted(h[hperm], torch.arange(N + 1), right=False).to(torch.int32).to(cuda)
+    t, h, hperm = t.to(cuda), h.to(cuda), hperm.to(cuda)
+    rows = rnd(T, D, dev=cuda, gen=g)
+    coef = rnd(T, dev=cuda, gen=g)
+    r_idx = torch.randint(0, R, (T,), generator=g).to(cuda)
+    rel = rnd(R, D, dev=cuda, gen=g)
+    X = torch.rand(N, D, generator=g, dtype=torch.float64).to(cuda)
+    out = torch.empty(N, D, device=cuda)
+    ops.seg_gather_reduce(hptr, rows.float(), out, perm=hperm.int(), coef=coef.float(), r_idx=r_idx.int(),
+                          rel=rel.float(), X=X.float())
+    ref = torch.zeros(N, D, dtype=torch.float64, device=cuda).index_add_(0, h, coef[:, None] * rel[r_idx] * rows)
+    close(out, ref * X * (1 - X), 1e-5)
+
+    W = torch.rand(N, R, generator=g, dtype=torch.float64).to(cuda)
+    P = rnd(R, N, D, dev=cuda, gen=g)
+    dO = rnd(T, D, dev=cuda, gen=g)
+    dP, dWe, dsum = torch.empty(R, N, D, device=cuda), torch.empty(T, R, device=cuda), torch.empty(N, D, device=cuda)
+    ops.tail_seg_reduce(tptr, h.int(), W.float(), dO.float(), P.float(), dP, dWe, dsum=dsum)
+    for r in range(R):
+        close(dP[r], torch.zeros(N, D, dtype=torch.float64, device=cuda).index_add_(0, t, W[h, r:r + 1] * dO), 1e-5)
+        close(dWe[:, r], (dO * P[r][t]).sum(-1), 1e-5)
+    close(dsum, torch.zeros(N, D, dtype=torch.float64, device=cuda).index_add_(0, t, dO), 1e-5)
+
+    dOn = rnd(N, D, dev=cuda, gen=g)
+    Ssm = torch.softmax(rnd(N, R, dev=cuda, gen=g), -1)
+    Wn = torch.sigmoid(Ssm)
+    dP0 = dP.clone()
+    dsum0 = dsum.clone()
+    dz = torch.empty(N, R, device=cuda)
+    ops.head_bwd_node(dOn.float(), P.float(), Ssm.float(), Wn.float(), dP, dz, hseg_ptr=hptr, hperm=hperm.int(),
+                      dWedge=dWe, dsum=dsum)
+    dWn = (dOn[None] * P).sum(-1).t() + torch.zeros(N, R, dtype=torch.float64, device=cuda).index_add_(0, h, dWe.double())
+    s_ = Ssm.clone().requires_grad_(True)
+    (torch.sigmoid(s_) * dWn).sum().backward()
+    ds = s_.grad
+    dz_ref = Ssm * (ds - (ds * Ssm).sum(-1, keepdim=True))
+    close(dz, dz_ref, 1e-5)
+    close(dP, dP0.double() + Wn.t()[:, :, None] * dOn[None], 1e-5)
+    close(dsum, dsum0.double() + dOn, 1e-6)
+
+
+def test_adam_kernel_matches_keras_forms(cuda):
+    g = torch.Generator().manual_seed(41)
+    n = 10001
+    var, gr = torch.randn(n, generator=g).to(cuda), torch.randn(n, generator=g).to(cuda) * 1e-3
+    m, v = torch.randn(n, generator=g).abs().to(cuda) * 1e-3, torch.rand(n, generator=g).to(cuda) * 1e-6
+    b1, b2, eps, alpha = 0.9, 0.999, 1e-7, 3e-4
+    for sparse in (0, 1):
+        var2, m2, v2 = var.clone(), m.clone(), v.clone()
+        ops.adam(var2, m2, v2, gr, alpha, b1, b2, eps, sparse)
+        vd, md, vvd, gd = var.double(), m.double(), v.double(), gr.double()
+        mr = md * b1 + gd * (1 - b1)
+        vr = vvd * b2 + gd * gd * (1 - b2)
+        close(m2, mr, 1e-6)
+        close(v2, vr, 1e-6)
+        close(var2, vd - alpha * mr / (vr.sqrt() + eps), 1e-6)

@@ -1,0 +1,165 @@
+"""Host logic of the product path (no GPU): graph build, layouts, C-ABI exports."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from iddgcn_amd import _lib
+from iddgcn_amd.graph import DeviceAdjacency, ScoredEdges, get_adj_mats
+from iddgcn_amd.utils import generate_reverse_triplets, get_y_true, synthetic_graph
+from oracle import ref_utils
+from tests.conftest import ROOT
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "iddgcn.h")).read()
+    return sorted(set(re.findall(r"^\s*int\s+(iddgcn_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()          # loads the .so, binds all prototypes, checks ABI version (no GPU call)
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} not bound in _lib.SIGNATURES"
+    assert lib.iddgcn_abi_version() == _lib.ABI_VERSION
+
+
+def test_block_helpers_are_pure_host():
+    lib = _lib.lib()
+    assert lib.iddgcn_gemm_tn_blocks(4_000_000, 256) == 256
+    assert lib.iddgcn_gemm_tn_blocks(10, 64) == 1
+    assert lib.iddgcn_distmult_blocks(1) == 1
+
+
+def test_invalid_args_rejected_before_launch():
+    lib = _lib.lib()
+    # D=48 unsupported, R=9 unsupported: rejected on the host, nothing launched
+    assert lib.iddgcn_spmm_csr_f32(None, 1, 4, 48, None, None, None, None, None, 0) == -1
+    assert lib.iddgcn_alpha_fwd_f32(None, 4, 64, 9, None, None, None, None, None, None) == -2
+    assert lib.iddgcn_adam_f32(None, 4, None, None, None, None, 1.0, .9, .999, 1e-7, 0) == -3
+
+
+@pytest.mark.parametrize("k", [0, 3])
+def test_get_adj_mats_matches_oracle_bit_exact(k, golden):
+    d = golden(f"fold{k}_data.npz")
+    data = np.concatenate([d["X_train"], d["X_test"]])
+    ours = get_adj_mats(data, 845, 4)
+    ref = ref_utils.get_adj_coo(data, 845, 4)
+    for a, (idx, val) in zip(ours, ref):
+        assert a.dense_shape == (1, 845, 845)
+        assert np.array_equal(a.indices[:, 0], np.zeros(a.nnz))
+        assert np.array_equal(a.indices[:, 1:], idx)
+        assert np.array_equal(a.values, val)
+    assert [a.nnz for a in get_adj_mats(d["X_train"], 845, 4)] == [1482, 1324, 2346, 32358] if k == 0 else True
+
+
+def test_empty_relation_placeholder():
+    tr = np.array([[0, 0, 1], [1, 0, 0]])
+    mats = get_adj_mats(tr, 3, 2)
+    assert mats[1].indices.tolist() == [[0, 0, 0]] and mats[1].values.tolist() == [0.0]
+    dev = DeviceAdjacency(mats, 3, "cpu")
+    assert dev.fwd_val is not None                  # placeholder value 0 is carried
+    assert dev.fwd_ptr.tolist() == [0, 1, 2, 2, 2, 3, 3, 3]
+
+
+def test_device_adjacency_csr_and_transpose():
+    pos, _ = synthetic_graph(300, 3, 2000, seed=1)
+    mats = get_adj_mats(pos, 300, 3)
+    dev = DeviceAdjacency(mats, 300, "cpu")
+    ptr, col = dev.fwd_ptr.numpy().reshape(3, 301), dev.fwd_col.numpy()
+    for r, a in enumerate(mats):
+        rows = np.repeat(np.arange(300), np.diff(ptr[r]))
+        cols = col[ptr[r, 0]:ptr[r, -1]]
+        assert np.array_equal(np.stack([rows, cols], 1), a.indices[:, 1:])    # CSR order == TF order
+    # merged transpose: row c lists r*N+m for every (m, c) in A_r, relation-major then m
+    bptr, bcol = dev.bwd_ptr.numpy(), dev.bwd_col.numpy()
+    dense = np.zeros((300, 3 * 300))
+    for r, a in enumerate(mats):
+        dense[a.cols, r * 300 + a.rows] = 1
+    got = np.zeros_like(dense)
+    for c in range(300):
+        seg = bcol[bptr[c]:bptr[c + 1]]
+        assert np.all(np.diff(seg) > 0)
+        got[c, seg] = 1
+    assert np.array_equal(got, dense)
+
+
+def test_scored_edges_layout():
+    rng = np.random.default_rng(0)
+    tr = np.stack([rng.integers(0, 50, 400), rng.integers(0, 2, 400), rng.integers(0, 50, 400)], 1)
+    lab = rng.random(400).astype(np.float32)
+    ed = ScoredEdges(tr, lab, 50, 2, "cpu")
+    t, h = ed.t.numpy(), ed.h.numpy()
+    assert np.all(np.diff(t) >= 0)                                     # tail-sorted
+    assert np.array_equal(tr[ed.order], np.stack([h, ed.r.numpy(), t], 1))
+    tptr = ed.tptr.numpy()
+    for n in range(50):
+        assert np.all(t[tptr[n]:tptr[n + 1]] == n)
+    hp, hptr = ed.hperm.numpy(), ed.hptr.numpy()
+    for n in range(50):
+        seg = hp[hptr[n]:hptr[n + 1]]
+        assert np.all(h[seg] == n) and np.all(np.diff(seg) > 0)        # stable
+    x = torch.arange(400, dtype=torch.float32)
+    assert np.array_equal(ed.unsort(x[torch.as_tensor(ed.order)]).numpy(), x.numpy())
+    assert np.array_equal(ed.y.numpy(), lab[ed.order])
+
+
+def test_index_validation():
+    with pytest.raises(_lib.IddgcnError):
+        ScoredEdges(np.array([[0, 0, 5]]), None, 5, 1, "cpu")
+    with pytest.raises(_lib.IddgcnError):
+        ScoredEdges(np.array([[0, 2, 1]]), None, 5, 2, "cpu")
+    with pytest.raises(_lib.IddgcnError):
+        get_adj_mats(np.array([[0, 0, 7]]), 5, 1)
+
+
+def test_utils_match_oracle():
+    rng = np.random.default_rng(3)
+    tr = np.stack([rng.integers(0, 9, 50), rng.integers(0, 2, 50), rng.integers(0, 9, 50)], 1)
+    assert np.array_equal(generate_reverse_triplets(tr), ref_utils.generate_reverse_triplets(tr))
+    assert np.array_equal(get_y_true(tr[:20], tr), ref_utils.get_y_true(tr[:20], tr))
+
+
+def test_synthetic_graph_shape_and_rules():
+    pos, neg = synthetic_graph(2000, 4, 20000, seed=0)
+    assert pos.shape == (20000, 3) and neg.shape == (20000, 3)
+    assert np.all(pos[:, 0] != pos[:, 2])
+    key = set(map(tuple, pos.tolist()))
+    assert len(key) == 20000                                           # unique directed edges
+    assert all((t, r, h) in key for h, r, t in pos[:200].tolist())     # reverse-closed
+    n_mut = int(round(2000 * 661 / 845))
+    resp = pos[pos[:, 1] < 2]
+    assert np.all((resp[:, 0] < n_mut) != (resp[:, 2] < n_mut))        # mutation <-> drug
+    same = (neg[:, 0] == pos[:, 0]) | (neg[:, 2] == pos[:, 2])
+    assert same.all()
+
+
+def test_model_surface_cpu_only():
+    from iddgcn_amd import get_IDDGCN_Model
+    m = get_IDDGCN_Model(845, 4, 64, 64, 89, None, 0, 0)
+    names = [l.name for l in m.layers]
+    assert names == ["entity_embeddings", "iddgcn__layer", "iddgcn__layer_1", "iddgcn__layer_2", "DistMult"]
+    shapes = [w.shape for w in m.get_layer("iddgcn__layer").get_weights()]
+    assert shapes == [(4, 64, 64), (64, 64), (4,), (64, 4), (4,)]
+    assert m.get_layer("DistMult").get_weights()[0].shape == (4, 64)
+    w = m.get_layer("entity_embeddings").get_weights()[0]
+    assert w.shape == (845, 64) and w.min() >= 0 and w.max() < 1
+
+
+def test_load_npz_weights(golden, tmp_path):
+    from iddgcn_amd import get_IDDGCN_Model
+    m = get_IDDGCN_Model(845, 4, 64, 64, 89, None, 0, 0)
+    m.load_weights(os.path.join(ROOT, "tests", "golden", "weights_fold0.npz"))
+    g = golden("weights_fold0.npz")
+    assert np.array_equal(m.get_layer("entity_embeddings").get_weights()[0], g["E"])
+    assert np.array_equal(m.get_layer("iddgcn__layer_2").get_weights()[3], g["Wa3"])
+    p = str(tmp_path / "w.npz")
+    m.save_weights(p)
+    m2 = get_IDDGCN_Model(845, 4, 64, 64, 1, None, 0, 0)
+    m2.load_weights(p)
+    for a, b in zip(m.get_weights(), m2.get_weights()):
+        assert np.array_equal(a, b)
