@@ -38,6 +38,7 @@ SIGNATURES = {
     "iddgcn_abi_version": (ci, []),
     "iddgcn_spmm_csr_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, ci]),
     "iddgcn_rowgemm_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
+    "iddgcn_set_rowgemm_path": (ci, [ci]),
     "iddgcn_gemm_tn_blocks": (ci, [cll, ci]),
     "iddgcn_gemm_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
     "iddgcn_gemm_tn_narrow_blocks": (ci, [cll]),

@@ -42,6 +42,8 @@ inline int launch_status() {
     return e == hipSuccess ? 0 : (int)e;
 }
 inline bool dim_ok(int d) { return d == 32 || d == 64 || d == 128 || d == 256; }
+// test hook: force the register-staged rowgemm (A/B comparisons of the two D=256 paths)
+static int g_force_v1 = 0;
 
 // ---------------------------------------------------------------------------
 // CSR SpMM: one row per group of D/4 lanes, sequential sum in CSR order.
@@ -189,6 +191,194 @@ __global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmP p) {
             }
             *cp = v;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Row GEMM, D = 256, pipelined with LDS-DMA (global_load_lds_dwordx4).
+//   One persistent 512-thread workgroup per CU walks a contiguous range of
+//   32-row tiles.  Per tile, BEFORE the 128 MFMAs of each wave are issued:
+//     - the next tile's A rows are DMA'd into the other half of a double buffer,
+//     - this tile's epilogue operand rows (R gathered P_r[v_idx[e]] rows, or the
+//       sigma' aux rows) are DMA'd into the epilogue buffer,
+//     - this tile's per-row coefficients are loaded into registers,
+//     - the row indices of the next tile are loaded,
+//   so the memory latency hides under the MFMA phase; the epilogue then reads
+//   LDS only.  One wave-instruction moves exactly one 1 KiB row, so LDS rows can
+//   be padded to 1040 B (conflict-free ds_read_b128 of the A fragments).
+//   All LDS lives in ONE __shared__ array (separate arrays make hipcc drain vmcnt).
+// ---------------------------------------------------------------------------
+namespace r256 {
+constexpr int D = 256, NW = 8, TR = 32, LDA = D + 4;
+constexpr int ROWS_PER_WAVE = TR / NW;                     // 4
+constexpr int A_FLOATS = TR * LDA;                         // one A buffer
+constexpr int EPI_MAX = 2;                                 // epilogue operand rows per output row
+constexpr int COEF_FLOATS = TR * MAX_R;
+constexpr int LDS_FLOATS = 2 * A_FLOATS + EPI_MAX * A_FLOATS + COEF_FLOATS;
+}  // namespace r256
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* gbl_vptr;
+
+__device__ __forceinline__ void dma_row_1k(const float* src_row, float* lds_row, int lane) {
+    __builtin_amdgcn_global_load_lds((gbl_vptr)(src_row + lane * 4), (lds_vptr)lds_row, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi_rows) {
+    using namespace r256;
+    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+    float* bufA = lds;                                  // [2][TR][LDA]
+    float* epi = lds + 2 * A_FLOATS;                    // [EPI_MAX][TR][LDA]
+    float* coefL = epi + EPI_MAX * A_FLOATS;            // [TR][MAX_R]
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int i = lane & 31, h = lane >> 5;
+    const int c0 = wave * 32;
+    const int R = p.R;
+    const bool gatherV = (R > 0) && (p.v_row_stride != 0);
+
+    float breg[D / 2];
+#pragma unroll
+    for (int s = 0; s < D / 2; ++s) {
+        const int kk = 8 * (s >> 2) + 4 * h + (s & 3);
+        breg[s] = p.b_trans ? p.B[(c0 + i) * D + kk] : p.B[kk * D + c0 + i];
+    }
+
+    const long long ntiles = ((long long)p.M + TR - 1) / TR;
+    const long long t_beg = (long long)blockIdx.x * p.tiles_per_block;
+    long long t_end = t_beg + p.tiles_per_block;
+    if (t_end > ntiles) t_end = ntiles;
+    if (t_beg >= t_end) return;
+    const long long Mlast = (long long)p.M - 1;
+
+    // row index of this wave's j-th row of tile t (clamped: rows past M load row M-1, never stored)
+    auto row_of = [&](long long t, int j) -> long long {
+        long long e = t * TR + wave * ROWS_PER_WAVE + j;
+        return e > Mlast ? Mlast : e;
+    };
+    // lanes 0..3 load the indices of the wave's 4 rows of tile t
+    auto load_idx = [&](const int* idx, long long t) -> int {
+        if (!idx || lane >= ROWS_PER_WAVE || t >= t_end) return 0;
+        return idx[row_of(t, lane)];
+    };
+    // wave-uniform copies (SGPRs) of the 4 row indices, made once the loads have landed
+    int sa[ROWS_PER_WAVE], sv[ROWS_PER_WAVE], sc[ROWS_PER_WAVE];
+    auto to_sgpr = [&](int v, int (&dst)[ROWS_PER_WAVE]) {
+#pragma unroll
+        for (int j = 0; j < ROWS_PER_WAVE; ++j) dst[j] = __builtin_amdgcn_readlane(v, j);
+    };
+
+    // prologue: A(t_beg) -> buffer 0; indices for A(t_beg+1) and the epilogue of t_beg
+    {
+        int ia0 = load_idx(p.a_idx, t_beg);
+        int ia1 = load_idx(p.a_idx, t_beg + 1);
+        int iv0 = load_idx(p.v_idx, t_beg);
+        int ic0 = load_idx(p.coef_idx, t_beg);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        to_sgpr(ia0, sa);
+#pragma unroll
+        for (int j = 0; j < ROWS_PER_WAVE; ++j) {
+            const long long src = p.a_idx ? (long long)sa[j] : row_of(t_beg, j);
+            dma_row_1k(p.A + src * D, bufA + (wave * ROWS_PER_WAVE + j) * LDA, lane);
+        }
+        to_sgpr(ia1, sa);
+        to_sgpr(iv0, sv);
+        to_sgpr(ic0, sc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    int b = 0;
+    for (long long t = t_beg; t < t_end; ++t, b ^= 1) {
+        const long long row0 = t * TR;
+        // (1) epilogue operand rows of tile t -> epi
+        if (gatherV) {
+#pragma unroll
+            for (int j = 0; j < ROWS_PER_WAVE; ++j) {
+                const long long vi = p.v_idx ? (long long)sv[j] : row_of(t, j);
+                for (int r = 0; r < R; ++r)
+                    dma_row_1k(p.V + r * p.v_rel_stride + vi * p.v_row_stride,
+                               epi + (r * TR + wave * ROWS_PER_WAVE + j) * LDA, lane);
+            }
+        } else if (epi_rows) {      // sigma' aux rows, same rows as the output
+#pragma unroll
+            for (int j = 0; j < ROWS_PER_WAVE; ++j)
+                dma_row_1k(p.aux + row_of(t, j) * D, epi + (wave * ROWS_PER_WAVE + j) * LDA, lane);
+        }
+        // (2) per-row coefficients of tile t (lanes 0 .. 4R-1)
+        float creg = 0.f;
+        if (R > 0 && lane < ROWS_PER_WAVE * R) {
+            const int j = lane / R, r = lane % R;
+            long long ci;
+            if (p.coef_idx)
+                ci = j == 0 ? sc[0] : j == 1 ? sc[1] : j == 2 ? sc[2] : sc[3];
+            else
+                ci = row_of(t, j);
+            creg = p.coef[ci * R + r];
+        }
+        // (3) A rows of tile t+1 -> the other buffer
+        if (t + 1 < t_end) {
+#pragma unroll
+            for (int j = 0; j < ROWS_PER_WAVE; ++j) {
+                const long long src = p.a_idx ? (long long)sa[j] : row_of(t + 1, j);
+                dma_row_1k(p.A + src * D, bufA + (b ^ 1) * A_FLOATS + (wave * ROWS_PER_WAVE + j) * LDA, lane);
+            }
+        }
+        // (4) indices for the next iteration
+        const int ia_n = load_idx(p.a_idx, t + 2);
+        const int iv_n = load_idx(p.v_idx, t + 1);
+        const int ic_n = load_idx(p.coef_idx, t + 1);
+
+        // (5) MFMA over A(t)
+        f32x16 acc;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+        const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h;
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            const f32x4 a4 = ld4(arow + 8 * q);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[0], breg[4 * q + 0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[1], breg[4 * q + 1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[2], breg[4 * q + 2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[3], breg[4 * q + 3], acc, 0, 0, 0);
+        }
+        // (6)-(9) everything this wave issued has landed; publish coefficients; barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (R > 0 && lane < ROWS_PER_WAVE * R) {
+            const int j = lane / R, r = lane % R;
+            coefL[(wave * ROWS_PER_WAVE + j) * MAX_R + r] = creg;
+        }
+        to_sgpr(ia_n, sa);
+        to_sgpr(iv_n, sv);
+        to_sgpr(ic_n, sc);
+        __syncthreads();
+
+        // (10) epilogue from LDS (same add order as rowgemm_kernel)
+        const int c = c0 + i;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const long long e = row0 + row;
+            if (e >= p.M) continue;
+            float v = acc[reg];
+            float* cp = p.C + e * D + c;
+            if (p.accumulate) v += *cp;
+            if (gatherV) {
+                for (int r = 0; r < R; ++r) v += coefL[row * MAX_R + r] * epi[(r * TR + row) * LDA + c];
+            } else if (R > 0) {        // broadcast V (v_row_stride == 0): tiny, cache-resident
+                for (int r = 0; r < R; ++r) v += coefL[row * MAX_R + r] * p.V[r * p.v_rel_stride + c];
+            }
+            if (p.act == IDDGCN_ACT_SIGMOID) {
+                v = sigmoidf_(v);
+            } else if (p.act == IDDGCN_ACT_DSIGMOID) {
+                const float x = epi[row * LDA + c];
+                v = v * (x * (1.0f - x));
+            }
+            *cp = v;
+        }
+        // (11) epilogue buffers free for the next tile
+        __syncthreads();
     }
 }
 
@@ -672,6 +862,12 @@ extern "C" {
 
 int iddgcn_abi_version(void) { return IDDGCN_ABI_VERSION; }
 
+int iddgcn_set_rowgemm_path(int force_register_staged) {
+    const int old = g_force_v1;
+    g_force_v1 = force_register_staged ? 1 : 0;
+    return old;
+}
+
 int iddgcn_spmm_csr_f32(void* stream, int n_seg, int n_rows, int d, const int* row_ptr, const int* col,
                         const float* vals, const float* X, float* Y, int accumulate) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
@@ -712,6 +908,18 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
         p.tiles_per_block = (int)((nt + nb - 1) / nb);                                          \
         nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;                                  \
         hipLaunchKernelGGL(rowgemm_kernel<DD>, dim3((unsigned)nb), dim3(RG<DD>::NW * 64), 0, st, p); \
+    }
+    const bool gatherV = p.R > 0 && p.v_row_stride != 0;
+    const int epi_rows = gatherV ? p.R : (p.act == IDDGCN_ACT_DSIGMOID ? 1 : 0);
+    const bool dma_ok = a->D == 256 && epi_rows <= r256::EPI_MAX && !(gatherV && p.act == IDDGCN_ACT_DSIGMOID) &&
+                        (!gatherV || p.v_row_stride == 256) && !g_force_v1;
+    if (dma_ok) {
+        const long long nt = ((long long)p.M + r256::TR - 1) / r256::TR;
+        long long nb = nt < 256 ? nt : 256;
+        p.tiles_per_block = (int)((nt + nb - 1) / nb);
+        nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
+        hipLaunchKernelGGL(rowgemm256_dma_kernel, dim3((unsigned)nb), dim3(512), 0, st, p, epi_rows);
+        return launch_status();
     }
     switch (a->D) {
         case 32: RGEMM(32, 2048); break;

@@ -68,6 +68,11 @@ typedef struct {
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 
+/* Select the D=256 row-GEMM pipeline: 0 (default) = LDS-DMA pipelined kernel where
+ * applicable, 1 = register-staged kernel everywhere.  Host-side switch for A/B
+ * tests and benchmarks; returns the previous setting. */
+int iddgcn_set_rowgemm_path(int force_register_staged);
+
 /* C[D][D] (+)= A^T · B over M rows (A, B are M x D).  Two stages: each of n_blocks
  * workgroups writes a D x D partial into `slab` (n_blocks*D*D floats), then the
  * partials are summed in block order (deterministic).  n_blocks from
