@@ -483,6 +483,86 @@ __global__ __launch_bounds__(TN<D>::NW * 64) void gemm_tn_kernel(long long M, lo
     }
 }
 
+// ---------------------------------------------------------------------------
+// TN reduction GEMM, D = 256, LDS-DMA double-buffered: the next 32-row tile of A
+// and B (64 one-KiB rows) is DMA'd while the 8 waves run the current tile's
+// 16 x 8 MFMAs; rows past the block's range are zero-filled with plain LDS stores.
+// ---------------------------------------------------------------------------
+namespace tn256 {
+constexpr int D = 256, TK = 32, TILE = TK * D;          // floats per operand tile
+}
+
+__global__ __launch_bounds__(512) void gemm_tn256_dma_kernel(long long M, long long rows_per_block,
+                                                             const float* __restrict__ A,
+                                                             const float* __restrict__ B,
+                                                             float* __restrict__ slab) {
+    using namespace tn256;
+    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * TILE];    // [buf][A|B][TK][D]
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int i = lane & 31, h = lane >> 5;
+
+    f32x16 acc[8];
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[cj][j] = 0.f;
+
+    const long long r_beg = (long long)blockIdx.x * rows_per_block;
+    long long r_end = r_beg + rows_per_block;
+    if (r_end > M) r_end = M;
+    const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
+
+    // wave w stages rows 4w..4w+3 of both operands
+    auto stage = [&](long long t, int b) {
+        float* As = lds + (b * 2 + 0) * TILE;
+        float* Bs = lds + (b * 2 + 1) * TILE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = wave * 4 + j;
+            const long long e = r_beg + t * TK + r;
+            if (e < r_end) {
+                dma_row_1k(A + e * D, As + r * D, lane);
+                dma_row_1k(B + e * D, Bs + r * D, lane);
+            } else {
+                st4(As + r * D + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                st4(Bs + r * D + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+            }
+        }
+    };
+
+    if (nt > 0) {
+        stage(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    int b = 0;
+    for (long long t = 0; t < nt; ++t, b ^= 1) {
+        if (t + 1 < nt) stage(t + 1, b ^ 1);
+        const float* As = lds + (b * 2 + 0) * TILE;
+        const float* Bs = lds + (b * 2 + 1) * TILE;
+#pragma unroll
+        for (int s = 0; s < TK / 2; ++s) {
+            const float a = As[(2 * s + h) * D + 32 * wave + i];
+#pragma unroll
+            for (int cj = 0; cj < 8; ++cj) {
+                const float bv = Bs[(2 * s + h) * D + 32 * cj + i];
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[cj], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    float* out = slab + (long long)blockIdx.x * D * D;
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int row = 32 * wave + (j & 3) + 8 * (j >> 2) + 4 * h;
+            out[row * D + 32 * cj + i] = acc[cj][j];
+        }
+}
+
 // out[D][R] partial of A^T dz and colsum(dz) per block; slab row layout [(D+1)][R]
 template <int D>
 __global__ __launch_bounds__(D) void gemm_tn_narrow_kernel(long long M, long long rows_per_block, int R,
@@ -697,10 +777,14 @@ __global__ __launch_bounds__(256) void seg_gather_reduce_kernel(int n_nodes, con
 }
 
 // ---------------------------------------------------------------------------
-// tail-side layer backward over tail-sorted contiguous segments
+// tail-side layer backward over tail-sorted contiguous segments.
+// One node per group of D/4 lanes; the node's edges are contiguous rows of dO,
+// walked 4 at a time with all 4 row loads (and their W[h] loads) issued before
+// any use, so each wave keeps 4 KiB in flight.  R is a template parameter so
+// the per-relation state stays in a handful of registers (occupancy 8).
 // ---------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, int R, const int* __restrict__ seg_ptr,
+template <int D, int R>
+__global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const int* __restrict__ seg_ptr,
                                                               const int* __restrict__ h_idx,
                                                               const float* __restrict__ W,
                                                               const float* __restrict__ dO,
@@ -708,49 +792,66 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, int R
                                                               float* __restrict__ dP, long long dp_rel_stride,
                                                               float* __restrict__ dsum, float* __restrict__ dWedge) {
     constexpr int LPR = D / 4;
+    constexpr int U = 4;
     const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
     const int sub = threadIdx.x % LPR;
     const bool live = n < n_nodes;
     const int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
-    f32x4 pr[MAX_R], acc[MAX_R];
+    f32x4 pr[R], acc[R];
 #pragma unroll
-    for (int r = 0; r < MAX_R; ++r) {
+    for (int r = 0; r < R; ++r) {
         acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-        pr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (live && r < R) pr[r] = ld4(P + r * p_rel_stride + n * D + sub * 4);
+        pr[r] = live ? ld4(P + r * p_rel_stride + n * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-    // every lane of a group iterates the same segment; groups of one wave may differ,
-    // so the shuffles below run under a wave-uniform trip count.
-    int len = end - beg;
+    const int len = end - beg;
+    // groups of one wave may hold different nodes (D < 256): trip count must be wave-uniform
     int maxlen = len;
+    if (LPR < 64) {
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, m, 64));
-    for (int k = 0; k < maxlen; ++k) {
-        const bool act = k < len;
-        const long long e = (long long)beg + k;
-        f32x4 d = {0.f, 0.f, 0.f, 0.f};
-        int hh = 0;
-        if (act) {
-            d = ld4(dO + e * D + sub * 4);
-            hh = h_idx[e];
+        for (int m = 32; m >= LPR; m >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, m, 64));
+    }
+    for (int k = 0; k < maxlen; k += U) {
+        f32x4 d[U];
+        int hh[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool a = k + u < len;
+            hh[u] = a ? h_idx[beg + k + u] : 0;
+            d[u] = a ? ld4(dO + (long long)(beg + k + u) * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        s4 += d;
+        float w[U][R];
 #pragma unroll
-        for (int r = 0; r < MAX_R; ++r) {
-            if (r < R) {
-                const float w = act ? W[(long long)hh * R + r] : 0.f;
-                acc[r] += w * d;
-                const f32x4 q = d * pr[r];
-                const float dw = group_sum<LPR>(q[0] + q[1] + q[2] + q[3]);
-                if (act && sub == 0) dWedge[e * R + r] = dw;
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int r = 0; r < R; ++r) w[u][r] = (k + u < len) ? W[(long long)hh[u] * R + r] : 0.f;
+        float dw[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            s4 += d[u];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                acc[r] += w[u][r] * d[u];
+                const f32x4 q = d[u] * pr[r];
+                dw[u][r] = q[0] + q[1] + q[2] + q[3];
             }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int r = 0; r < R; ++r) dw[u][r] = group_sum<LPR>(dw[u][r]);
+        if (sub == 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (k + u < len) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) dWedge[(long long)(beg + k + u) * R + r] = dw[u][r];
+                }
         }
     }
     if (!live) return;
 #pragma unroll
-    for (int r = 0; r < MAX_R; ++r)
-        if (r < R) st4(dP + r * dp_rel_stride + n * D + sub * 4, acc[r]);
+    for (int r = 0; r < R; ++r) st4(dP + r * dp_rel_stride + n * D + sub * 4, acc[r]);
     if (dsum) st4(dsum + n * D + sub * 4, s4);
 }
 
@@ -947,7 +1048,9 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
-    switch (d) {
+    if (d == 256 && !g_force_v1) {
+        hipLaunchKernelGGL(gemm_tn256_dma_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
+    } else switch (d) {
         case 32: TNK(32); break;
         case 64: TNK(64); break;
         case 128: TNK(128); break;
@@ -1095,13 +1198,25 @@ int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const in
     if (n_nodes == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     const unsigned grid = grid_for(n_nodes, d / 4);
-#define TK(DD) hipLaunchKernelGGL(tail_seg_reduce_kernel<DD>, dim3(grid), dim3(256), 0, st, n_nodes, R, seg_ptr, h_idx, W, dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge)
-    switch (d) {
-        case 32: TK(32); break;
-        case 64: TK(64); break;
-        case 128: TK(128); break;
-        default: TK(256); break;
+#define TK(DD, RR) hipLaunchKernelGGL((tail_seg_reduce_kernel<DD, RR>), dim3(grid), dim3(256), 0, st, n_nodes, seg_ptr, h_idx, W, dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge)
+#define TKR(DD)                \
+    switch (R) {               \
+        case 1: TK(DD, 1); break; \
+        case 2: TK(DD, 2); break; \
+        case 3: TK(DD, 3); break; \
+        case 4: TK(DD, 4); break; \
+        case 5: TK(DD, 5); break; \
+        case 6: TK(DD, 6); break; \
+        case 7: TK(DD, 7); break; \
+        default: TK(DD, 8); break; \
     }
+    switch (d) {
+        case 32: TKR(32); break;
+        case 64: TKR(64); break;
+        case 128: TKR(128); break;
+        default: TKR(256); break;
+    }
+#undef TKR
 #undef TK
     return launch_status();
 }

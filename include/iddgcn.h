@@ -68,7 +68,7 @@ typedef struct {
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 
-/* Select the D=256 row-GEMM pipeline: 0 (default) = LDS-DMA pipelined kernel where
+/* Select the D=256 row-GEMM and TN-GEMM pipelines: 0 (default) = LDS-DMA pipelined kernels where
  * applicable, 1 = register-staged kernel everywhere.  Host-side switch for A/B
  * tests and benchmarks; returns the previous setting. */
 int iddgcn_set_rowgemm_path(int force_register_staged);

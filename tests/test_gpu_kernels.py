@@ -325,3 +325,24 @@ def test_rowgemm_dma_path_bitwise_equals_register_path(mode, cuda):
         finally:
             L.lib().iddgcn_set_rowgemm_path(old)
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("M", [31, 5003, 300_017])
+def test_gemm_tn_dma_path_bitwise_equals_register_path(M, cuda):
+    """D=256 LDS-DMA TN kernel == register-staged TN kernel, bit for bit (same MFMA order,
+    zero-filled partial tiles)."""
+    g = torch.Generator().manual_seed(M)
+    D = 256
+    A, B = torch.randn(M, D, generator=g).to(cuda), torch.randn(M, D, generator=g).to(cuda)
+    slab = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
+    out = []
+    for force in (0, 1):
+        old = L.lib().iddgcn_set_rowgemm_path(force)
+        try:
+            C = torch.empty(D, D, device=cuda)
+            ops.gemm_tn(A, B, C, slab)
+            out.append(C)
+        finally:
+            L.lib().iddgcn_set_rowgemm_path(old)
+    assert torch.equal(out[0], out[1])
+    close(out[0], A.double().t() @ B.double(), 2e-6 * np.sqrt(M))
