@@ -26,6 +26,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 namespace {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// layer activations: v_exp_f32 + v_rcp_f32 (~2 ulp; saturates to exactly 0 / 1 like the accurate form)
+__device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 template <int LPR>
 __device__ __forceinline__ float group_sum(float v) {
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmP p) {
                 for (int r = 0; r < p.R; ++r) v += p.coef[ci * p.R + r] * vb[r * p.v_rel_stride];
             }
             if (p.act == IDDGCN_ACT_SIGMOID) {
-                v = sigmoidf_(v);
+                v = sigmoid_fast(v);
             } else if (p.act == IDDGCN_ACT_DSIGMOID) {
                 const float x = p.aux[e * D + c];
                 v = v * (x * (1.0f - x));
@@ -370,7 +372,7 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
                 for (int r = 0; r < R; ++r) v += coefL[row * MAX_R + r] * p.V[r * p.v_rel_stride + c];
             }
             if (p.act == IDDGCN_ACT_SIGMOID) {
-                v = sigmoidf_(v);
+                v = sigmoid_fast(v);
             } else if (p.act == IDDGCN_ACT_DSIGMOID) {
                 const float x = epi[row * LDA + c];
                 v = v * (x * (1.0f - x));
@@ -669,7 +671,7 @@ __global__ __launch_bounds__(256) void combine_kernel(int M, int R, const float*
         v += w * pv;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = sigmoidf_(v[j]);
+    for (int j = 0; j < 4; ++j) v[j] = sigmoid_fast(v[j]);
     st4(out + e * D + sub * 4, v);
 }
 
@@ -697,34 +699,61 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
     for (int r = 0; r < MAX_R; ++r) dr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
     float lacc = 0.f;
 
-    for (long long e = (long long)blockIdx.x * GROUPS + grp; e < T; e += (long long)gridDim.x * GROUPS) {
-        const int hr = h_idx[e];
-        const int rr = r_idx[e];
-        const long long ti = t_idx ? (long long)t_idx[e] : e;
-        const f32x4 a = ld4(Xh + (long long)hr * D + sub * 4);
-        const f32x4 b = ld4(Xt + ti * D + sub * 4);
-        const f32x4 rho = ld4(rel + (long long)rr * D + sub * 4);
-        const f32x4 prod = a * rho * b;
-        const float s = group_sum<LPR>(prod[0] + prod[1] + prod[2] + prod[3]);
-        const float p = sigmoidf_(s);
-        if (p_out && sub == 0) p_out[e] = p;
-        if (!train) continue;
-        const float yy = y[e];
-        const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
-        const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
-        const float g = pass ? scale * (-(yy / (pc + EPS_BCE)) + (1.0f - yy) / (1.0f - pc + EPS_BCE)) : 0.f;
-        const float ds = g * p * (1.0f - p);
-        if (sub == 0) {
-            ds_out[e] = ds;
-            lacc += -(yy * logf(pc + EPS_BCE) + (1.0f - yy) * logf(1.0f - pc + EPS_BCE));
-        }
-        f32x4 dx = (ds * rho) * a;
-        dx = dx * (b * (1.0f - b));
-        st4(do_out + e * D + sub * 4, dx);
-        const f32x4 dre = ds * (a * b);
+    // two rows per group per iteration, all loads issued before any use (same visit order as a
+    // plain grid-stride loop, so the drel / loss partial sums are order-identical)
+    constexpr int U = 2;
+    const long long stride = (long long)gridDim.x * GROUPS;
+    for (long long e0 = (long long)blockIdx.x * GROUPS + grp; e0 < T; e0 += U * stride) {
+        long long e[U];
+        int hr[U], rr[U];
+        long long ti[U];
 #pragma unroll
-        for (int r = 0; r < MAX_R; ++r)
-            if (r == rr) dr[r] += dre;
+        for (int u = 0; u < U; ++u) {
+            e[u] = e0 + u * stride;
+            const bool ok = e[u] < T;
+            hr[u] = ok ? h_idx[e[u]] : 0;
+            rr[u] = ok ? r_idx[e[u]] : 0;
+            ti[u] = ok ? (t_idx ? (long long)t_idx[e[u]] : e[u]) : 0;
+        }
+        f32x4 a[U], b[U], rho[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = ld4(Xh + (long long)hr[u] * D + sub * 4);
+            b[u] = ld4(Xt + ti[u] * D + sub * 4);
+            rho[u] = ld4(rel + (long long)rr[u] * D + sub * 4);
+        }
+        float yy[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) yy[u] = (train && e[u] < T) ? y[e[u]] : 0.f;
+        float sc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const f32x4 prod = a[u] * rho[u] * b[u];
+            sc[u] = group_sum<LPR>(prod[0] + prod[1] + prod[2] + prod[3]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (e[u] >= T) continue;
+            const float p = sigmoidf_(sc[u]);
+            if (p_out && sub == 0) p_out[e[u]] = p;
+            if (!train) continue;
+            const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
+            const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
+            const float g =
+                pass ? scale * (-(yy[u] / (pc + EPS_BCE)) + (1.0f - yy[u]) / (1.0f - pc + EPS_BCE)) : 0.f;
+            const float ds = g * p * (1.0f - p);
+            if (sub == 0) {
+                ds_out[e[u]] = ds;
+                lacc += -(yy[u] * logf(pc + EPS_BCE) + (1.0f - yy[u]) * logf(1.0f - pc + EPS_BCE));
+            }
+            f32x4 dx = (ds * rho[u]) * a[u];
+            dx = dx * (b[u] * (1.0f - b[u]));
+            st4(do_out + e[u] * D + sub * 4, dx);
+            const f32x4 dre = ds * (a[u] * b[u]);
+#pragma unroll
+            for (int r = 0; r < MAX_R; ++r)
+                if (r == rr[u]) dr[r] += dre;
+        }
     }
     if (!train) return;
 #pragma unroll
@@ -762,12 +791,22 @@ __global__ __launch_bounds__(256) void seg_gather_reduce_kernel(int n_nodes, con
     if (n >= n_nodes) return;
     const int beg = seg_ptr[n], end = seg_ptr[n + 1];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k = beg; k < end; ++k) {
-        const long long e = perm ? (long long)perm[k] : (long long)k;
-        f32x4 v = ld4(rows + e * D + sub * 4);
-        if (coef) v *= coef[e];
-        if (rel) v *= ld4(rel + (long long)r_idx[e] * D + sub * 4);
-        acc += v;
+    constexpr int U = 4;
+    for (int k0 = beg; k0 < end; k0 += U) {
+        long long e[U];
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) e[u] = (k0 + u < end) ? (perm ? (long long)perm[k0 + u] : (long long)(k0 + u)) : -1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (e[u] < 0) continue;
+            v[u] = ld4(rows + e[u] * D + sub * 4);
+            if (coef) v[u] *= coef[e[u]];
+            if (rel) v[u] *= ld4(rel + (long long)r_idx[e[u]] * D + sub * 4);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (e[u] >= 0) acc += v[u];
     }
     if (X) {
         const f32x4 x = ld4(X + n * D + sub * 4);
@@ -925,6 +964,7 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(int n_slabs, long lon
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float s = 0.f;
+#pragma unroll 8
     for (int b = 0; b < n_slabs; ++b) s += slab[(long long)b * n + i];
     s *= scale;
     out[i] = accumulate ? out[i] + s : s;
