@@ -44,8 +44,9 @@ inline int launch_status() {
     return e == hipSuccess ? 0 : (int)e;
 }
 inline bool dim_ok(int d) { return d == 32 || d == 64 || d == 128 || d == 256; }
-// test hook: force the register-staged rowgemm (A/B comparisons of the two D=256 paths)
-static int g_force_v1 = 0;
+// test/bench hook selecting the D=256 GEMM pipelines: 0 = best (v3 row GEMM, DMA TN),
+// 1 = register-staged kernels, 2 = v2 DMA row GEMM
+static int g_rowgemm_path = 0;
 
 // ---------------------------------------------------------------------------
 // CSR SpMM: one row per group of D/4 lanes, sequential sum in CSR order.
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmP p) {
                 const long long ci = p.coef_idx ? (long long)p.coef_idx[e] : e;
                 const long long vi = p.v_idx ? (long long)p.v_idx[e] : e;
                 const float* vb = p.V + vi * p.v_row_stride + c;
-                for (int r = 0; r < p.R; ++r) v += p.coef[ci * p.R + r] * vb[r * p.v_rel_stride];
+                for (int r = 0; r < p.R; ++r) v = fmaf(p.coef[ci * p.R + r], vb[r * p.v_rel_stride], v);
             }
             if (p.act == IDDGCN_ACT_SIGMOID) {
                 v = sigmoid_fast(v);
@@ -367,9 +368,9 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
             float* cp = p.C + e * D + c;
             if (p.accumulate) v += *cp;
             if (gatherV) {
-                for (int r = 0; r < R; ++r) v += coefL[row * MAX_R + r] * epi[(r * TR + row) * LDA + c];
+                for (int r = 0; r < R; ++r) v = fmaf(coefL[row * MAX_R + r], epi[(r * TR + row) * LDA + c], v);
             } else if (R > 0) {        // broadcast V (v_row_stride == 0): tiny, cache-resident
-                for (int r = 0; r < R; ++r) v += coefL[row * MAX_R + r] * p.V[r * p.v_rel_stride + c];
+                for (int r = 0; r < R; ++r) v = fmaf(coefL[row * MAX_R + r], p.V[r * p.v_rel_stride + c], v);
             }
             if (p.act == IDDGCN_ACT_SIGMOID) {
                 v = sigmoid_fast(v);
@@ -382,6 +383,222 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
         // (11) epilogue buffers free for the next tile
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------
+// Row GEMM, D = 256, v3: staggered waves, wave-private epilogue slabs.
+//   * A tiles: LDS-DMA double buffer, rows unpadded and XOR-swizzled (float4 slot
+//     s of row r holds logical slot s ^ (r & 15)); the DMA writes lane-linearly
+//     and the swizzle is applied on the per-lane SOURCE address, so the
+//     ds_read_b128 fragment reads stay conflict-free without padding.
+//   * Epilogue operands: each wave DMAs only the 32 columns it owns (gathered
+//     P_r[t] rows and/or sigma' aux rows, 32 rows x 32 cols = 4 KiB per slab) plus
+//     its per-row coefficients into a private LDS region.  Producer == consumer,
+//     so these need no barrier, only the wave's own vmcnt.
+//   * Stagger: waves 4-7 (one partner per SIMD) run the epilogue of tile t-1 at
+//     the top of iteration t, while waves 0-3 run tile t's epilogue after its
+//     MFMAs: each SIMD overlaps one wave's epilogue VALU with its partner's
+//     MFMAs.  One barrier per tile (A buffers), raw s_barrier so the slab DMA of
+//     the next tile stays in flight across it.
+// ---------------------------------------------------------------------------
+#ifndef V3_STAGGER
+#define V3_STAGGER 1
+#endif
+namespace r3 {
+constexpr int D = 256, NW = 8, TR = 32;
+constexpr int ROWS_PER_WAVE = TR / NW;                 // A rows each wave stages
+constexpr int A_FLOATS = TR * D;                       // 32 KiB
+constexpr int SLAB = TR * 32;                          // 32 rows x 32 cols
+constexpr int NS_MAX = 2;
+constexpr int COEF = 64;                               // 32 rows x R (R <= 2)
+constexpr int IDX = 64;                                // next tile's v_idx (32) + coef_idx (32)
+constexpr int WAVE_FLOATS = NS_MAX * SLAB + COEF + IDX;
+constexpr int LDS_FLOATS = 2 * A_FLOATS + NW * WAVE_FLOATS;   // 130 KiB
+}  // namespace r3
+
+template <int NV, bool AUX, bool HAS_COEF>
+__global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
+    using namespace r3;
+    constexpr int NS = NV + (AUX ? 1 : 0);
+    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool late = V3_STAGGER && wave >= 4;         // staggered half
+    const int i = lane & 31, h = lane >> 5;
+    const int c0 = wave * 32;
+    float* bufA = lds;
+    float* slabw = lds + 2 * A_FLOATS + wave * WAVE_FLOATS;   // [NS][32][32]
+    float* coefw = slabw + NS_MAX * SLAB;                     // [32][R]
+    const int R = p.R;
+
+    float breg[D / 2];
+#pragma unroll
+    for (int s = 0; s < D / 2; ++s) {
+        const int kk = 8 * (s >> 2) + 4 * h + (s & 3);
+        breg[s] = p.b_trans ? p.B[(c0 + i) * D + kk] : p.B[kk * D + c0 + i];
+    }
+
+    const long long ntiles = ((long long)p.M + TR - 1) / TR;
+    const long long t_beg = (long long)blockIdx.x * p.tiles_per_block;
+    long long t_end = t_beg + p.tiles_per_block;
+    if (t_end > ntiles) t_end = ntiles;
+    if (t_beg >= t_end) return;
+    const long long Mlast = (long long)p.M - 1;
+    auto clampe = [&](long long e) { return e > Mlast ? Mlast : e; };
+
+    // ---- row indices of the next tile: DMA'd into a wave-private LDS slot -------------
+    int* idxw = reinterpret_cast<int*>(coefw + r3::COEF);      // [0,32) v_idx, [32,64) coef_idx
+    const bool need_idx = (NV > 0 && p.v_idx) || (HAS_COEF && p.coef_idx);
+    auto dma_idx = [&](long long t) {
+        if (!need_idx || t >= t_end) return;
+        const int* g = p.v_idx ? p.v_idx : p.coef_idx;          // valid dummy for unused lanes
+        if (lane < 32) {
+            if (NV > 0 && p.v_idx) g = p.v_idx + clampe(t * TR + lane);
+        } else if (HAS_COEF && p.coef_idx) {
+            g = p.coef_idx + clampe(t * TR + lane - 32);
+        }
+        __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)idxw, 4, 0, 0);
+    };
+    // A-row gather indices: lanes 0..3 hold this wave's 4 rows; SGPR copies sa[]
+    auto load_aidx = [&](long long t) -> int {
+        if (!p.a_idx || lane >= ROWS_PER_WAVE || t >= t_end) return 0;
+        return p.a_idx[clampe(t * TR + wave * ROWS_PER_WAVE + lane)];
+    };
+    int sa[ROWS_PER_WAVE];
+    auto to_sgpr = [&](int v) {
+#pragma unroll
+        for (int j = 0; j < ROWS_PER_WAVE; ++j) sa[j] = __builtin_amdgcn_readlane(v, j);
+    };
+
+    auto dma_A = [&](long long t, int b) {
+#pragma unroll
+        for (int j = 0; j < ROWS_PER_WAVE; ++j) {
+            const int r = wave * ROWS_PER_WAVE + j;
+            const long long e = clampe(t * TR + r);
+            const long long src = p.a_idx ? (long long)sa[j] : e;
+            const float* g = p.A + src * D + ((lane ^ (r & 15)) * 4);
+            __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * D), 16, 0, 0);
+        }
+    };
+    auto dma_slabs = [&](long long t) {
+        if (NV > 0) {
+#pragma unroll
+            for (int r = 0; r < NV; ++r)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const long long e = clampe(t * TR + 8 * k + (lane >> 3));
+                    const long long vi = p.v_idx ? (long long)idxw[8 * k + (lane >> 3)] : e;
+                    const float* g = p.V + r * p.v_rel_stride + vi * D + c0 + (lane & 7) * 4;
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(slabw + r * SLAB + k * 256), 16, 0, 0);
+                }
+        }
+        if (AUX) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const long long e = clampe(t * TR + 8 * k + (lane >> 3));
+                const float* g = p.aux + e * D + c0 + (lane & 7) * 4;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(slabw + NV * SLAB + k * 256), 16, 0, 0);
+            }
+        }
+        if (HAS_COEF) {
+            const float* g = p.coef;             // lanes past 32*R read a valid dummy
+            if (lane < TR * R) {
+                const int row = lane / R, r = lane % R;
+                const long long ci = p.coef_idx ? (long long)idxw[32 + row] : clampe(t * TR + row);
+                g = p.coef + ci * R + r;
+            }
+            __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)coefw, 4, 0, 0);
+        }
+    };
+
+    const int c = c0 + i;
+    auto epilogue = [&](long long t, const f32x16& acc) {
+        const long long row0 = t * TR;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const long long e = row0 + row;
+            if (e >= p.M) continue;
+            float v = acc[reg];
+            float* cp = p.C + e * D + c;
+            if (p.accumulate) v += *cp;
+            if (NV > 0) {
+#pragma unroll
+                for (int r = 0; r < NV; ++r) v = fmaf(coefw[row * NV + r], slabw[r * SLAB + row * 32 + i], v);
+            } else if (HAS_COEF) {      // broadcast V rows (v_row_stride == 0): tiny, cache-resident
+                for (int r = 0; r < R; ++r) v = fmaf(coefw[row * R + r], p.V[r * p.v_rel_stride + c], v);
+            }
+            if (p.act == IDDGCN_ACT_SIGMOID) {
+                v = sigmoid_fast(v);
+            } else if (p.act == IDDGCN_ACT_DSIGMOID) {
+                const float x = slabw[NV * SLAB + row * 32 + i];
+                v = v * (x * (1.0f - x));
+            }
+            *cp = v;
+        }
+    };
+
+    // ---- prologue ---------------------------------------------------------------------
+    {
+        const int a0 = load_aidx(t_beg);
+        dma_idx(t_beg);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        to_sgpr(a0);
+        dma_A(t_beg, 0);
+        const int a1 = load_aidx(t_beg + 1);
+        if (!late) {
+            dma_slabs(t_beg);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            dma_idx(t_beg + 1);                    // group 0 consumes tile t_beg's indices here
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        to_sgpr(a1);
+        __syncthreads();
+    }
+
+    f32x16 acc;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    int b = 0;
+    for (long long t = t_beg; t < t_end; ++t, b ^= 1) {
+        if (late) {
+            if (t > t_beg) epilogue(t - 1, acc);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // epilogue LDS reads done before overwrite
+            dma_slabs(t);                                          // reads idx(t) from the slot
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            dma_idx(t + 1);                                        // slot now free for idx(t+1)
+        }
+        if (t + 1 < t_end) dma_A(t + 1, b ^ 1);
+        const int an = load_aidx(t + 2);
+
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+        const float* arow = bufA + b * A_FLOATS + i * D;
+        const int sw = i & 15;
+#pragma unroll
+        for (int q = 0; q < D / 8; ++q) {
+            const f32x4 a4 = ld4(arow + (((2 * q + h) ^ sw) * 4));
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[0], breg[4 * q + 0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[1], breg[4 * q + 1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[2], breg[4 * q + 2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[3], breg[4 * q + 3], acc, 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // A(t+1), indices, own slabs landed
+        if (!late) {
+            epilogue(t, acc);
+            if (t + 1 < t_end) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                dma_slabs(t + 1);                                     // in flight across the barrier
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                dma_idx(t + 2);
+            }
+        }
+        to_sgpr(an);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");                             // no LDS access crosses the barrier
+    }
+    if (late) epilogue(t_end - 1, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1003,9 +1220,9 @@ extern "C" {
 
 int iddgcn_abi_version(void) { return IDDGCN_ABI_VERSION; }
 
-int iddgcn_set_rowgemm_path(int force_register_staged) {
-    const int old = g_force_v1;
-    g_force_v1 = force_register_staged ? 1 : 0;
+int iddgcn_set_rowgemm_path(int path) {
+    const int old = g_rowgemm_path;
+    g_rowgemm_path = (path < 0 || path > 2) ? 0 : path;
     return old;
 }
 
@@ -1051,9 +1268,27 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
         hipLaunchKernelGGL(rowgemm_kernel<DD>, dim3((unsigned)nb), dim3(RG<DD>::NW * 64), 0, st, p); \
     }
     const bool gatherV = p.R > 0 && p.v_row_stride != 0;
-    const int epi_rows = gatherV ? p.R : (p.act == IDDGCN_ACT_DSIGMOID ? 1 : 0);
-    const bool dma_ok = a->D == 256 && epi_rows <= r256::EPI_MAX && !(gatherV && p.act == IDDGCN_ACT_DSIGMOID) &&
-                        (!gatherV || p.v_row_stride == 256) && !g_force_v1;
+    const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
+    // v3 (staggered, wave-private slabs): D=256, R <= 2
+    const bool v3_ok = a->D == 256 && p.R <= 2 && !(gatherV && dsig) && (!gatherV || p.v_row_stride == 256) &&
+                       g_rowgemm_path == 0;
+    if (v3_ok) {
+        const long long nt = ((long long)p.M + r3::TR - 1) / r3::TR;
+        long long nb = nt < 256 ? nt : 256;
+        p.tiles_per_block = (int)((nt + nb - 1) / nb);
+        nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
+        const dim3 g((unsigned)nb), blk(512);
+        if (gatherV && p.R == 1) hipLaunchKernelGGL((rowgemm256_v3_kernel<1, false, true>), g, blk, 0, st, p);
+        else if (gatherV) hipLaunchKernelGGL((rowgemm256_v3_kernel<2, false, true>), g, blk, 0, st, p);
+        else if (p.R > 0 && dsig) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, true, true>), g, blk, 0, st, p);
+        else if (p.R > 0) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, false, true>), g, blk, 0, st, p);
+        else if (dsig) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, true, false>), g, blk, 0, st, p);
+        else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, false, false>), g, blk, 0, st, p);
+        return launch_status();
+    }
+    const int epi_rows = gatherV ? p.R : (dsig ? 1 : 0);
+    const bool dma_ok = a->D == 256 && epi_rows <= r256::EPI_MAX && !(gatherV && dsig) &&
+                        (!gatherV || p.v_row_stride == 256) && g_rowgemm_path != 1;
     if (dma_ok) {
         const long long nt = ((long long)p.M + r256::TR - 1) / r256::TR;
         long long nb = nt < 256 ? nt : 256;
@@ -1088,7 +1323,7 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
-    if (d == 256 && !g_force_v1) {
+    if (d == 256 && g_rowgemm_path != 1) {
         hipLaunchKernelGGL(gemm_tn256_dma_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
     } else switch (d) {
         case 32: TNK(32); break;

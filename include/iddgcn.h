@@ -68,10 +68,10 @@ typedef struct {
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 
-/* Select the D=256 row-GEMM and TN-GEMM pipelines: 0 (default) = LDS-DMA pipelined kernels where
- * applicable, 1 = register-staged kernel everywhere.  Host-side switch for A/B
- * tests and benchmarks; returns the previous setting. */
-int iddgcn_set_rowgemm_path(int force_register_staged);
+/* Select the D=256 GEMM pipelines (host-side switch for A/B tests and benchmarks;
+ * all paths are bitwise identical): 0 (default) = staggered v3 row GEMM + LDS-DMA TN GEMM,
+ * 1 = register-staged kernels, 2 = v2 LDS-DMA row GEMM.  Returns the previous setting. */
+int iddgcn_set_rowgemm_path(int path);
 
 /* C[D][D] (+)= A^T · B over M rows (A, B are M x D).  Two stages: each of n_blocks
  * workgroups writes a D x D partial into `slab` (n_blocks*D*D floats), then the

@@ -292,16 +292,17 @@ def test_adam_kernel_matches_keras_forms(cuda):
         close(var2, vd - alpha * mr / (vr.sqrt() + eps), 1e-6)
 
 
-@pytest.mark.parametrize("mode", ["plain", "combine", "dsig", "rank_bcast", "accumulate", "gatherA"])
+@pytest.mark.parametrize("mode", ["plain", "combine", "combine_r1", "dsig", "rank_bcast", "rank_bcast_nodsig",
+                                  "accumulate", "gatherA", "small_M"])
 def test_rowgemm_dma_path_bitwise_equals_register_path(mode, cuda):
     """D=256 LDS-DMA pipelined kernel == register-staged kernel, bit for bit (same MFMA chain,
     same epilogue order), including a ragged last tile and multi-tile persistent blocks."""
     g = torch.Generator().manual_seed(43)
-    D, N, M, R = 256, 700, 40_000 + 17, 2
+    D, N, M, R = 256, 700, (77 if mode == "small_M" else 40_000 + 17), (1 if mode == "combine_r1" else 2)
     A = torch.randn(M, D, generator=g).to(cuda)
     S = (torch.randn(D, D, generator=g) / 16).to(cuda)
     kw = {}
-    if mode == "combine":
+    if mode in ("combine", "combine_r1"):
         kw = dict(coef=torch.rand(N, R, generator=g).to(cuda), coef_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
                   V=torch.randn(R, N, D, generator=g).to(cuda), v_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
                   v_rel_stride=N * D, act=L.ACT_SIGMOID)
@@ -310,13 +311,16 @@ def test_rowgemm_dma_path_bitwise_equals_register_path(mode, cuda):
     elif mode == "rank_bcast":
         kw = dict(b_trans=True, coef=torch.randn(M, R, generator=g).to(cuda), V=torch.randn(R, D, generator=g).to(cuda),
                   v_rel_stride=D, v_row_stride=0, act=L.ACT_DSIGMOID, aux=torch.rand(M, D, generator=g).to(cuda))
+    elif mode == "rank_bcast_nodsig":
+        kw = dict(b_trans=True, coef=torch.randn(M, R, generator=g).to(cuda), V=torch.randn(R, D, generator=g).to(cuda),
+                  v_rel_stride=D, v_row_stride=0)
     elif mode == "accumulate":
         kw = dict(accumulate=True, b_trans=True)
     elif mode == "gatherA":
         kw = dict(a_idx=torch.randint(0, M, (M,), generator=g).int().to(cuda))
     C0 = torch.randn(M, D, generator=g).to(cuda)
     out = []
-    for force in (0, 1):
+    for force in (0, 1, 2):
         old = L.lib().iddgcn_set_rowgemm_path(force)
         try:
             C = C0.clone()
@@ -325,6 +329,7 @@ def test_rowgemm_dma_path_bitwise_equals_register_path(mode, cuda):
         finally:
             L.lib().iddgcn_set_rowgemm_path(old)
     assert torch.equal(out[0], out[1])
+    assert torch.equal(out[0], out[2])
 
 
 @pytest.mark.parametrize("M", [31, 5003, 300_017])
