@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/iddgcn.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -34,6 +36,35 @@ __device__ __forceinline__ float group_sum(float v) {
 #pragma unroll
     for (int m = LPR / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
     return v;
+}
+
+// Reduce K values (K a power of two, K <= LPR) over an aligned group of LPR lanes with a
+// butterfly that halves the value set at each level: K-1 + log2(LPR/K) ... shuffles instead of
+// K*log2(LPR).  On return v[0] holds, in every lane, the full sum of value index
+// sub / (LPR/K).  Pairwise adds happen in the same order as group_sum (bitwise identical).
+template <int LPR, int K>
+__device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
+    static_assert((K & (K - 1)) == 0 && K <= LPR, "K must be a power of two <= LPR");
+    int kc = K;
+#pragma unroll
+    for (int m = LPR / 2; m >= 1; m >>= 1) {
+        if (kc > 1) {
+            const bool up = (sub & m) != 0;
+            const int half = kc / 2;
+#pragma unroll
+            for (int j = 0; j < K / 2; ++j) {
+                if (j < half) {
+                    const float keep = up ? v[half + j] : v[j];
+                    const float send = up ? v[j] : v[half + j];
+                    v[j] = keep + __shfl_xor(send, m, 64);
+                }
+            }
+            kc = half;
+        } else {
+            v[0] += __shfl_xor(v[0], m, 64);
+        }
+    }
+    return v[0];
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
@@ -387,10 +418,9 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
 
 // ---------------------------------------------------------------------------
 // Row GEMM, D = 256, v3: staggered waves, wave-private epilogue slabs.
-//   * A tiles: LDS-DMA double buffer, rows unpadded and XOR-swizzled (float4 slot
-//     s of row r holds logical slot s ^ (r & 15)); the DMA writes lane-linearly
-//     and the swizzle is applied on the per-lane SOURCE address, so the
-//     ds_read_b128 fragment reads stay conflict-free without padding.
+//   * A tiles: LDS-DMA double buffer, 1040-B padded rows (one 1 KiB DMA
+//     wave-instruction per row, so padding between rows is allowed): conflict-free
+//     ds_read_b128 fragment reads at one base register + immediate offsets.
 //   * Epilogue operands: each wave DMAs only the 32 columns it owns (gathered
 //     P_r[t] rows and/or sigma' aux rows, 32 rows x 32 cols = 4 KiB per slab) plus
 //     its per-row coefficients into a private LDS region.  Producer == consumer,
@@ -404,10 +434,14 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
 #ifndef V3_STAGGER
 #define V3_STAGGER 1
 #endif
+#ifndef V3_PRIO
+#define V3_PRIO 0
+#endif
 namespace r3 {
 constexpr int D = 256, NW = 8, TR = 32;
 constexpr int ROWS_PER_WAVE = TR / NW;                 // A rows each wave stages
-constexpr int A_FLOATS = TR * D;                       // 32 KiB
+constexpr int LDA = D + 4;                             // padded rows: conflict-free ds_read_b128
+constexpr int A_FLOATS = TR * LDA;                     // 33,280 B
 constexpr int SLAB = TR * 32;                          // 32 rows x 32 cols
 constexpr int NS_MAX = 2;
 constexpr int COEF = 64;                               // 32 rows x R (R <= 2)
@@ -476,8 +510,8 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             const int r = wave * ROWS_PER_WAVE + j;
             const long long e = clampe(t * TR + r);
             const long long src = p.a_idx ? (long long)sa[j] : e;
-            const float* g = p.A + src * D + ((lane ^ (r & 15)) * 4);
-            __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * D), 16, 0, 0);
+            const float* g = p.A + src * D + lane * 4;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * LDA), 16, 0, 0);
         }
     };
     auto dma_slabs = [&](long long t) {
@@ -512,16 +546,20 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     };
 
     const int c = c0 + i;
+    // Epilogue: 16 values per lane -> this wave's 32x32 output tile staged in its private
+    // slab (slab 0, whose operand values are already in registers) -> 4 buffer_store_dwordx4
+    // per wave through a per-tile buffer resource whose range check drops rows past M.
     auto epilogue = [&](long long t, const f32x16& acc) {
         const long long row0 = t * TR;
+        const long long left = (long long)p.M - row0;
+        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C + row0 * D, (short)0, nbytes, 0x00020000);
+        float vals[16];
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
             const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            const long long e = row0 + row;
-            if (e >= p.M) continue;
             float v = acc[reg];
-            float* cp = p.C + e * D + c;
-            if (p.accumulate) v += *cp;
+            if (p.accumulate) v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, (row * D + c) * 4, 0, 0));
             if (NV > 0) {
 #pragma unroll
                 for (int r = 0; r < NV; ++r) v = fmaf(coefw[row * NV + r], slabw[r * SLAB + row * 32 + i], v);
@@ -534,11 +572,24 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
                 const float x = slabw[NV * SLAB + row * 32 + i];
                 v = v * (x * (1.0f - x));
             }
-            *cp = v;
+            vals[reg] = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // operand reads done: reuse slab 0
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            slabw[row * 32 + i] = vals[reg];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int row = 8 * k + (lane >> 3), c4 = lane & 7;
+            const f32x4 o = ld4(slabw + row * 32 + c4 * 4);
+            __builtin_amdgcn_raw_buffer_store_b128(o, rc, (row * D + c0 + c4 * 4) * 4, 0, 0);
         }
     };
 
-    // ---- prologue ---------------------------------------------------------------------
+    // ---- prologue: A(t_beg), indices and epilogue slabs of t_beg, indices of t_beg+1 ------
     {
         const int a0 = load_aidx(t_beg);
         dma_idx(t_beg);
@@ -546,59 +597,70 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
         to_sgpr(a0);
         dma_A(t_beg, 0);
         const int a1 = load_aidx(t_beg + 1);
-        if (!late) {
-            dma_slabs(t_beg);
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            dma_idx(t_beg + 1);                    // group 0 consumes tile t_beg's indices here
-        }
+        dma_slabs(t_beg);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        dma_idx(t_beg + 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         to_sgpr(a1);
         __syncthreads();
     }
 
-    f32x16 acc;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-    int b = 0;
-    for (long long t = t_beg; t < t_end; ++t, b ^= 1) {
-        if (late) {
-            if (t > t_beg) epilogue(t - 1, acc);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // epilogue LDS reads done before overwrite
-            dma_slabs(t);                                          // reads idx(t) from the slot
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            dma_idx(t + 1);                                        // slot now free for idx(t+1)
-        }
-        if (t + 1 < t_end) dma_A(t + 1, b ^ 1);
-        const int an = load_aidx(t + 2);
-
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-        const float* arow = bufA + b * A_FLOATS + i * D;
-        const int sw = i & 15;
-#pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            const f32x4 a4 = ld4(arow + (((2 * q + h) ^ sw) * 4));
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[0], breg[4 * q + 0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[1], breg[4 * q + 1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[2], breg[4 * q + 2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[3], breg[4 * q + 3], acc, 0, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // A(t+1), indices, own slabs landed
-        if (!late) {
-            epilogue(t, acc);
-            if (t + 1 < t_end) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                dma_slabs(t + 1);                                     // in flight across the barrier
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                dma_idx(t + 2);
-            }
-        }
-        to_sgpr(an);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");                             // no LDS access crosses the barrier
+    // ---- main loop, specialised per half: LATE waves run epilogue(t-1) before MFMA(t),
+    // early waves epilogue(t) after it.  Branching once per wave into two compile-time copies
+    // keeps one epilogue site per copy (the register allocator sees each path separately).
+    // main loop, specialised per half (early / LATE); a macro keeps breg[] a plain local array
+    // (capturing it in a lambda made hipcc place it in scratch).
+#define V3_MAIN_LOOP(LATE) \
+    { \
+        f32x16 acc; \
+_Pragma("unroll") \
+        for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
+        int b = 0; \
+        for (long long t = t_beg; t < t_end; ++t, b ^= 1) { \
+            if (LATE && t > t_beg) { \
+                epilogue(t - 1, acc); \
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+                dma_slabs(t); \
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+                dma_idx(t + 1); \
+            } \
+            if (t + 1 < t_end) dma_A(t + 1, b ^ 1); \
+            const int an = load_aidx(t + 2); \
+_Pragma("unroll") \
+            for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
+            const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
+            f32x4 a_cur = ld4(arow); \
+_Pragma("unroll") \
+            for (int q = 0; q < D / 8; ++q) { \
+                f32x4 a_nxt = a_cur; \
+                if (q + 1 < D / 8) a_nxt = ld4(arow + 8 * (q + 1)); \
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[0], breg[4 * q + 0], acc, 0, 0, 0); \
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[1], breg[4 * q + 1], acc, 0, 0, 0); \
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[2], breg[4 * q + 2], acc, 0, 0, 0); \
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[3], breg[4 * q + 3], acc, 0, 0, 0); \
+                __builtin_amdgcn_sched_barrier(0); \
+                a_cur = a_nxt; \
+            } \
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+            if (!LATE) { \
+                epilogue(t, acc); \
+                if (t + 1 < t_end) { \
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+                    dma_slabs(t + 1); \
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+                    dma_idx(t + 2); \
+                } \
+            } \
+            to_sgpr(an); \
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+            __builtin_amdgcn_s_barrier(); \
+            asm volatile("" ::: "memory"); \
+        } \
+        if (LATE) epilogue(t_end - 1, acc); \
     }
-    if (late) epilogue(t_end - 1, acc);
+    if (V3_PRIO && late) __builtin_amdgcn_s_setprio(1);
+    if (late) V3_MAIN_LOOP(true) else V3_MAIN_LOOP(false)
+#undef V3_MAIN_LOOP
 }
 
 // ---------------------------------------------------------------------------
@@ -760,14 +822,27 @@ __global__ __launch_bounds__(512) void gemm_tn256_dma_kernel(long long M, long l
         if (t + 1 < nt) stage(t + 1, b ^ 1);
         const float* As = lds + (b * 2 + 0) * TILE;
         const float* Bs = lds + (b * 2 + 1) * TILE;
+        float a_cur = As[h * D + 32 * wave + i];
+        float b_cur[8];
+#pragma unroll
+        for (int cj = 0; cj < 8; ++cj) b_cur[cj] = Bs[h * D + 32 * cj + i];
 #pragma unroll
         for (int s = 0; s < TK / 2; ++s) {
-            const float a = As[(2 * s + h) * D + 32 * wave + i];
+            float a_nxt = a_cur, b_nxt[8];
 #pragma unroll
-            for (int cj = 0; cj < 8; ++cj) {
-                const float bv = Bs[(2 * s + h) * D + 32 * cj + i];
-                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[cj], 0, 0, 0);
+            for (int cj = 0; cj < 8; ++cj) b_nxt[cj] = b_cur[cj];
+            if (s + 1 < TK / 2) {
+                a_nxt = As[(2 * (s + 1) + h) * D + 32 * wave + i];
+#pragma unroll
+                for (int cj = 0; cj < 8; ++cj) b_nxt[cj] = Bs[(2 * (s + 1) + h) * D + 32 * cj + i];
             }
+#pragma unroll
+            for (int cj = 0; cj < 8; ++cj)
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur, b_cur[cj], acc[cj], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            a_cur = a_nxt;
+#pragma unroll
+            for (int cj = 0; cj < 8; ++cj) b_cur[cj] = b_nxt[cj];
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -868,6 +943,9 @@ __global__ __launch_bounds__(256) void alpha_kernel(int M, int R, const float* _
 // ---------------------------------------------------------------------------
 // combine (no GEMM): out = sigmoid(Y[yi] + sum_r coef[ci][r] * V_r[vi])
 // ---------------------------------------------------------------------------
+// Each lane group handles CU_ROWS rows (stride GROUPS within the block) with every index and
+// row load issued before any use: ~1/8 the workgroups of a row-per-group launch.
+constexpr int CU_ROWS = 8;
 template <int D>
 __global__ __launch_bounds__(256) void combine_kernel(int M, int R, const float* __restrict__ Y,
                                                       const int* __restrict__ y_idx, const float* __restrict__ coef,
@@ -875,21 +953,41 @@ __global__ __launch_bounds__(256) void combine_kernel(int M, int R, const float*
                                                       const int* __restrict__ v_idx, long long v_rel_stride,
                                                       float* __restrict__ out) {
     constexpr int LPR = D / 4;
-    const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    constexpr int GROUPS = 256 / LPR;
+    const int grp = threadIdx.x / LPR;
     const int sub = threadIdx.x % LPR;
-    if (e >= M) return;
-    const long long yi = y_idx ? (long long)y_idx[e] : e;
-    const long long ci = coef_idx ? (long long)coef_idx[e] : e;
-    const long long vi = v_idx ? (long long)v_idx[e] : e;
-    f32x4 v = ld4(Y + yi * D + sub * 4);
+    const long long base = (long long)blockIdx.x * GROUPS * CU_ROWS + grp;
+    long long yi[CU_ROWS], ci[CU_ROWS], vi[CU_ROWS];
+#pragma unroll
+    for (int u = 0; u < CU_ROWS; ++u) {
+        const long long e = base + (long long)u * GROUPS;
+        const bool ok = e < M;
+        yi[u] = ok ? (y_idx ? (long long)y_idx[e] : e) : 0;
+        ci[u] = ok ? (coef_idx ? (long long)coef_idx[e] : e) : 0;
+        vi[u] = ok ? (v_idx ? (long long)v_idx[e] : e) : 0;
+    }
+    f32x4 v[CU_ROWS];
+#pragma unroll
+    for (int u = 0; u < CU_ROWS; ++u) v[u] = ld4(Y + yi[u] * D + sub * 4);
     for (int r = 0; r < R; ++r) {
-        const float w = coef[ci * R + r];
-        const f32x4 pv = ld4(V + r * v_rel_stride + vi * D + sub * 4);
-        v += w * pv;
+        f32x4 pv[CU_ROWS];
+        float w[CU_ROWS];
+#pragma unroll
+        for (int u = 0; u < CU_ROWS; ++u) {
+            w[u] = coef[ci[u] * R + r];
+            pv[u] = ld4(V + r * v_rel_stride + vi[u] * D + sub * 4);
+        }
+#pragma unroll
+        for (int u = 0; u < CU_ROWS; ++u) v[u] += w[u] * pv[u];
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = sigmoid_fast(v[j]);
-    st4(out + e * D + sub * 4, v);
+    for (int u = 0; u < CU_ROWS; ++u) {
+        const long long e = base + (long long)u * GROUPS;
+        if (e >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[u][j] = sigmoid_fast(v[u][j]);
+        st4(out + e * D + sub * 4, v[u]);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1081,7 +1179,11 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int r = 0; r < R; ++r) w[u][r] = (k + u < len) ? W[(long long)hh[u] * R + r] : 0.f;
-        float dw[U][R];
+        constexpr int KV = U * R;
+        constexpr int KP = KV <= 4 ? 4 : KV <= 8 ? 8 : KV <= 16 ? 16 : 32;   // padded to a power of two
+        float dw[KP];
+#pragma unroll
+        for (int j = 0; j < KP; ++j) dw[j] = 0.f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             s4 += d[u];
@@ -1089,20 +1191,25 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             for (int r = 0; r < R; ++r) {
                 acc[r] += w[u][r] * d[u];
                 const f32x4 q = d[u] * pr[r];
-                dw[u][r] = q[0] + q[1] + q[2] + q[3];
+                dw[u * R + r] = q[0] + q[1] + q[2] + q[3];
             }
         }
+        if constexpr (KP <= LPR) {
+            const float tot = multi_reduce<LPR, KP>(dw, sub);
+            constexpr int SPAN = LPR / KP;                 // lanes sharing one value
+            const int j = sub / SPAN;
+            if (sub % SPAN == 0 && j < KV) {
+                const int u = j / R, r = j % R;
+                if (k + u < len) dWedge[(long long)(beg + k + u) * R + r] = tot;
+            }
+        } else {
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+            for (int j = 0; j < KV; ++j) dw[j] = group_sum<LPR>(dw[j]);
+            if (sub == 0) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) dw[u][r] = group_sum<LPR>(dw[u][r]);
-        if (sub == 0) {
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (k + u < len) {
-#pragma unroll
-                    for (int r = 0; r < R; ++r) dWedge[(long long)(beg + k + u) * R + r] = dw[u][r];
-                }
+                for (int j = 0; j < KV; ++j)
+                    if (k + j / R < len) dWedge[(long long)(beg + k + j / R) * R + j % R] = dw[j];
+            }
         }
     }
     if (!live) return;
@@ -1406,7 +1513,7 @@ int iddgcn_combine_f32(void* stream, int M, int d, int R, const float* Y, const 
     if (M < 0 || !Y || !out || (R > 0 && (!coef || !V))) return IDDGCN_E_BAD_ARG;
     if (M == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const unsigned grid = grid_for(M, d / 4);
+    const unsigned grid = (unsigned)(((long long)M + (256 / (d / 4)) * CU_ROWS - 1) / ((256 / (d / 4)) * CU_ROWS));
 #define CK(DD) hipLaunchKernelGGL(combine_kernel<DD>, dim3(grid), dim3(256), 0, st, M, R, Y, y_idx, coef, coef_idx, V, v_idx, v_rel_stride, out)
     switch (d) {
         case 32: CK(32); break;
