@@ -50,6 +50,7 @@ SIGNATURES = {
     "iddgcn_seg_gather_reduce_f32": (ci, [vp, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iddgcn_tail_seg_reduce_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, cll, vp, cll, vp, vp]),
     "iddgcn_head_bwd_node_f32": (ci, [vp, ci, ci, ci, vp, vp, cll, vp, vp, vp, vp, vp, vp, cll, vp, vp]),
+    "iddgcn_gather_rows_f32": (ci, [vp, cll, ci, vp, vp, vp]),
     "iddgcn_reduce_slabs_f32": (ci, [vp, ci, cll, vp, vp, ci, cf]),
     "iddgcn_adam_f32": (ci, [vp, cll, vp, vp, vp, vp, cf, cf, cf, cf, ci]),
 }

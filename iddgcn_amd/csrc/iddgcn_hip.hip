@@ -437,6 +437,10 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
 #ifndef V3_PRIO
 #define V3_PRIO 0
 #endif
+// ablation switches for the GEMM microbenchmark (never set in the product build)
+#ifndef V3_ABL
+#define V3_ABL 0
+#endif
 namespace r3 {
 constexpr int D = 256, NW = 8, TR = 32;
 constexpr int ROWS_PER_WAVE = TR / NW;                 // A rows each wave stages
@@ -515,6 +519,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
         }
     };
     auto dma_slabs = [&](long long t) {
+        if (V3_ABL & 1) return;
         if (NV > 0) {
 #pragma unroll
             for (int r = 0; r < NV; ++r)
@@ -560,6 +565,10 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
             float v = acc[reg];
             if (p.accumulate) v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, (row * D + c) * 4, 0, 0));
+            if (V3_ABL & 2) {
+                vals[reg] = v;
+                continue;
+            }
             if (NV > 0) {
 #pragma unroll
                 for (int r = 0; r < NV; ++r) v = fmaf(coefw[row * NV + r], slabw[r * SLAB + row * 32 + i], v);
@@ -585,6 +594,10 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
         for (int k = 0; k < 4; ++k) {
             const int row = 8 * k + (lane >> 3), c4 = lane & 7;
             const f32x4 o = ld4(slabw + row * 32 + c4 * 4);
+            if (V3_ABL & 4) {
+                asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
+                continue;
+            }
             __builtin_amdgcn_raw_buffer_store_b128(o, rc, (row * D + c0 + c4 * 4) * 4, 0, 0);
         }
     };
@@ -943,9 +956,11 @@ __global__ __launch_bounds__(256) void alpha_kernel(int M, int R, const float* _
 // ---------------------------------------------------------------------------
 // combine (no GEMM): out = sigmoid(Y[yi] + sum_r coef[ci][r] * V_r[vi])
 // ---------------------------------------------------------------------------
-// Each lane group handles CU_ROWS rows (stride GROUPS within the block) with every index and
-// row load issued before any use: ~1/8 the workgroups of a row-per-group launch.
-constexpr int CU_ROWS = 8;
+// Persistent, software-pipelined: each lane group walks batches of CU_ROWS rows (stride GROUPS
+// inside a block-batch); the next batch's indices load while the current batch's rows are in
+// flight, so no wave ever waits on an index load followed by a dependent row load.
+constexpr int CU_ROWS = 4;
+constexpr int CU_BLOCKS = 2048;
 template <int D>
 __global__ __launch_bounds__(256) void combine_kernel(int M, int R, const float* __restrict__ Y,
                                                       const int* __restrict__ y_idx, const float* __restrict__ coef,
@@ -954,39 +969,52 @@ __global__ __launch_bounds__(256) void combine_kernel(int M, int R, const float*
                                                       float* __restrict__ out) {
     constexpr int LPR = D / 4;
     constexpr int GROUPS = 256 / LPR;
+    constexpr int BATCH = GROUPS * CU_ROWS;          // rows per block-batch
     const int grp = threadIdx.x / LPR;
     const int sub = threadIdx.x % LPR;
-    const long long base = (long long)blockIdx.x * GROUPS * CU_ROWS + grp;
-    long long yi[CU_ROWS], ci[CU_ROWS], vi[CU_ROWS];
-#pragma unroll
-    for (int u = 0; u < CU_ROWS; ++u) {
-        const long long e = base + (long long)u * GROUPS;
-        const bool ok = e < M;
-        yi[u] = ok ? (y_idx ? (long long)y_idx[e] : e) : 0;
-        ci[u] = ok ? (coef_idx ? (long long)coef_idx[e] : e) : 0;
-        vi[u] = ok ? (v_idx ? (long long)v_idx[e] : e) : 0;
-    }
-    f32x4 v[CU_ROWS];
-#pragma unroll
-    for (int u = 0; u < CU_ROWS; ++u) v[u] = ld4(Y + yi[u] * D + sub * 4);
-    for (int r = 0; r < R; ++r) {
-        f32x4 pv[CU_ROWS];
-        float w[CU_ROWS];
+    const long long nbatch = ((long long)M + BATCH - 1) / BATCH;
+    auto load_idx = [&](long long bt, long long (&yi)[CU_ROWS], long long (&ci)[CU_ROWS], long long (&vi)[CU_ROWS]) {
 #pragma unroll
         for (int u = 0; u < CU_ROWS; ++u) {
-            w[u] = coef[ci[u] * R + r];
-            pv[u] = ld4(V + r * v_rel_stride + vi[u] * D + sub * 4);
+            const long long e = bt * BATCH + grp + (long long)u * GROUPS;
+            const bool ok = bt < nbatch && e < M;
+            yi[u] = ok ? (y_idx ? (long long)y_idx[e] : e) : 0;
+            ci[u] = ok ? (coef_idx ? (long long)coef_idx[e] : e) : 0;
+            vi[u] = ok ? (v_idx ? (long long)v_idx[e] : e) : 0;
         }
+    };
+    long long yi[CU_ROWS], ci[CU_ROWS], vi[CU_ROWS];
+    long long bt = blockIdx.x;
+    load_idx(bt, yi, ci, vi);
+    for (; bt < nbatch; bt += gridDim.x) {
+        f32x4 v[CU_ROWS];
 #pragma unroll
-        for (int u = 0; u < CU_ROWS; ++u) v[u] += w[u] * pv[u];
-    }
+        for (int u = 0; u < CU_ROWS; ++u) v[u] = ld4(Y + yi[u] * D + sub * 4);
+        for (int r = 0; r < R; ++r) {
+            f32x4 pv[CU_ROWS];
+            float w[CU_ROWS];
 #pragma unroll
-    for (int u = 0; u < CU_ROWS; ++u) {
-        const long long e = base + (long long)u * GROUPS;
-        if (e >= M) continue;
+            for (int u = 0; u < CU_ROWS; ++u) {
+                w[u] = coef[ci[u] * R + r];
+                pv[u] = ld4(V + r * v_rel_stride + vi[u] * D + sub * 4);
+            }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[u][j] = sigmoid_fast(v[u][j]);
-        st4(out + e * D + sub * 4, v[u]);
+            for (int u = 0; u < CU_ROWS; ++u) v[u] += w[u] * pv[u];
+        }
+        long long yn[CU_ROWS], cn[CU_ROWS], vn[CU_ROWS];
+        load_idx(bt + gridDim.x, yn, cn, vn);
+#pragma unroll
+        for (int u = 0; u < CU_ROWS; ++u) {
+            const long long e = bt * BATCH + grp + (long long)u * GROUPS;
+            if (e < M) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[u][j] = sigmoid_fast(v[u][j]);
+                st4(out + e * D + sub * 4, v[u]);
+            }
+            yi[u] = yn[u];
+            ci[u] = cn[u];
+            vi[u] = vn[u];
+        }
     }
 }
 
@@ -1171,7 +1199,8 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool a = k + u < len;
-            hh[u] = a ? h_idx[beg + k + u] : 0;
+            // h_idx == NULL: W is already per edge (W[e][r], gathered once per layer)
+            hh[u] = a ? (h_idx ? h_idx[beg + k + u] : beg + k + u) : 0;
             d[u] = a ? ld4(dO + (long long)(beg + k + u) * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
         float w[U][R];
@@ -1281,6 +1310,16 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
             float* pp = dP + r * dp_rel_stride + n * D + sub * 4;
             st4(pp, ld4(pp) + w[r] * d);
         }
+}
+
+// dst[e][j] = src[idx[e]][j] for a narrow row width (per-edge copies of node tables)
+__global__ __launch_bounds__(256) void gather_rows_kernel(long long M, int width, const float* __restrict__ src,
+                                                          const int* __restrict__ idx, float* __restrict__ dst) {
+    const long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= M * width) return;
+    const long long e = x / width;
+    const int j = (int)(x % width);
+    dst[x] = src[(long long)idx[e] * width + j];
 }
 
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(int n_slabs, long long n, const float* __restrict__ slab,
@@ -1513,7 +1552,8 @@ int iddgcn_combine_f32(void* stream, int M, int d, int R, const float* Y, const 
     if (M < 0 || !Y || !out || (R > 0 && (!coef || !V))) return IDDGCN_E_BAD_ARG;
     if (M == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const unsigned grid = (unsigned)(((long long)M + (256 / (d / 4)) * CU_ROWS - 1) / ((256 / (d / 4)) * CU_ROWS));
+    const long long nbatch = ((long long)M + (256 / (d / 4)) * CU_ROWS - 1) / ((256 / (d / 4)) * CU_ROWS);
+    const unsigned grid = (unsigned)(nbatch < CU_BLOCKS ? nbatch : CU_BLOCKS);
 #define CK(DD) hipLaunchKernelGGL(combine_kernel<DD>, dim3(grid), dim3(256), 0, st, M, R, Y, y_idx, coef, coef_idx, V, v_idx, v_rel_stride, out)
     switch (d) {
         case 32: CK(32); break;
@@ -1576,7 +1616,7 @@ int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const in
                                long long dp_rel_stride, float* dsum, float* dWedge) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
-    if (n_nodes < 0 || !seg_ptr || !h_idx || !W || !dO || !P || !dP || !dWedge) return IDDGCN_E_BAD_ARG;
+    if (n_nodes < 0 || !seg_ptr || !W || !dO || !P || !dP || !dWedge) return IDDGCN_E_BAD_ARG;
     if (n_nodes == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     const unsigned grid = grid_for(n_nodes, d / 4);
@@ -1622,6 +1662,15 @@ int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const floa
         default: HK(256); break;
     }
 #undef HK
+    return launch_status();
+}
+
+int iddgcn_gather_rows_f32(void* stream, long long M, int width, const float* src, const int* idx, float* dst) {
+    if (M < 0 || width < 1 || !src || !idx || !dst) return IDDGCN_E_BAD_ARG;
+    if (M == 0) return 0;
+    const long long n = M * width;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, M,
+                       width, src, idx, dst);
     return launch_status();
 }
 

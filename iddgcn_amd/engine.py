@@ -105,6 +105,7 @@ class Workspace:
         self.Ssm = e(NUM_LAYERS, N, R)
         self.W = e(NUM_LAYERS, N, R)
         self.xt = e(NUM_LAYERS, T, D)           # tail chain x^1..x^3
+        self.Wedge = e(NUM_LAYERS, T, R)        # W^l[h_e]: per-edge copy of the dynamic weights
         self.p = e(T)
         self.nb_dm = ops.distmult_blocks(T)
         self.train = train
@@ -185,16 +186,18 @@ class Engine:
         # layer 1: x·S1 is node-level for both sides (inputs are E[h], E[t])
         ops.rowgemm(E, P["S1"], ws.ES1)
         ops.alpha_fwd(E, P["Wa1"], P["ba1"], ws.Ssm[0], ws.W[0])
+        ops.gather_rows(ws.W[0], ed.h, ws.Wedge[0])
         ops.combine(ws.ES1, ws.W[0], ws.P[0], ws.X[0])
-        ops.combine(ws.ES1, ws.W[0], ws.P[0], ws.xt[0], y_idx=ed.t, coef_idx=ed.h, v_idx=ed.t)
+        ops.combine(ws.ES1, ws.Wedge[0], ws.P[0], ws.xt[0], y_idx=ed.t, v_idx=ed.t)
         # layers 2, 3
         for l in (1, 2):
             S = P[f"S{l + 1}"]
             ops.alpha_fwd(ws.X[l - 1], P[f"Wa{l + 1}"], P[f"ba{l + 1}"], ws.Ssm[l], ws.W[l])
+            ops.gather_rows(ws.W[l], ed.h, ws.Wedge[l])
             ops.rowgemm(ws.X[l - 1], S, ws.X[l], coef=ws.W[l], V=ws.P[l], v_rel_stride=N * D,
                         act=L.ACT_SIGMOID)
             with self._mark("tail_fwd_gemm"):
-                ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.W[l], coef_idx=ed.h, V=ws.P[l], v_idx=ed.t,
+                ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID)
         # DistMult (+ BCE and backward seed when training)
         if train:
@@ -217,7 +220,7 @@ class Engine:
         for l in (2, 1, 0):                     # layer index l -> reference layer l+1
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
             # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part
-            ops.tail_seg_reduce(ed.tptr, ed.h, Wl, do, Pl, ws.dP, ws.dWedge, dsum=ws.dES if l == 0 else None)
+            ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge, dsum=ws.dES if l == 0 else None)
             if l > 0:
                 # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x)
                 with self._mark("tail_dS_tn"):

@@ -183,6 +183,8 @@ def tail_seg_reduce(seg_ptr, h_idx, W, dO, P, dP, dWedge, dsum=None):
     _req(P, _F32, (R, n_nodes, D), "P")
     _req(dP, _F32, (R, n_nodes, D), "dP")
     _req(dsum, _F32, (n_nodes, D), "dsum")
+    if h_idx is None and W.shape[0] != dO.shape[0]:
+        raise L.IddgcnError("tail_seg_reduce: per-edge W must have one row per edge")
     L.check(L.lib().iddgcn_tail_seg_reduce_f32(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(h_idx), _ptr(W),
                                                _ptr(dO), _ptr(P), n_nodes * D, _ptr(dP), n_nodes * D, _ptr(dsum),
                                                _ptr(dWedge)), "tail_seg_reduce")
@@ -198,6 +200,17 @@ def head_bwd_node(dO, P, Ssm, W, dP, dz, *, hseg_ptr=None, hperm=None, dWedge=No
     L.check(L.lib().iddgcn_head_bwd_node_f32(_stream(), n_nodes, D, R, _ptr(dO), _ptr(P), n_nodes * D, _ptr(Ssm),
                                              _ptr(W), _ptr(hseg_ptr), _ptr(hperm), _ptr(dWedge), _ptr(dP),
                                              n_nodes * D, _ptr(dsum), _ptr(dz)), "head_bwd_node")
+
+
+def gather_rows(src, idx, dst):
+    """dst[e] = src[idx[e]] for narrow rows (src: (N, w), idx: (M,) int32, dst: (M, w))."""
+    M, w = dst.shape
+    _req(src, _F32, None, "src")
+    _req(idx, _I32, (M,), "idx")
+    _req(dst, _F32, (M, w), "dst")
+    if src.dim() != 2 or src.shape[1] != w:
+        raise L.IddgcnError("gather_rows: width mismatch")
+    L.check(L.lib().iddgcn_gather_rows_f32(_stream(), M, w, _ptr(src), _ptr(idx), _ptr(dst)), "gather_rows")
 
 
 def reduce_slabs(slab, n_slabs, out, accumulate=False, scale=1.0):

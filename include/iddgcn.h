@@ -130,6 +130,7 @@ int iddgcn_seg_gather_reduce_f32(void* stream, int n_nodes, int d, const int* se
 
 /* Tail-side backward of one layer over edges sorted by tail (contiguous segments):
  *   dP[r][n][:]   = sum_{e in seg(n)} W[h_idx[e]][r] * dO[e][:]        (gradient of P_r[t])
+ *                   (h_idx == NULL: W is per edge, W[e][r] — see iddgcn_gather_rows_f32)
  *   dsum[n][:]    = sum_{e in seg(n)} dO[e][:]                          (if dsum; layer-1 x·S input)
  *   dWedge[e][r]  = <dO[e], P[r][n]>                                    (gradient of sigmoid(alpha_r)) */
 int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const int* seg_ptr,
@@ -146,6 +147,10 @@ int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const floa
                              const float* P, long long p_rel_stride, const float* Ssm, const float* W,
                              const int* hseg_ptr, const int* hperm, const float* dWedge,
                              float* dP, long long dp_rel_stride, float* dsum, float* dz);
+
+/* dst[e][j] = src[idx[e]][j], j < width: per-edge copies of narrow node tables
+ * (the dynamic weights W[h_e] of each layer, IDDGCN.py:66,75, reused by forward and backward). */
+int iddgcn_gather_rows_f32(void* stream, long long M, int width, const float* src, const int* idx, float* dst);
 
 /* out[i] = (accumulate ? out[i] : 0) + scale * sum_{b<n_slabs} slab[b*n + i]  (block order) */
 int iddgcn_reduce_slabs_f32(void* stream, int n_slabs, long long n, const float* slab,
