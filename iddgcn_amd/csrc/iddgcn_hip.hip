@@ -518,6 +518,9 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * LDA), 16, 0, 0);
         }
     };
+    // Slabs are [32 rows][32 cols] with the 16-B column groups of row r XOR-swizzled by
+    // (r >> 1) & 7: the DMA (lane-linear destination) picks the swizzled source column, so
+    // both the per-row epilogue reads and the row-major store reads are conflict-free.
     auto dma_slabs = [&](long long t) {
         if (V3_ABL & 1) return;
         if (NV > 0) {
@@ -525,18 +528,22 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             for (int r = 0; r < NV; ++r)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const long long e = clampe(t * TR + 8 * k + (lane >> 3));
-                    const long long vi = p.v_idx ? (long long)idxw[8 * k + (lane >> 3)] : e;
-                    const float* g = p.V + r * p.v_rel_stride + vi * D + c0 + (lane & 7) * 4;
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(slabw + r * SLAB + k * 256), 16, 0, 0);
+                    const int row = 8 * k + (lane >> 3);
+                    const int g = (lane & 7) ^ ((row >> 1) & 7);
+                    const long long e = clampe(t * TR + row);
+                    const long long vi = p.v_idx ? (long long)idxw[row] : e;
+                    const float* gp = p.V + r * p.v_rel_stride + vi * D + c0 + g * 4;
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + r * SLAB + k * 256), 16, 0, 0);
                 }
         }
         if (AUX) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const long long e = clampe(t * TR + 8 * k + (lane >> 3));
-                const float* g = p.aux + e * D + c0 + (lane & 7) * 4;
-                __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(slabw + NV * SLAB + k * 256), 16, 0, 0);
+                const int row = 8 * k + (lane >> 3);
+                const int g = (lane & 7) ^ ((row >> 1) & 7);
+                const long long e = clampe(t * TR + row);
+                const float* gp = p.aux + e * D + c0 + g * 4;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + NV * SLAB + k * 256), 16, 0, 0);
             }
         }
         if (HAS_COEF) {
@@ -550,55 +557,68 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
         }
     };
 
-    const int c = c0 + i;
-    // Epilogue: 16 values per lane -> this wave's 32x32 output tile staged in its private
-    // slab (slab 0, whose operand values are already in registers) -> 4 buffer_store_dwordx4
+    // Epilogue.  The MFMA computes the transposed tile (weights as operand A), so lane (i, h)
+    // holds edge row i of the tile at columns c0 + 8j + 4h + {0..3}, j = 0..3: one coefficient
+    // read per lane and 16-B slab reads.  Results are staged in place in slab 0 (each lane
+    // rewrites exactly the slots it read), then re-read row-major for 4 buffer_store_dwordx4
     // per wave through a per-tile buffer resource whose range check drops rows past M.
+    const int sw = (i >> 1) & 7;
     auto epilogue = [&](long long t, const f32x16& acc) {
         const long long row0 = t * TR;
         const long long left = (long long)p.M - row0;
         const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
         const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C + row0 * D, (short)0, nbytes, 0x00020000);
-        float vals[16];
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            float v = acc[reg];
-            if (p.accumulate) v += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, (row * D + c) * 4, 0, 0));
-            if (V3_ABL & 2) {
-                vals[reg] = v;
-                continue;
+        float cf[NS_MAX] = {0.f, 0.f};
+        if (HAS_COEF) {
+            if (NV == 2 || (NV == 0 && R == 2)) {
+                const float2 c2 = *reinterpret_cast<const float2*>(coefw + i * 2);
+                cf[0] = c2.x;
+                cf[1] = c2.y;
+            } else {
+                cf[0] = coefw[i];
             }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int off = i * 32 + 4 * ((2 * j + h) ^ sw);
+            const int col = c0 + 8 * j + 4 * h;
+            f32x4 v = {acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
+            if (p.accumulate)
+                v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (i * D + col) * 4, 0, 0));
             if (NV > 0) {
 #pragma unroll
-                for (int r = 0; r < NV; ++r) v = fmaf(coefw[row * NV + r], slabw[r * SLAB + row * 32 + i], v);
+                for (int r = 0; r < NV; ++r) {
+                    const f32x4 s = ld4(slabw + r * SLAB + off);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
+                }
             } else if (HAS_COEF) {      // broadcast V rows (v_row_stride == 0): tiny, cache-resident
-                for (int r = 0; r < R; ++r) v = fmaf(coefw[row * R + r], p.V[r * p.v_rel_stride + c], v);
+                for (int r = 0; r < R; ++r) {
+                    const f32x4 s = ld4(p.V + r * p.v_rel_stride + col);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
+                }
             }
             if (p.act == IDDGCN_ACT_SIGMOID) {
-                v = sigmoid_fast(v);
-            } else if (p.act == IDDGCN_ACT_DSIGMOID) {
-                const float x = slabw[NV * SLAB + row * 32 + i];
-                v = v * (x * (1.0f - x));
-            }
-            vals[reg] = v;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // operand reads done: reuse slab 0
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            slabw[row * 32 + i] = vals[reg];
+                for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
+            } else if (p.act == IDDGCN_ACT_DSIGMOID) {
+                const f32x4 x = ld4(slabw + NV * SLAB + off);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = v[q] * (x[q] * (1.0f - x[q]));
+            }
+            st4(slabw + off, v);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int row = 8 * k + (lane >> 3), c4 = lane & 7;
-            const f32x4 o = ld4(slabw + row * 32 + c4 * 4);
+            const int row = 8 * k + (lane >> 3), cg = lane & 7;
+            const f32x4 o = ld4(slabw + row * 32 + 4 * (cg ^ ((row >> 1) & 7)));
             if (V3_ABL & 4) {
                 asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
                 continue;
             }
-            __builtin_amdgcn_raw_buffer_store_b128(o, rc, (row * D + c0 + c4 * 4) * 4, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(o, rc, (row * D + c0 + cg * 4) * 4, 0, 0);
         }
     };
 
@@ -647,10 +667,10 @@ _Pragma("unroll") \
             for (int q = 0; q < D / 8; ++q) { \
                 f32x4 a_nxt = a_cur; \
                 if (q + 1 < D / 8) a_nxt = ld4(arow + 8 * (q + 1)); \
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[0], breg[4 * q + 0], acc, 0, 0, 0); \
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[1], breg[4 * q + 1], acc, 0, 0, 0); \
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[2], breg[4 * q + 2], acc, 0, 0, 0); \
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[3], breg[4 * q + 3], acc, 0, 0, 0); \
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 0], a_cur[0], acc, 0, 0, 0); \
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 1], a_cur[1], acc, 0, 0, 0); \
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 2], a_cur[2], acc, 0, 0, 0); \
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 3], a_cur[3], acc, 0, 0, 0); \
                 __builtin_amdgcn_sched_barrier(0); \
                 a_cur = a_nxt; \
             } \
