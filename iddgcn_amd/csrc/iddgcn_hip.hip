@@ -31,20 +31,106 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 // layer activations: v_exp_f32 + v_rcp_f32 (~2 ulp; saturates to exactly 0 / 1 like the accurate form)
 __device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
+// ---- in-register cross-lane exchange for full-wave (64-lane) groups: no LDS round trip ----
+// v_permlane{32,16}_swap exchange half-waves / odd-even 16-lane rows between two registers;
+// DPP row_mirror (l^15), row_half_mirror (l^7) and quad_perm (l^2, l^1) pair each lane with one
+// whose bit m is flipped and whose higher bits match, which is all a butterfly level needs.
+// (inline asm: this hipcc returns the same register for both halves of the swap builtins;
+// the two v_nop are the VALU-write -> permlane hazard.)
+__device__ __forceinline__ void pl_swap32(float& a, float& b) {
+    asm volatile("v_nop\n\tv_nop\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void pl_swap16(float& a, float& b) {
+    asm volatile("v_nop\n\tv_nop\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_XOR2 = 0x4E, DPP_XOR1 = 0xB1;
+template <int M>
+__device__ __forceinline__ float xpartner_dpp(float v) {   // M in {8, 4, 2, 1}
+    if constexpr (M == 8) return dpp<DPP_ROW_MIRROR>(v);
+    else if constexpr (M == 4) return dpp<DPP_ROW_HALF_MIRROR>(v);
+    else if constexpr (M == 2) return dpp<DPP_XOR2>(v);
+    else return dpp<DPP_XOR1>(v);
+}
+
 template <int LPR>
 __device__ __forceinline__ float group_sum(float v) {
+    if constexpr (LPR == 64) {
+        float a = v, b = v;
+        pl_swap32(a, b);
+        v = a + b;
+        a = v, b = v;
+        pl_swap16(a, b);
+        v = a + b;
+        v += xpartner_dpp<8>(v);
+        v += xpartner_dpp<4>(v);
+        v += xpartner_dpp<2>(v);
+        v += xpartner_dpp<1>(v);
+        return v;
+    } else {
 #pragma unroll
-    for (int m = LPR / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-    return v;
+        for (int m = LPR / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+        return v;
+    }
 }
 
 // Reduce K values (K a power of two, K <= LPR) over an aligned group of LPR lanes with a
 // butterfly that halves the value set at each level: K-1 + log2(LPR/K) ... shuffles instead of
 // K*log2(LPR).  On return v[0] holds, in every lane, the full sum of value index
-// sub / (LPR/K).  Pairwise adds happen in the same order as group_sum (bitwise identical).
+// sub / (LPR/K).  LPR == 64 uses the permlane/DPP exchanges above.
 template <int LPR, int K>
 __device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
     static_assert((K & (K - 1)) == 0 && K <= LPR, "K must be a power of two <= LPR");
+    if constexpr (LPR == 64) {
+        // levels 32 and 16: one register swap exchanges the kept/sent halves of a value pair
+        int kc = K;
+        auto swap_level = [&](auto swapper) {
+            if (kc > 1) {
+                const int half = kc / 2;
+#pragma unroll
+                for (int j = 0; j < K / 2; ++j) {
+                    if (j < half) {
+                        float a = v[j], b = v[half + j];
+                        swapper(a, b);
+                        v[j] = a + b;
+                    }
+                }
+                kc = half;
+            } else {
+                float a = v[0], b = v[0];
+                swapper(a, b);
+                v[0] = a + b;
+            }
+        };
+        swap_level([](float& a, float& b) { pl_swap32(a, b); });
+        swap_level([](float& a, float& b) { pl_swap16(a, b); });
+        auto dpp_level = [&](auto mtag) {
+            constexpr int m = decltype(mtag)::value;
+            if (kc > 1) {
+                const bool up = (sub & m) != 0;
+                const int half = kc / 2;
+#pragma unroll
+                for (int j = 0; j < K / 2; ++j) {
+                    if (j < half) {
+                        const float keep = up ? v[half + j] : v[j];
+                        const float send = up ? v[j] : v[half + j];
+                        v[j] = keep + xpartner_dpp<m>(send);
+                    }
+                }
+                kc = half;
+            } else {
+                v[0] += xpartner_dpp<m>(v[0]);
+            }
+        };
+        dpp_level(std::integral_constant<int, 8>{});
+        dpp_level(std::integral_constant<int, 4>{});
+        dpp_level(std::integral_constant<int, 2>{});
+        dpp_level(std::integral_constant<int, 1>{});
+        return v[0];
+    }
     int kc = K;
 #pragma unroll
     for (int m = LPR / 2; m >= 1; m >>= 1) {
@@ -450,7 +536,8 @@ constexpr int SLAB = TR * 32;                          // 32 rows x 32 cols
 constexpr int NS_MAX = 2;
 constexpr int COEF = 64;                               // 32 rows x R (R <= 2)
 constexpr int IDX = 64;                                // next tile's v_idx (32) + coef_idx (32)
-constexpr int WAVE_FLOATS = NS_MAX * SLAB + COEF + IDX;
+constexpr int CMP = 32;                                // distinct V rows of the tile (run starts)
+constexpr int WAVE_FLOATS = NS_MAX * SLAB + COEF + IDX + CMP;
 constexpr int LDS_FLOATS = 2 * A_FLOATS + NW * WAVE_FLOATS;   // 130 KiB
 }  // namespace r3
 
@@ -486,6 +573,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
 
     // ---- row indices of the next tile: DMA'd into a wave-private LDS slot -------------
     int* idxw = reinterpret_cast<int*>(coefw + r3::COEF);      // [0,32) v_idx, [32,64) coef_idx
+    int vslot = 0;                                               // slab row of this lane's V row
     const bool need_idx = (NV > 0 && p.v_idx) || (HAS_COEF && p.coef_idx);
     auto dma_idx = [&](long long t) {
         if (!need_idx || t >= t_end) return;
@@ -521,20 +609,38 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     // Slabs are [32 rows][32 cols] with the 16-B column groups of row r XOR-swizzled by
     // (r >> 1) & 7: the DMA (lane-linear destination) picks the swizzled source column, so
     // both the per-row epilogue reads and the row-major store reads are conflict-free.
+    // V slabs hold only the tile's DISTINCT V rows (consecutive rows with the same v_idx form
+    // a run; tail-sorted edges give 1-2 runs per tile): a ballot over the 32 row indices finds
+    // the run starts, the starts' indices are compacted into a wave-private list, and
+    // ceil(u / 8) DMA instructions per relation fetch the u distinct rows.  Each lane keeps the
+    // slot of its row for the epilogue (vslot).
+    int* cmpw = idxw + r3::IDX;
     auto dma_slabs = [&](long long t) {
         if (V3_ABL & 1) return;
         if (NV > 0) {
+            int vi = 0;
+            bool start = false;
+            if (lane < 32) {
+                const long long e = clampe(t * TR + lane);
+                vi = p.v_idx ? idxw[lane] : (int)e;
+                const int prev = p.v_idx ? idxw[lane > 0 ? lane - 1 : 0] : (int)e - 1;
+                start = lane == 0 || vi != prev;
+            }
+            const unsigned long long m = __ballot(start);
+            const int u = __popcll(m);
+            vslot = __popcll(m & ((2ull << (lane & 31)) - 1)) - 1;
+            if (start) cmpw[vslot] = vi;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int kb = 0; kb < u; kb += 8) {
+                const int row = kb + (lane >> 3);
+                const int g = (lane & 7) ^ ((row >> 1) & 7);
+                const long long v = cmpw[row < u ? row : u - 1];
 #pragma unroll
-            for (int r = 0; r < NV; ++r)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int row = 8 * k + (lane >> 3);
-                    const int g = (lane & 7) ^ ((row >> 1) & 7);
-                    const long long e = clampe(t * TR + row);
-                    const long long vi = p.v_idx ? (long long)idxw[row] : e;
-                    const float* gp = p.V + r * p.v_rel_stride + vi * D + c0 + g * 4;
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + r * SLAB + k * 256), 16, 0, 0);
+                for (int r = 0; r < NV; ++r) {
+                    const float* gp = p.V + r * p.v_rel_stride + v * D + c0 + g * 4;
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + r * SLAB + kb * 32), 16, 0, 0);
                 }
+            }
         }
         if (AUX) {
 #pragma unroll
@@ -585,10 +691,11 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             f32x4 v = {acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
             if (p.accumulate)
                 v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (i * D + col) * 4, 0, 0));
-            if (NV > 0) {
+            if (NV > 0 && !(V3_ABL & 2)) {
+                const int offv = vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
 #pragma unroll
                 for (int r = 0; r < NV; ++r) {
-                    const f32x4 s = ld4(slabw + r * SLAB + off);
+                    const f32x4 s = ld4(slabw + r * SLAB + offv);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
                 }
@@ -599,7 +706,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
                 }
             }
-            if (p.act == IDDGCN_ACT_SIGMOID) {
+            if (p.act == IDDGCN_ACT_SIGMOID && !(V3_ABL & 8)) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
             } else if (p.act == IDDGCN_ACT_DSIGMOID) {
@@ -977,12 +1084,13 @@ __global__ __launch_bounds__(256) void alpha_kernel(int M, int R, const float* _
 // combine (no GEMM): out = sigmoid(Y[yi] + sum_r coef[ci][r] * V_r[vi])
 // ---------------------------------------------------------------------------
 // Persistent, software-pipelined: each lane group walks batches of CU_ROWS rows (stride GROUPS
-// inside a block-batch); the next batch's indices load while the current batch's rows are in
-// flight, so no wave ever waits on an index load followed by a dependent row load.
+// inside a block-batch).  vmcnt counts loads and stores together in issue order, so the rows of
+// batch b+1 (and the indices of batch b+2) are issued BEFORE batch b's stores: no load ever
+// waits behind a store acknowledgement.
 constexpr int CU_ROWS = 4;
 constexpr int CU_BLOCKS = 2048;
-template <int D>
-__global__ __launch_bounds__(256) void combine_kernel(int M, int R, const float* __restrict__ Y,
+template <int D, int R>
+__global__ __launch_bounds__(256) void combine_kernel(int M, const float* __restrict__ Y,
                                                       const int* __restrict__ y_idx, const float* __restrict__ coef,
                                                       const int* __restrict__ coef_idx, const float* __restrict__ V,
                                                       const int* __restrict__ v_idx, long long v_rel_stride,
@@ -990,51 +1098,150 @@ __global__ __launch_bounds__(256) void combine_kernel(int M, int R, const float*
     constexpr int LPR = D / 4;
     constexpr int GROUPS = 256 / LPR;
     constexpr int BATCH = GROUPS * CU_ROWS;          // rows per block-batch
+    constexpr int RR = R > 0 ? R : 1;
     const int grp = threadIdx.x / LPR;
     const int sub = threadIdx.x % LPR;
     const long long nbatch = ((long long)M + BATCH - 1) / BATCH;
-    auto load_idx = [&](long long bt, long long (&yi)[CU_ROWS], long long (&ci)[CU_ROWS], long long (&vi)[CU_ROWS]) {
-#pragma unroll
-        for (int u = 0; u < CU_ROWS; ++u) {
-            const long long e = bt * BATCH + grp + (long long)u * GROUPS;
-            const bool ok = bt < nbatch && e < M;
-            yi[u] = ok ? (y_idx ? (long long)y_idx[e] : e) : 0;
-            ci[u] = ok ? (coef_idx ? (long long)coef_idx[e] : e) : 0;
-            vi[u] = ok ? (v_idx ? (long long)v_idx[e] : e) : 0;
-        }
-    };
-    long long yi[CU_ROWS], ci[CU_ROWS], vi[CU_ROWS];
+    const long long gstride = gridDim.x;
+    // indices of one batch (rows past M / batches past the end read row 0: harmless, never stored)
+    int yi[CU_ROWS], ci[CU_ROWS], vi[CU_ROWS];
+#define CB_LOAD_IDX(BT)                                                           \
+    _Pragma("unroll") for (int u = 0; u < CU_ROWS; ++u) {                          \
+        const long long e = (BT) * BATCH + grp + (long long)u * GROUPS;            \
+        const bool ok = (BT) < nbatch && e < M;                                    \
+        yi[u] = ok ? (y_idx ? y_idx[e] : (int)e) : 0;                              \
+        ci[u] = ok ? (coef_idx ? coef_idx[e] : (int)e) : 0;                        \
+        vi[u] = ok ? (v_idx ? v_idx[e] : (int)e) : 0;                              \
+    }
+#define CB_LOAD_ROWS(YV, PV, WV)                                                   \
+    _Pragma("unroll") for (int u = 0; u < CU_ROWS; ++u) {                          \
+        YV[u] = ld4(Y + (long long)yi[u] * D + sub * 4);                           \
+        _Pragma("unroll") for (int r = 0; r < R; ++r) {                            \
+            WV[r][u] = coef[(long long)ci[u] * R + r];                             \
+            PV[r][u] = ld4(V + r * v_rel_stride + (long long)vi[u] * D + sub * 4); \
+        }                                                                          \
+    }
+    f32x4 yc[CU_ROWS], pc[RR][CU_ROWS];
+    float wc[RR][CU_ROWS];
+#ifndef COMBINE_XCD
+#define COMBINE_XCD 0
+#endif
+    // XCD-aware order: blocks are dealt round-robin over the 8 XCDs, so logical block
+    // (b % 8) * (G / 8) + b / 8 gives each XCD a contiguous run of batches at every step
+    // (the tail rows they gather then live in ONE XCD's L2).
     long long bt = blockIdx.x;
-    load_idx(bt, yi, ci, vi);
-    for (; bt < nbatch; bt += gridDim.x) {
-        f32x4 v[CU_ROWS];
-#pragma unroll
-        for (int u = 0; u < CU_ROWS; ++u) v[u] = ld4(Y + yi[u] * D + sub * 4);
-        for (int r = 0; r < R; ++r) {
-            f32x4 pv[CU_ROWS];
-            float w[CU_ROWS];
-#pragma unroll
-            for (int u = 0; u < CU_ROWS; ++u) {
-                w[u] = coef[ci[u] * R + r];
-                pv[u] = ld4(V + r * v_rel_stride + vi[u] * D + sub * 4);
-            }
-#pragma unroll
-            for (int u = 0; u < CU_ROWS; ++u) v[u] += w[u] * pv[u];
-        }
-        long long yn[CU_ROWS], cn[CU_ROWS], vn[CU_ROWS];
-        load_idx(bt + gridDim.x, yn, cn, vn);
+    if (COMBINE_XCD && (gstride & 7) == 0) bt = (long long)(blockIdx.x & 7) * (gstride >> 3) + (blockIdx.x >> 3);
+    CB_LOAD_IDX(bt)
+    CB_LOAD_ROWS(yc, pc, wc)
+    CB_LOAD_IDX(bt + gstride)
+    for (; bt < nbatch; bt += gstride) {
+        f32x4 yn[CU_ROWS], pn[RR][CU_ROWS];
+        float wn[RR][CU_ROWS];
+        CB_LOAD_ROWS(yn, pn, wn)
+        CB_LOAD_IDX(bt + 2 * gstride)
 #pragma unroll
         for (int u = 0; u < CU_ROWS; ++u) {
+            f32x4 v = yc[u];
+#pragma unroll
+            for (int r = 0; r < R; ++r) v += wc[r][u] * pc[r][u];
             const long long e = bt * BATCH + grp + (long long)u * GROUPS;
             if (e < M) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[u][j] = sigmoid_fast(v[u][j]);
-                st4(out + e * D + sub * 4, v[u]);
+                for (int j = 0; j < 4; ++j) v[j] = sigmoid_fast(v[j]);
+                st4(out + e * D + sub * 4, v);
             }
-            yi[u] = yn[u];
-            ci[u] = cn[u];
-            vi[u] = vn[u];
         }
+#pragma unroll
+        for (int u = 0; u < CU_ROWS; ++u) {
+            yc[u] = yn[u];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                pc[r][u] = pn[r][u];
+                wc[r][u] = wn[r][u];
+            }
+        }
+    }
+#undef CB_LOAD_IDX
+#undef CB_LOAD_ROWS
+}
+
+// Run combine, D = 256, shared row index (y_idx == v_idx, typically tail-sorted edges):
+// out[e] = sigmoid(Y[t_e] + sum_r coef[e][r] * V_r[t_e]).  One wave per 64-edge chunk, one
+// row per wave instruction.  Consecutive edges with the same t form a run; the node rows
+// (Y, V_r) are loaded once per run, and the NEXT run's rows (or the next chunk's first run)
+// are issued before the current run's stores, so the only loads a store ever sits in front
+// of are the ones already needed.  Per-edge indices/coefficients: one per lane, broadcast
+// with readlane.
+constexpr int RC_CH = 64;
+template <int R>
+__global__ __launch_bounds__(256) void run_combine256_kernel(int M, const float* __restrict__ Y,
+                                                             const int* __restrict__ idx,
+                                                             const float* __restrict__ coef,
+                                                             const float* __restrict__ V, long long v_rel_stride,
+                                                             float* __restrict__ out) {
+    constexpr int D = 256;
+    constexpr int RR = R > 0 ? R : 1;
+    const int lane = threadIdx.x & 63;
+    const long long nchunk = ((long long)M + RC_CH - 1) / RC_CH;
+    const long long wstride = (long long)gridDim.x * 4;
+    long long c = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= nchunk) return;
+    // per-lane edge state of a chunk
+    auto load_chunk = [&](long long ch, int& tv, float (&cf)[RR]) {
+        const long long e = ch * RC_CH + lane;
+        const bool ok = ch < nchunk && e < M;
+        tv = ok ? idx[e] : -1;
+#pragma unroll
+        for (int r = 0; r < R; ++r) cf[r] = ok ? coef[e * R + r] : 0.f;
+    };
+    int tv;
+    float cf[RR];
+    load_chunk(c, tv, cf);
+    f32x4 yc, pc[RR], yn, pn[RR];
+    auto load_rows = [&](int t, f32x4& yv, f32x4 (&pv)[RR]) {
+        yv = ld4(Y + (long long)t * D + lane * 4);
+#pragma unroll
+        for (int r = 0; r < R; ++r) pv[r] = ld4(V + r * v_rel_stride + (long long)t * D + lane * 4);
+    };
+    load_rows(__builtin_amdgcn_readfirstlane(tv), yc, pc);
+    for (; c < nchunk; c += wstride) {
+        const long long e0 = c * RC_CH;
+        const int nvalid = (int)((long long)M - e0 < RC_CH ? (long long)M - e0 : RC_CH);
+        const int tprev = __shfl_up(tv, 1, 64);
+        unsigned long long starts = __ballot(lane < nvalid && (lane == 0 || tv != tprev));
+        starts &= starts - 1;                          // run 0 is already loaded
+        // next chunk's per-lane state, issued now (tiny loads, long before they are needed)
+        int tv_n;
+        float cf_n[RR];
+        load_chunk(c + wstride, tv_n, cf_n);
+        int cur = 0;
+        while (true) {
+            int next;
+            if (starts) {
+                next = __builtin_ctzll(starts);
+                starts &= starts - 1;
+                load_rows(__builtin_amdgcn_readlane(tv, next), yn, pn);
+            } else {
+                next = nvalid;
+                if (c + wstride < nchunk) load_rows(__builtin_amdgcn_readfirstlane(tv_n), yn, pn);
+            }
+            for (int j = cur; j < next; ++j) {
+                f32x4 v = yc;
+#pragma unroll
+                for (int r = 0; r < R; ++r) v += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cf[r]), j)) * pc[r];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
+                st4(out + (e0 + j) * D + lane * 4, v);
+            }
+            yc = yn;
+#pragma unroll
+            for (int r = 0; r < R; ++r) pc[r] = pn[r];
+            if (next >= nvalid) break;
+            cur = next;
+        }
+        tv = tv_n;
+#pragma unroll
+        for (int r = 0; r < R; ++r) cf[r] = cf_n[r];
     }
 }
 
@@ -1062,32 +1269,45 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
     for (int r = 0; r < MAX_R; ++r) dr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
     float lacc = 0.f;
 
-    // two rows per group per iteration, all loads issued before any use (same visit order as a
-    // plain grid-stride loop, so the drel / loss partial sums are order-identical)
+    // U rows per group per iteration (same visit order as a plain grid-stride loop, so the
+    // drel / loss partial sums are order-identical).  Software-pipelined: the rows of the next
+    // iteration and the indices of the one after are issued before this iteration's stores
+    // (vmcnt counts loads and stores together, in order).
     constexpr int U = 2;
     const long long stride = (long long)gridDim.x * GROUPS;
-    for (long long e0 = (long long)blockIdx.x * GROUPS + grp; e0 < T; e0 += U * stride) {
-        long long e[U];
-        int hr[U], rr[U];
-        long long ti[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            e[u] = e0 + u * stride;
-            const bool ok = e[u] < T;
-            hr[u] = ok ? h_idx[e[u]] : 0;
-            rr[u] = ok ? r_idx[e[u]] : 0;
-            ti[u] = ok ? (t_idx ? (long long)t_idx[e[u]] : e[u]) : 0;
-        }
-        f32x4 a[U], b[U], rho[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            a[u] = ld4(Xh + (long long)hr[u] * D + sub * 4);
-            b[u] = ld4(Xt + ti[u] * D + sub * 4);
-            rho[u] = ld4(rel + (long long)rr[u] * D + sub * 4);
-        }
-        float yy[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) yy[u] = (train && e[u] < T) ? y[e[u]] : 0.f;
+    int hr[U], rr[U];
+    long long ti[U];
+    float yv[U];
+#define DM_LOAD_IDX(E0)                                                        \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                             \
+        const long long ee = (E0) + u * stride;                                 \
+        const bool ok = ee < T;                                                 \
+        hr[u] = ok ? h_idx[ee] : 0;                                             \
+        rr[u] = ok ? r_idx[ee] : 0;                                             \
+        ti[u] = ok ? (t_idx ? (long long)t_idx[ee] : ee) : 0;                   \
+        yv[u] = (train && ok) ? y[ee] : 0.f;                                    \
+    }
+#define DM_LOAD_ROWS(A, B, RHO, YY, RI)                                        \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                             \
+        A[u] = ld4(Xh + (long long)hr[u] * D + sub * 4);                        \
+        B[u] = ld4(Xt + ti[u] * D + sub * 4);                                   \
+        RHO[u] = ld4(rel + (long long)rr[u] * D + sub * 4);                     \
+        YY[u] = yv[u];                                                          \
+        RI[u] = rr[u];                                                          \
+    }
+    long long e0 = (long long)blockIdx.x * GROUPS + grp;
+    f32x4 a[U], b[U], rho[U];
+    float yy[U];
+    int rc[U];
+    DM_LOAD_IDX(e0)
+    DM_LOAD_ROWS(a, b, rho, yy, rc)
+    DM_LOAD_IDX(e0 + U * stride)
+    for (; e0 < T; e0 += U * stride) {
+        f32x4 an[U], bn[U], rhon[U];
+        float yn[U];
+        int rn[U];
+        DM_LOAD_ROWS(an, bn, rhon, yn, rn)
+        DM_LOAD_IDX(e0 + 2 * U * stride)
         float sc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1096,9 +1316,10 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (e[u] >= T) continue;
+            const long long e = e0 + u * stride;
+            if (e >= T) continue;
             const float p = sigmoidf_(sc[u]);
-            if (p_out && sub == 0) p_out[e[u]] = p;
+            if (p_out && sub == 0) p_out[e] = p;
             if (!train) continue;
             const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
             const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
@@ -1106,18 +1327,28 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
                 pass ? scale * (-(yy[u] / (pc + EPS_BCE)) + (1.0f - yy[u]) / (1.0f - pc + EPS_BCE)) : 0.f;
             const float ds = g * p * (1.0f - p);
             if (sub == 0) {
-                ds_out[e[u]] = ds;
+                ds_out[e] = ds;
                 lacc += -(yy[u] * logf(pc + EPS_BCE) + (1.0f - yy[u]) * logf(1.0f - pc + EPS_BCE));
             }
             f32x4 dx = (ds * rho[u]) * a[u];
             dx = dx * (b[u] * (1.0f - b[u]));
-            st4(do_out + e[u] * D + sub * 4, dx);
+            st4(do_out + e * D + sub * 4, dx);
             const f32x4 dre = ds * (a[u] * b[u]);
 #pragma unroll
             for (int r = 0; r < MAX_R; ++r)
-                if (r == rr[u]) dr[r] += dre;
+                if (r == rc[u]) dr[r] += dre;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = an[u];
+            b[u] = bn[u];
+            rho[u] = rhon[u];
+            yy[u] = yn[u];
+            rc[u] = rn[u];
         }
     }
+#undef DM_LOAD_IDX
+#undef DM_LOAD_ROWS
     if (!train) return;
 #pragma unroll
     for (int r = 0; r < MAX_R; ++r)
@@ -1194,7 +1425,10 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
                                                               float* __restrict__ dP, long long dp_rel_stride,
                                                               float* __restrict__ dsum, float* __restrict__ dWedge) {
     constexpr int LPR = D / 4;
-    constexpr int U = 4;
+#ifndef TS_U
+#define TS_U 4
+#endif
+    constexpr int U = TS_U;
     const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
     const int sub = threadIdx.x % LPR;
     const bool live = n < n_nodes;
@@ -1572,15 +1806,43 @@ int iddgcn_combine_f32(void* stream, int M, int d, int R, const float* Y, const 
     if (M < 0 || !Y || !out || (R > 0 && (!coef || !V))) return IDDGCN_E_BAD_ARG;
     if (M == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    if (d == 256 && y_idx && y_idx == v_idx && !coef_idx && R <= 4) {
+        const long long nchunk = ((long long)M + RC_CH - 1) / RC_CH;
+        long long nb = (nchunk + 3) / 4;
+        if (nb > 2048) nb = 2048;
+#define RCK(RR) hipLaunchKernelGGL((run_combine256_kernel<RR>), dim3((unsigned)nb), dim3(256), 0, st, M, Y, y_idx, coef, V, v_rel_stride, out)
+        switch (R) {
+            case 0: RCK(0); break;
+            case 1: RCK(1); break;
+            case 2: RCK(2); break;
+            case 3: RCK(3); break;
+            default: RCK(4); break;
+        }
+#undef RCK
+        return launch_status();
+    }
     const long long nbatch = ((long long)M + (256 / (d / 4)) * CU_ROWS - 1) / ((256 / (d / 4)) * CU_ROWS);
     const unsigned grid = (unsigned)(nbatch < CU_BLOCKS ? nbatch : CU_BLOCKS);
-#define CK(DD) hipLaunchKernelGGL(combine_kernel<DD>, dim3(grid), dim3(256), 0, st, M, R, Y, y_idx, coef, coef_idx, V, v_idx, v_rel_stride, out)
-    switch (d) {
-        case 32: CK(32); break;
-        case 64: CK(64); break;
-        case 128: CK(128); break;
-        default: CK(256); break;
+#define CK(DD, RR) hipLaunchKernelGGL((combine_kernel<DD, RR>), dim3(grid), dim3(256), 0, st, M, Y, y_idx, coef, coef_idx, V, v_idx, v_rel_stride, out)
+#define CKR(DD)                    \
+    switch (R) {                   \
+        case 0: CK(DD, 0); break;  \
+        case 1: CK(DD, 1); break;  \
+        case 2: CK(DD, 2); break;  \
+        case 3: CK(DD, 3); break;  \
+        case 4: CK(DD, 4); break;  \
+        case 5: CK(DD, 5); break;  \
+        case 6: CK(DD, 6); break;  \
+        case 7: CK(DD, 7); break;  \
+        default: CK(DD, 8); break; \
     }
+    switch (d) {
+        case 32: CKR(32); break;
+        case 64: CKR(64); break;
+        case 128: CKR(128); break;
+        default: CKR(256); break;
+    }
+#undef CKR
 #undef CK
     return launch_status();
 }

@@ -187,6 +187,33 @@ def test_combine(D, cuda):
     close(out, torch.sigmoid(ref), 1e-5)
 
 
+@pytest.mark.parametrize("R", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M,order", [(1, "sorted"), (63, "sorted"), (65, "unsorted"), (20_011, "sorted"),
+                                     (20_011, "unsorted"), (20_011, "one_run")])
+def test_combine_runs(R, M, order, cuda):
+    """Run-combine path (D = 256, y_idx is v_idx, per-edge coef): equal to torch and bitwise to the
+    generic edge-parallel kernel (reached by passing a copy of the index as v_idx)."""
+    g = torch.Generator().manual_seed(1000 * R + M)
+    N, D = 300, 256
+    Y, P = rnd(N, D, dev=cuda, gen=g).float(), rnd(max(R, 1), N, D, dev=cuda, gen=g).float()[:R]
+    W = torch.rand(M, R, generator=g).to(cuda)
+    t = torch.randint(0, N, (M,), generator=g)
+    if order == "sorted":
+        t = t.sort().values
+    elif order == "one_run":
+        t = torch.full((M,), 7)
+    t = t.to(cuda).int()
+    out = torch.empty(M, D, device=cuda)
+    ops.combine(Y, W, P, out, y_idx=t, v_idx=t, v_rel_stride=N * D)
+    ref = Y.double()[t.long()]
+    for r in range(R):
+        ref = ref + W.double()[:, r:r + 1] * P.double()[r][t.long()]
+    close(out, torch.sigmoid(ref), 1e-5)
+    out2 = torch.empty_like(out)
+    ops.combine(Y, W, P, out2, y_idx=t, v_idx=t.clone(), v_rel_stride=N * D)
+    assert torch.equal(out, out2)
+
+
 @pytest.mark.parametrize("D", DIMS)
 def test_distmult_bce_matches_autograd(D, cuda):
     g = torch.Generator().manual_seed(31 + D)
