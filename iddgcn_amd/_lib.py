@@ -47,6 +47,8 @@ SIGNATURES = {
     "iddgcn_combine_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cll, vp]),
     "iddgcn_distmult_blocks": (ci, [cll]),
     "iddgcn_distmult_bce_f32": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, ci]),
+    "iddgcn_distmult_bce_heads_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
+                                           ci]),
     "iddgcn_seg_gather_reduce_f32": (ci, [vp, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iddgcn_tail_seg_reduce_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, cll, vp, cll, vp, vp]),
     "iddgcn_head_bwd_node_f32": (ci, [vp, ci, ci, ci, vp, vp, cll, vp, vp, vp, vp, vp, vp, cll, vp, vp]),

@@ -155,6 +155,9 @@ __device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ f32x4 fma4(f32x4 a, f32x4 b, f32x4 c) {
+    return f32x4{fmaf(a[0], b[0], c[0]), fmaf(a[1], b[1], c[1]), fmaf(a[2], b[2], c[2]), fmaf(a[3], b[3], c[3])};
+}
 
 inline int launch_status() {
     hipError_t e = hipGetLastError();
@@ -1369,6 +1372,115 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
 }
 
 // ---------------------------------------------------------------------------
+// DistMult + Keras BCE + both backward seeds, one pass over edges grouped by HEAD.
+// A lane group owns one head node at a time (persistent loop): Xh[n] is read once, each edge's
+// tail row Xt[e] once (the tail-seed do_out[e] is written from it), and the head seed
+// dXh[n] = Xh(1-Xh) * sum ds_e rel[r_e] Xt[e] accumulates in registers in perm order.  Per-edge
+// arithmetic is that of distmult_kernel + seg_gather_reduce_kernel, so p / ds / do / dXh are
+// bitwise the same; only the drel / loss partial sums visit edges in another order.
+// ---------------------------------------------------------------------------
+template <int D, int RT>
+__global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R, const int* __restrict__ seg_ptr,
+                                                             const int* __restrict__ perm,
+                                                             const float* __restrict__ Xh,
+                                                             const float* __restrict__ Xt,
+                                                             const int* __restrict__ r_idx,
+                                                             const float* __restrict__ rel,
+                                                             const float* __restrict__ y, float scale,
+                                                             float* __restrict__ p_out, float* __restrict__ ds_out,
+                                                             float* __restrict__ do_out, float* __restrict__ dXh,
+                                                             float* __restrict__ drel_slab,
+                                                             float* __restrict__ loss_slab) {
+    constexpr int LPR = D / 4;
+    constexpr int GROUPS = 256 / LPR;
+    constexpr int U = 4;
+    __shared__ __attribute__((aligned(16))) float red[GROUPS * RT * D];
+    __shared__ float lred[GROUPS];
+    const int grp = threadIdx.x / LPR;
+    const int sub = threadIdx.x % LPR;
+    f32x4 dr[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) dr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float lacc = 0.f;
+    const long long nstride = (long long)gridDim.x * GROUPS;
+    for (long long n0 = (long long)blockIdx.x * GROUPS; n0 < n_nodes; n0 += nstride) {
+        const long long n = n0 + grp;
+        const bool live = n < n_nodes;
+        const int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
+        const int len = end - beg;
+        int maxlen = len;       // groups of one wave may hold different nodes (D < 256)
+        if (LPR < 64) {
+#pragma unroll
+            for (int m = 32; m >= LPR; m >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, m, 64));
+        }
+        const f32x4 a = live ? ld4(Xh + n * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < maxlen; k += U) {
+            long long e[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) e[u] = (k + u < len) ? (long long)perm[beg + k + u] : -1;
+            int rr[U];
+            float yy[U];
+            f32x4 b[U], rho[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool ok = e[u] >= 0;
+                rr[u] = ok ? r_idx[e[u]] : 0;
+                yy[u] = ok ? y[e[u]] : 0.f;
+                b[u] = ok ? ld4(Xt + e[u] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) rho[u] = ld4(rel + (long long)rr[u] * D + sub * 4);
+            float sc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const f32x4 prod = a * rho[u] * b[u];
+                sc[u] = group_sum<LPR>(prod[0] + prod[1] + prod[2] + prod[3]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (e[u] < 0) continue;
+                const float p = sigmoidf_(sc[u]);
+                if (p_out && sub == 0) p_out[e[u]] = p;
+                const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
+                const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
+                const float g =
+                    pass ? scale * (-(yy[u] / (pc + EPS_BCE)) + (1.0f - yy[u]) / (1.0f - pc + EPS_BCE)) : 0.f;
+                const float ds = g * p * (1.0f - p);
+                if (sub == 0) {
+                    if (ds_out) ds_out[e[u]] = ds;
+                    lacc += -(yy[u] * logf(pc + EPS_BCE) + (1.0f - yy[u]) * logf(1.0f - pc + EPS_BCE));
+                }
+                f32x4 dx = (ds * rho[u]) * a;
+                dx = dx * (b[u] * (1.0f - b[u]));
+                st4(do_out + e[u] * D + sub * 4, dx);
+                const f32x4 dre = ds * (a * b[u]);
+#pragma unroll
+                for (int r = 0; r < RT; ++r)
+                    if (r == rr[u]) dr[r] += dre;
+                acc = fma4(b[u] * ds, rho[u], acc);     // same explicit fma as seg_gather_reduce
+            }
+        }
+        if (live) st4(dXh + n * D + sub * 4, acc * (a * (1.0f - a)));
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r) st4(red + (grp * RT + r) * D + sub * 4, dr[r]);
+    if (sub == 0) lred[grp] = lacc;
+    __syncthreads();
+    for (int x = threadIdx.x; x < R * D; x += 256) {
+        const int r = x / D, c = x % D;
+        float s = 0.f;
+        for (int gq = 0; gq < GROUPS; ++gq) s += red[(gq * RT + r) * D + c];
+        drel_slab[(long long)blockIdx.x * R * D + x] = s;
+    }
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int gq = 0; gq < GROUPS; ++gq) s += lred[gq];
+        loss_slab[blockIdx.x] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // segmented gather-reduce (head side): out[n] = dsig * sum coef[e] rel[r_e] rows[e]
 // ---------------------------------------------------------------------------
 template <int D>
@@ -1388,7 +1500,7 @@ __global__ __launch_bounds__(256) void seg_gather_reduce_kernel(int n_nodes, con
     constexpr int U = 4;
     for (int k0 = beg; k0 < end; k0 += U) {
         long long e[U];
-        f32x4 v[U];
+        f32x4 v[U], q[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) e[u] = (k0 + u < end) ? (perm ? (long long)perm[k0 + u] : (long long)(k0 + u)) : -1;
 #pragma unroll
@@ -1396,11 +1508,13 @@ __global__ __launch_bounds__(256) void seg_gather_reduce_kernel(int n_nodes, con
             if (e[u] < 0) continue;
             v[u] = ld4(rows + e[u] * D + sub * 4);
             if (coef) v[u] *= coef[e[u]];
-            if (rel) v[u] *= ld4(rel + (long long)r_idx[e[u]] * D + sub * 4);
+            if (rel) q[u] = ld4(rel + (long long)r_idx[e[u]] * D + sub * 4);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (e[u] >= 0) acc += v[u];
+        for (int u = 0; u < U; ++u) {
+            if (e[u] < 0) continue;
+            acc = rel ? fma4(v[u], q[u], acc) : acc + v[u];   // explicit fma: no contraction ambiguity
+        }
     }
     if (X) {
         const f32x4 x = ld4(X + n * D + sub * 4);
@@ -1871,6 +1985,35 @@ int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R, const float
         default: DK(256); break;
     }
 #undef DK
+    return launch_status();
+}
+
+int iddgcn_distmult_bce_heads_f32(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* perm,
+                                  const float* Xh, const float* Xt, const int* r_idx, const float* rel,
+                                  const float* y, float scale, float* p_out, float* ds_out, float* do_out,
+                                  float* dXh, float* drel_slab, float* loss_slab, int n_blocks) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (n_nodes < 0 || n_blocks < 1 || !seg_ptr || !perm || !Xh || !Xt || !r_idx || !rel || !y || !do_out ||
+        !dXh || !drel_slab || !loss_slab)
+        return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+#define HK(DD, RT) hipLaunchKernelGGL((distmult_heads_kernel<DD, RT>), dim3(n_blocks), dim3(256), 0, st, n_nodes, R, seg_ptr, perm, Xh, Xt, r_idx, rel, y, scale, p_out, ds_out, do_out, dXh, drel_slab, loss_slab)
+#define HKR(DD)                                            \
+    {                                                      \
+        if (R <= 1) HK(DD, 1);                             \
+        else if (R <= 2) HK(DD, 2);                        \
+        else if (R <= 4) HK(DD, 4);                        \
+        else HK(DD, 8);                                    \
+    }
+    switch (d) {
+        case 32: HKR(32); break;
+        case 64: HKR(64); break;
+        case 128: HKR(128); break;
+        default: HKR(256); break;
+    }
+#undef HKR
+#undef HK
     return launch_status();
 }
 

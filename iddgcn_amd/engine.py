@@ -111,7 +111,6 @@ class Workspace:
         self.train = train
         if not train:
             return
-        self.ds = e(T)
         self.dE_a = e(T, D)                     # edge-level grads, ping-pong
         self.dE_b = e(T, D)
         self.dWedge = e(T, R)
@@ -201,22 +200,22 @@ class Engine:
                             v_rel_stride=N * D, act=L.ACT_SIGMOID)
         # DistMult (+ BCE and backward seed when training)
         if train:
+            # one pass over head segments: p / loss / drel partials, the tail seed do^3 (per edge)
+            # and the head seed dO^3[n] = X3(1-X3) * sum_{h_e=n} ds_e rel[r_e] * x3_e
             scale = 1.0 / (float(self._t_global or T) * float(N))
-            ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], y=ed.y, scale=scale, p_out=ws.p,
-                             ds_out=ws.ds, do_out=ws.dE_a, drel_slab=ws.drel_slab, loss_slab=ws.loss_slab)
+            ops.distmult_bce_heads(ed.hptr, ed.hperm, ws.X[2], ws.xt[2], ed.r, P["rel"], ed.y, ws.dE_a, ws.dOn_a,
+                                   ws.drel_slab, ws.loss_slab, scale=scale, p_out=ws.p if self._want_p else None)
         else:
             ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], p_out=ws.p)
 
     _t_global = None
+    _want_p = False        # per-edge probabilities are only materialised for loss_and_grads
 
     # -- backward -----------------------------------------------------------
     def backward(self, P, G, adj, ed, ws):
         N, R, D = self.N, self.R, self.D
-        # head-side seed: dO^3[n] = X3(1-X3) * sum_{h_e=n} ds_e rel[r_e] * x3_e
-        dOn, dOn_next = ws.dOn_a, ws.dOn_b
-        ops.seg_gather_reduce(ed.hptr, ws.xt[2], dOn, perm=ed.hperm, coef=ws.ds, r_idx=ed.r, rel=P["rel"],
-                              X=ws.X[2])
-        do, do_next = ws.dE_a, ws.dE_b          # do^3 written by distmult
+        dOn, dOn_next = ws.dOn_a, ws.dOn_b      # head seed dO^3, written by distmult_bce_heads
+        do, do_next = ws.dE_a, ws.dE_b          # tail seed do^3, written by distmult_bce_heads
         for l in (2, 1, 0):                     # layer index l -> reference layer l+1
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
             # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part
@@ -277,7 +276,11 @@ class Engine:
     def loss_and_grads(self, params, grads, adj, ed, t_global=None):
         ws = self.workspace(ed.T, True)
         self._t_global = t_global
-        self.forward(params, adj, ed, ws, True)
+        self._want_p = True
+        try:
+            self.forward(params, adj, ed, ws, True)
+        finally:
+            self._want_p = False
         self.backward(params, grads, adj, ed, ws)
         return ws.loss, ed.unsort(ws.p)
 

@@ -168,6 +168,33 @@ def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_
     return nb
 
 
+def distmult_bce_heads(seg_ptr, perm, Xh, Xt, r_idx, rel, y, do_out, dXh, drel_slab, loss_slab, *, scale=1.0,
+                      p_out=None, ds_out=None):
+    """Training DistMult + BCE + tail seed (do_out) + head seed (dXh) in one pass over head segments."""
+    T = r_idx.shape[0]
+    n_nodes, D = dXh.shape
+    R = rel.shape[0]
+    _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")
+    _req(perm, _I32, (T,), "perm")
+    _req(r_idx, _I32, (T,), "r_idx")
+    _req(Xh, _F32, (n_nodes, D), "Xh")
+    _req(Xt, _F32, (T, D), "Xt")
+    _req(rel, _F32, (R, D), "rel")
+    _req(y, _F32, (T,), "y")
+    _req(do_out, _F32, (T, D), "do_out")
+    _req(dXh, _F32, (n_nodes, D), "dXh")
+    _req(p_out, _F32, (T,), "p_out")
+    _req(ds_out, _F32, (T,), "ds_out")
+    nb = distmult_blocks(T)
+    if drel_slab.numel() < nb * R * D or loss_slab.numel() < nb:
+        raise L.IddgcnError("distmult slabs too small")
+    L.check(L.lib().iddgcn_distmult_bce_heads_f32(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(perm), _ptr(Xh),
+                                                  _ptr(Xt), _ptr(r_idx), _ptr(rel), _ptr(y), float(scale),
+                                                  _ptr(p_out), _ptr(ds_out), _ptr(do_out), _ptr(dXh),
+                                                  _ptr(drel_slab), _ptr(loss_slab), nb), "distmult_bce_heads")
+    return nb
+
+
 def seg_gather_reduce(seg_ptr, rows, out, *, perm=None, coef=None, r_idx=None, rel=None, X=None):
     n_nodes, D = out.shape
     _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")

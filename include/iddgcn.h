@@ -119,6 +119,23 @@ int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R,
                             float* p_out, float* ds_out, float* do_out,
                             float* drel_slab, float* loss_slab, int n_blocks);
 
+/* Training form of the above that also produces the head-side seed, in ONE pass over the
+ * scored edges grouped by head (seg_ptr/perm: head segments, perm in edge order within a head):
+ * for head node n and e = perm[k], k in [seg_ptr[n], seg_ptr[n+1]), with a = Xh[n], b = Xt[e]:
+ * p_out / ds_out (both optional), do_out, drel_slab and loss_slab exactly as
+ * iddgcn_distmult_bce_f32 (t_idx = NULL), and
+ *   dXh[n][c] = a(1-a) * sum_k (b[c]*ds_e)*rel[r_idx[e]][c]     (summed in perm order)
+ * which is iddgcn_seg_gather_reduce_f32(seg_ptr, perm, ds, r_idx, rel, Xt, Xh).  Rows of nodes with
+ * no edge get zeros.  n_blocks from iddgcn_distmult_blocks(); the drel / loss partials are
+ * per block, as for iddgcn_distmult_bce_f32.
+ * Replaces IDDGCN.py:103-109 + the loss of 161-168 and the head-side gradient of
+ * DistMult's embedding lookup, one launch. */
+int iddgcn_distmult_bce_heads_f32(void* stream, int n_nodes, int d, int R, const int* seg_ptr,
+                                  const int* perm, const float* Xh, const float* Xt, const int* r_idx,
+                                  const float* rel, const float* y, float scale, float* p_out,
+                                  float* ds_out, float* do_out, float* dXh, float* drel_slab,
+                                  float* loss_slab, int n_blocks);
+
 /* Deterministic segmented gather-reduce (replaces the UnsortedSegmentSum of
  * embedding_lookup's gradient): for node n,
  *   out[n][c] = (dsig ? X[n][c](1-X[n][c]) : 1)

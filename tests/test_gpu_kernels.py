@@ -253,6 +253,53 @@ def test_distmult_bce_matches_autograd(D, cuda):
 
 
 @pytest.mark.parametrize("D", DIMS)
+@pytest.mark.parametrize("R,skew", [(1, False), (3, True), (5, False)])
+def test_distmult_bce_heads_fused(D, R, skew, cuda):
+    """One-pass head-grouped form == distmult_bce + seg_gather_reduce: p / ds / do / dXh bitwise,
+    drel / loss to rounding (partial sums visit edges in head order)."""
+    g = torch.Generator().manual_seed(41 + D + R)
+    N, T = 300, 7001
+    Xh = torch.rand(N, D, generator=g).to(cuda)
+    Xt = torch.rand(T, D, generator=g).to(cuda)
+    rel = (torch.randn(R, D, generator=g) * 0.3).to(cuda)
+    if skew:   # a few very hot heads, many heads without edges
+        h = torch.where(torch.rand(T, generator=g) < 0.5, torch.randint(0, 3, (T,), generator=g),
+                        torch.randint(0, N // 2, (T,), generator=g))
+    else:
+        h = torch.randint(0, N, (T,), generator=g)
+    r = torch.randint(0, R, (T,), generator=g)
+    y = (torch.rand(T, generator=g) < 0.5).float().to(cuda)
+    hperm = torch.argsort(h, stable=True)
+    hptr = torch.searchsorted(h[hperm], torch.arange(N + 1), right=False).to(torch.int32).to(cuda)
+    h, r, hperm = h.int().to(cuda), r.int().to(cuda), hperm.int().to(cuda)
+    scale = 1.0 / (T * N)
+    nb = ops.distmult_blocks(T)
+    p, ds, do = torch.empty(T, device=cuda), torch.empty(T, device=cuda), torch.empty(T, D, device=cuda)
+    sl_r, sl_l = torch.empty(nb * R * D, device=cuda), torch.empty(nb, device=cuda)
+    ops.distmult_bce(Xh, h, Xt, r, rel, y=y, scale=scale, p_out=p, ds_out=ds, do_out=do, drel_slab=sl_r,
+                     loss_slab=sl_l)
+    dXh = torch.empty(N, D, device=cuda)
+    ops.seg_gather_reduce(hptr, Xt, dXh, perm=hperm, coef=ds, r_idx=r, rel=rel, X=Xh)
+    drel, loss = torch.empty(R, D, device=cuda), torch.empty(1, device=cuda)
+    ops.reduce_slabs(sl_r, nb, drel)
+    ops.reduce_slabs(sl_l, nb, loss)
+
+    p2, ds2 = torch.full((T,), 7.0, device=cuda), torch.full((T,), 7.0, device=cuda)
+    do2, dXh2 = torch.full((T, D), 7.0, device=cuda), torch.full((N, D), 7.0, device=cuda)
+    sl_r2, sl_l2 = torch.empty(nb * R * D, device=cuda), torch.empty(nb, device=cuda)
+    ops.distmult_bce_heads(hptr, hperm, Xh, Xt, r, rel, y, do2, dXh2, sl_r2, sl_l2, scale=scale, p_out=p2,
+                           ds_out=ds2)
+    drel2, loss2 = torch.empty(R, D, device=cuda), torch.empty(1, device=cuda)
+    ops.reduce_slabs(sl_r2, nb, drel2)
+    ops.reduce_slabs(sl_l2, nb, loss2)
+    assert torch.equal(p, p2) and torch.equal(ds, ds2)
+    assert torch.equal(do, do2)
+    assert torch.equal(dXh, dXh2)           # includes zero rows of heads without edges
+    close(drel2, drel.double(), 1e-5)
+    assert abs(loss2.item() - loss.item()) <= 1e-5 * abs(loss.item())
+
+
+@pytest.mark.parametrize("D", DIMS)
 def test_segment_reductions(D, cuda):
     """seg_gather_reduce / tail_seg_reduce / head_bwd_node against index_add references."""
     g = torch.Generator().manual_seed(37 + D)

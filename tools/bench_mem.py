@@ -43,6 +43,10 @@ def inputs(T=4_000_000, N=100_000, D=256, R=2):
     x["y"] = (torch.rand(T, device=dev, generator=g) > 0.5).float()
     cnt = torch.bincount(t, minlength=N)
     x["tptr"] = torch.cat([torch.zeros(1, dtype=torch.long, device=dev), torch.cumsum(cnt, 0)]).int()
+    hperm = torch.argsort(x["h"].long(), stable=True)
+    x["hperm"] = hperm.int()
+    x["hptr"] = torch.searchsorted(x["h"].long()[hperm], torch.arange(N + 1, device=dev), right=False).int()
+    x["dXh"] = torch.empty(N, D, device=dev)
     x["dP"] = torch.empty(R, N, D, device=dev)
     x["dW"] = torch.empty(T, R, device=dev)
     x["ds"] = torch.empty(T, device=dev)
@@ -67,6 +71,14 @@ def run(libpath, x):
         "distmult": (lambda: ops.distmult_bce(x["Xh"], x["h"], x["A"], x["r"], x["rel"], y=x["y"], scale=1e-5,
                                               ds_out=x["ds"], do_out=x["C"], drel_slab=x["drel_slab"],
                                               loss_slab=x["loss_slab"]), 2 * gb),
+        "dm+seg_gather": (lambda: (ops.distmult_bce(x["Xh"], x["h"], x["A"], x["r"], x["rel"], y=x["y"], scale=1e-5,
+                                                    ds_out=x["ds"], do_out=x["C"], drel_slab=x["drel_slab"],
+                                                    loss_slab=x["loss_slab"]),
+                                   ops.seg_gather_reduce(x["hptr"], x["A"], x["dXh"], perm=x["hperm"], coef=x["ds"],
+                                                         r_idx=x["r"], rel=x["rel"], X=x["Xh"])), 3 * gb),
+        "dm_heads": (lambda: ops.distmult_bce_heads(x["hptr"], x["hperm"], x["Xh"], x["A"], x["r"], x["rel"], x["y"],
+                                                    x["C"], x["dXh"], x["drel_slab"], x["loss_slab"], scale=1e-5),
+                     2 * gb),
         "tail_seg": (lambda: ops.tail_seg_reduce(x["tptr"], None, x["Wedge"], x["A"], x["P"], x["dP"], x["dW"]), gb),
     }
     res = []
