@@ -11,6 +11,7 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 ABI_VERSION = 1
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
+GEMM_EXACT_F32, GEMM_SPLIT_F16 = 0, 1
 
 vp = ctypes.c_void_p
 ci = ctypes.c_int
@@ -39,6 +40,7 @@ SIGNATURES = {
     "iddgcn_spmm_csr_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, ci]),
     "iddgcn_rowgemm_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
     "iddgcn_set_rowgemm_path": (ci, [ci]),
+    "iddgcn_set_gemm_precision": (ci, [ci]),
     "iddgcn_gemm_tn_blocks": (ci, [cll, ci]),
     "iddgcn_gemm_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
     "iddgcn_gemm_tn_narrow_blocks": (ci, [cll]),

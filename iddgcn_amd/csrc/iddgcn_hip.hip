@@ -21,6 +21,8 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 #define MAX_R 8
 #define EPS_BCE 1e-7f
@@ -167,6 +169,9 @@ inline bool dim_ok(int d) { return d == 32 || d == 64 || d == 128 || d == 256; }
 // test/bench hook selecting the D=256 GEMM pipelines: 0 = best (v3 row GEMM, DMA TN),
 // 1 = register-staged kernels, 2 = v2 DMA row GEMM
 static int g_rowgemm_path = 0;
+// D=256 GEMM operand precision: 0 = exact f32 MFMA (bitwise an fmaf chain), 1 = split-fp16
+// operands (hi + lo*2^-11 per value, 3 f16 MFMAs per k-step, fp32 accumulation)
+static int g_gemm_split = 0;
 
 // ---------------------------------------------------------------------------
 // CSR SpMM: one row per group of D/4 lanes, sequential sum in CSR order.
@@ -540,11 +545,48 @@ constexpr int NS_MAX = 2;
 constexpr int COEF = 64;                               // 32 rows x R (R <= 2)
 constexpr int IDX = 64;                                // next tile's v_idx (32) + coef_idx (32)
 constexpr int CMP = 32;                                // distinct V rows of the tile (run starts)
-constexpr int WAVE_FLOATS = NS_MAX * SLAB + COEF + IDX + CMP;
-constexpr int LDS_FLOATS = 2 * A_FLOATS + NW * WAVE_FLOATS;   // 130 KiB
+constexpr int CINV = 32;                               // split mode: 1/scale of the wave's 32 columns
+constexpr int WAVE_FLOATS = NS_MAX * SLAB + COEF + IDX + CMP + CINV;
+constexpr int ROWINV = 2 * TR;                         // split mode: 1/scale of each A row, per buffer
+constexpr int LDS_FLOATS = 2 * A_FLOATS + NW * WAVE_FLOATS + ROWINV;   // 131 KiB
 }  // namespace r3
 
-template <int NV, bool AUX, bool HAS_COEF>
+// ---- split-fp16 operands (X3 kernels) -------------------------------------------------------
+// A value x of a row (or column) whose max |x| is m is scaled by s = 2^k so that m*s lies in
+// [2^14, 2^15), then split  x*s = hi + lo*2^-11  with hi = fp16_rne(x*s) and
+// lo = fp16_rne((x*s - hi) * 2^11)  (x*s - hi is exact in fp32).  hi + lo*2^-11 carries 22
+// significant bits: the representation error is <= 2^-22 |x*s| (<= 2^-25 absolute below 2^-3 of
+// scaled range), under the sqrt(K)*2^-24 error of the K = 256 fp32 dot product itself.  A row GEMM
+// then takes three f16 MFMAs per k-step (hi*hi into one accumulator, hi*lo + lo*hi into a second,
+// combined as acc_hi + 2^-11 acc_lo) in place of eight f32 ones: 96 instead of 512 MFMA cycles.
+__device__ __forceinline__ float pow2_scale(float amax) {     // s with amax*s in [2^14, 2^15)
+    const int eb = (__float_as_int(amax) >> 23) & 0xFF;
+    int se = 268 - eb;                                         // 2^(15 - (eb - 126))
+    se = se < 1 ? 1 : (se > 253 ? 253 : se);                  // keep s and 1/s normal
+    return __int_as_float(se << 23);
+}
+__device__ __forceinline__ float pow2_inv(float s) {           // exact 1/s for s = pow2_scale(.)
+    return __int_as_float((254 - ((__float_as_int(s) >> 23) & 0xFF)) << 23);
+}
+__device__ __forceinline__ void split16(float xs, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)xs;
+    lo = (_Float16)((xs - (float)hi) * 2048.0f);
+}
+__device__ __forceinline__ float wave_max(float v) {             // max over the 64 lanes
+    float a = v, b = v;
+    pl_swap32(a, b);
+    v = fmaxf(a, b);
+    a = v, b = v;
+    pl_swap16(a, b);
+    v = fmaxf(a, b);
+    v = fmaxf(v, xpartner_dpp<8>(v));
+    v = fmaxf(v, xpartner_dpp<4>(v));
+    v = fmaxf(v, xpartner_dpp<2>(v));
+    v = fmaxf(v, xpartner_dpp<1>(v));
+    return v;
+}
+
+template <int NV, bool AUX, bool HAS_COEF, bool X3>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     using namespace r3;
     constexpr int NS = NV + (AUX ? 1 : 0);
@@ -557,14 +599,72 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     float* bufA = lds;
     float* slabw = lds + 2 * A_FLOATS + wave * WAVE_FLOATS;   // [NS][32][32]
     float* coefw = slabw + NS_MAX * SLAB;                     // [32][R]
+    float* cinvw = slabw + WAVE_FLOATS - CINV;                 // [32] (X3)
+    float* rowinv = lds + 2 * A_FLOATS + NW * WAVE_FLOATS;     // [2][TR] (X3)
     const int R = p.R;
 
-    float breg[D / 2];
+    // weights: exact f32 (breg, B[kk][c0+i] for 4 k-steps of 32x32x2 per ds_read) or, X3, the
+    // hi / lo fp16 planes of the column-scaled weights, k = 16q + 8h + e for k-step q
+    float breg[X3 ? 1 : D / 2];
+    f16x8 bhi[X3 ? D / 16 : 1], blo[X3 ? D / 16 : 1];
+    if constexpr (!X3) {
 #pragma unroll
-    for (int s = 0; s < D / 2; ++s) {
-        const int kk = 8 * (s >> 2) + 4 * h + (s & 3);
-        breg[s] = p.b_trans ? p.B[(c0 + i) * D + kk] : p.B[kk * D + c0 + i];
+        for (int s = 0; s < D / 2; ++s) {
+            const int kk = 8 * (s >> 2) + 4 * h + (s & 3);
+            breg[s] = p.b_trans ? p.B[(c0 + i) * D + kk] : p.B[kk * D + c0 + i];
+        }
+    } else {
+        auto bval = [&](int k) { return p.b_trans ? p.B[(c0 + i) * D + k] : p.B[k * D + c0 + i]; };
+        float cm = 0.f;
+        for (int q = 0; q < D / 16; ++q)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cm = fmaxf(cm, fabsf(bval(16 * q + 8 * h + e)));
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        const float cs = pow2_scale(cm);
+        if (h == 0) cinvw[i] = pow2_inv(cs);
+#pragma unroll
+        for (int q = 0; q < D / 16; ++q)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                _Float16 hi, lo;
+                split16(bval(16 * q + 8 * h + e) * cs, hi, lo);
+                bhi[q][e] = hi;
+                blo[q][e] = lo;
+            }
     }
+    // X3: the wave converts its own ROWS_PER_WAVE rows of A buffer bb in place, fp32 row ->
+    // [hi plane 512 B | lo plane 512 B] (k-natural order), and records 1/scale per row
+    auto convert_rows = [&](int bb) {
+        if constexpr (X3) {
+            float* base = bufA + bb * A_FLOATS;
+            f32x4 x[ROWS_PER_WAVE];
+            float m[ROWS_PER_WAVE];
+#pragma unroll
+            for (int j = 0; j < ROWS_PER_WAVE; ++j) {
+                x[j] = ld4(base + (wave * ROWS_PER_WAVE + j) * LDA + lane * 4);
+                m[j] = fmaxf(fmaxf(fabsf(x[j][0]), fabsf(x[j][1])), fmaxf(fabsf(x[j][2]), fabsf(x[j][3])));
+            }
+#pragma unroll
+            for (int j = 0; j < ROWS_PER_WAVE; ++j) m[j] = wave_max(m[j]);
+#pragma unroll
+            for (int j = 0; j < ROWS_PER_WAVE; ++j) {
+                const int r = wave * ROWS_PER_WAVE + j;
+                const float s = pow2_scale(m[j]);
+                f16x4 hv, lv;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    _Float16 hi, lo;
+                    split16(x[j][e] * s, hi, lo);
+                    hv[e] = hi;
+                    lv[e] = lo;
+                }
+                char* rowp = reinterpret_cast<char*>(base + r * LDA);
+                *reinterpret_cast<f16x4*>(rowp + lane * 8) = hv;
+                *reinterpret_cast<f16x4*>(rowp + 512 + lane * 8) = lv;
+                if (lane == 0) rowinv[bb * TR + r] = pow2_inv(s);
+            }
+        }
+    };
 
     const long long ntiles = ((long long)p.M + TR - 1) / TR;
     const long long t_beg = (long long)blockIdx.x * p.tiles_per_block;
@@ -742,6 +842,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
         const int a1 = load_aidx(t_beg + 1);
         dma_slabs(t_beg);
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        convert_rows(0);
         dma_idx(t_beg + 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         to_sgpr(a1);
@@ -769,22 +870,56 @@ _Pragma("unroll") \
             } \
             if (t + 1 < t_end) dma_A(t + 1, b ^ 1); \
             const int an = load_aidx(t + 2); \
+            if constexpr (!X3) { \
 _Pragma("unroll") \
-            for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
-            const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
-            f32x4 a_cur = ld4(arow); \
+                for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
+                const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
+                f32x4 a_cur = ld4(arow); \
 _Pragma("unroll") \
-            for (int q = 0; q < D / 8; ++q) { \
-                f32x4 a_nxt = a_cur; \
-                if (q + 1 < D / 8) a_nxt = ld4(arow + 8 * (q + 1)); \
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 0], a_cur[0], acc, 0, 0, 0); \
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 1], a_cur[1], acc, 0, 0, 0); \
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 2], a_cur[2], acc, 0, 0, 0); \
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 3], a_cur[3], acc, 0, 0, 0); \
-                __builtin_amdgcn_sched_barrier(0); \
-                a_cur = a_nxt; \
+                for (int q = 0; q < D / 8; ++q) { \
+                    f32x4 a_nxt = a_cur; \
+                    if (q + 1 < D / 8) a_nxt = ld4(arow + 8 * (q + 1)); \
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 0], a_cur[0], acc, 0, 0, 0); \
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 1], a_cur[1], acc, 0, 0, 0); \
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 2], a_cur[2], acc, 0, 0, 0); \
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 3], a_cur[3], acc, 0, 0, 0); \
+                    __builtin_amdgcn_sched_barrier(0); \
+                    a_cur = a_nxt; \
+                } \
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+            } else { \
+                f32x16 acc_hi, acc_lo; \
+_Pragma("unroll") \
+                for (int j = 0; j < 16; ++j) acc_hi[j] = acc_lo[j] = 0.f; \
+                const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
+                f16x8 ah = __builtin_bit_cast(f16x8, ld4(arow)); \
+                f16x8 al = __builtin_bit_cast(f16x8, ld4(arow + 128)); \
+_Pragma("unroll") \
+                for (int q = 0; q < D / 16; ++q) { \
+                    f16x8 ah_n = ah, al_n = al; \
+                    if (q + 1 < D / 16) { \
+                        ah_n = __builtin_bit_cast(f16x8, ld4(arow + 8 * (q + 1))); \
+                        al_n = __builtin_bit_cast(f16x8, ld4(arow + 128 + 8 * (q + 1))); \
+                    } \
+                    acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], ah, acc_hi, 0, 0, 0); \
+                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], al, acc_lo, 0, 0, 0); \
+                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(blo[q], ah, acc_lo, 0, 0, 0); \
+                    __builtin_amdgcn_sched_barrier(0); \
+                    ah = ah_n; \
+                    al = al_n; \
+                } \
+                /* unscale: row i (1/s_row of this buffer), columns c0+8j+4h+q (1/s_col) */ \
+                const float ri = rowinv[b * TR + i]; \
+_Pragma("unroll") \
+                for (int j = 0; j < 4; ++j) { \
+                    const f32x4 cv = ld4(cinvw + 8 * j + 4 * h); \
+_Pragma("unroll") \
+                    for (int q = 0; q < 4; ++q) \
+                        acc[4 * j + q] = (fmaf(acc_lo[4 * j + q], 0x1p-11f, acc_hi[4 * j + q]) * ri) * cv[q]; \
+                } \
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+                if (t + 1 < t_end) convert_rows(b ^ 1); \
             } \
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
             if (!LATE) { \
                 epilogue(t, acc); \
                 if (t + 1 < t_end) { \
@@ -1740,6 +1875,12 @@ int iddgcn_set_rowgemm_path(int path) {
     return old;
 }
 
+int iddgcn_set_gemm_precision(int mode) {
+    const int old = g_gemm_split;
+    g_gemm_split = mode == IDDGCN_GEMM_SPLIT_F16 ? 1 : 0;
+    return old;
+}
+
 int iddgcn_spmm_csr_f32(void* stream, int n_seg, int n_rows, int d, const int* row_ptr, const int* col,
                         const float* vals, const float* X, float* Y, int accumulate) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
@@ -1786,18 +1927,25 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     // v3 (staggered, wave-private slabs): D=256, R <= 2
     const bool v3_ok = a->D == 256 && p.R <= 2 && !(gatherV && dsig) && (!gatherV || p.v_row_stride == 256) &&
                        g_rowgemm_path == 0;
-    if (v3_ok) {
+    if (v3_ok || (a->D == 256 && g_gemm_split && p.R <= 2 && !(gatherV && dsig) &&
+                  (!gatherV || p.v_row_stride == 256))) {
         const long long nt = ((long long)p.M + r3::TR - 1) / r3::TR;
         long long nb = nt < 256 ? nt : 256;
         p.tiles_per_block = (int)((nt + nb - 1) / nb);
         nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
         const dim3 g((unsigned)nb), blk(512);
-        if (gatherV && p.R == 1) hipLaunchKernelGGL((rowgemm256_v3_kernel<1, false, true>), g, blk, 0, st, p);
-        else if (gatherV) hipLaunchKernelGGL((rowgemm256_v3_kernel<2, false, true>), g, blk, 0, st, p);
-        else if (p.R > 0 && dsig) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, true, true>), g, blk, 0, st, p);
-        else if (p.R > 0) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, false, true>), g, blk, 0, st, p);
-        else if (dsig) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, true, false>), g, blk, 0, st, p);
-        else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, false, false>), g, blk, 0, st, p);
+#define V3K(NV, AUX, HC)                                                                             \
+        {                                                                                            \
+            if (g_gemm_split) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true>), g, blk, 0, st, p); \
+            else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, false>), g, blk, 0, st, p);           \
+        }
+        if (gatherV && p.R == 1) V3K(1, false, true)
+        else if (gatherV) V3K(2, false, true)
+        else if (p.R > 0 && dsig) V3K(0, true, true)
+        else if (p.R > 0) V3K(0, false, true)
+        else if (dsig) V3K(0, true, false)
+        else V3K(0, false, false)
+#undef V3K
         return launch_status();
     }
     const int epi_rows = gatherV ? p.R : (dsig ? 1 : 0);

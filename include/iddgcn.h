@@ -73,6 +73,19 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
  * 1 = register-staged kernels, 2 = v2 LDS-DMA row GEMM.  Returns the previous setting. */
 int iddgcn_set_rowgemm_path(int path);
 
+/* Operand precision of the D=256 row GEMMs (process-wide; returns the previous mode):
+ *   IDDGCN_GEMM_EXACT_F32 (default): v_mfma_f32_32x32x2_f32, bitwise an fmaf chain;
+ *   IDDGCN_GEMM_SPLIT_F16: each operand row (A) / column (B) is scaled by a power of two so its
+ *     max lies in [2^14, 2^15), every value is split as hi + lo*2^-11 (two fp16, 22 significant
+ *     bits), and hi*hi + 2^-11 (hi*lo + lo*hi) runs on v_mfma_f32_32x32x16_f16 with fp32
+ *     accumulation; the power-of-two scales are undone exactly in the epilogue.  Accuracy is
+ *     fp32-class (operand error <= 2^-22 relative, below the K=256 fp32 summation error);
+ *     results are deterministic but not bitwise equal to the exact mode.
+ * Row GEMMs for D < 256 and every other kernel always compute in exact f32. */
+#define IDDGCN_GEMM_EXACT_F32 0
+#define IDDGCN_GEMM_SPLIT_F16 1
+int iddgcn_set_gemm_precision(int mode);
+
 /* C[D][D] (+)= A^T · B over M rows (A, B are M x D).  Two stages: each of n_blocks
  * workgroups writes a D x D partial into `slab` (n_blocks*D*D floats), then the
  * partials are summed in block order (deterministic).  n_blocks from

@@ -1,8 +1,11 @@
-"""Time the edge-level GEMM kernels alone at config-3 shape (T = 4M rows, D = 256, R = 2).
+"""Time and check the edge-level GEMM kernels alone at config-3 shape (T = 4M rows, D = 256, R = 2),
+in both operand-precision modes (exact f32 MFMA, split-fp16 MFMA).
 
-usage: python tools/bench_gemm.py [libpath ...]   (each lib is loaded in turn, same inputs)
+For each case it prints the time per launch, the algorithmic TFLOP/s, and the max error of each
+mode against an fp64 torch reference on the first `check` rows (absolute, over max |ref|).
+
+usage: python tools/bench_gemm.py [T]
 """
-import ctypes
 import sys
 
 import torch
@@ -12,42 +15,57 @@ from iddgcn_amd import _lib as L  # noqa: E402
 from iddgcn_amd import ops  # noqa: E402
 
 
-def run(libpath, T=4_000_000, N=100_000, D=256, R=2, reps=5):
-    L._lib = L.load(libpath)
+def run(T=4_000_000, N=100_000, D=256, R=2, reps=5, check=20_000):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     A = torch.rand(T, D, device=dev, generator=g)
-    S = torch.randn(D, D, device=dev, generator=g) / 16
+    S = torch.randn(D, D, device=dev, generator=g)
     W = torch.rand(N, R, device=dev, generator=g)
-    P = torch.randn(R, N, D, device=dev, generator=g)
+    P = torch.randn(R, N, D, device=dev, generator=g) * 4
     t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
     h = torch.randint(0, N, (T,), device=dev, generator=g).int()
     aux = torch.rand(T, D, device=dev, generator=g)
+    dO = torch.randn(T, D, device=dev, generator=g) * 1e-12
     C = torch.empty(T, D, device=dev)
     slab = torch.empty(ops.tn_blocks(T, D) * D * D, device=dev)
     dS = torch.empty(D, D, device=dev)
+    n = check
+    Ad, Sd = A[:n].double(), S.double()
+    refs = {
+        "fwd_combine": torch.sigmoid(Ad @ Sd + sum(W.double()[h[:n].long(), r:r + 1] * P.double()[r][t[:n].long()]
+                                                   for r in range(R))),
+        "bwd_dsig": (dO[:n].double() @ Sd.t()) * aux[:n].double() * (1 - aux[:n].double()),
+        "plain": Ad @ Sd,
+    }
     cases = {
         "fwd_combine": lambda: ops.rowgemm(A, S, C, coef=W, coef_idx=h, V=P, v_idx=t, v_rel_stride=N * D,
                                            act=L.ACT_SIGMOID),
-        "bwd_dsig": lambda: ops.rowgemm(A, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux),
+        "bwd_dsig": lambda: ops.rowgemm(dO, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux),
         "plain": lambda: ops.rowgemm(A, S, C),
         "tn": lambda: ops.gemm_tn(A, aux, dS, slab),
     }
-    out = {}
-    for name, fn in cases.items():
-        fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        out[name] = (ms, 2.0 * D * D * T / ms / 1e9)
-    print(libpath.split("/")[-1], " ".join(f"{k}={v[0]:.3f}ms/{v[1]:.1f}TF" for k, v in out.items()), flush=True)
+    for mode, mname in ((L.GEMM_EXACT_F32, "exact"), (L.GEMM_SPLIT_F16, "split")):
+        old = L.lib().iddgcn_set_gemm_precision(mode)
+        try:
+            for name, fn in cases.items():
+                fn()
+                torch.cuda.synchronize()
+                err = ""
+                if name in refs:
+                    ref = refs[name]
+                    e = ((C[:n].double() - ref).abs().max() / ref.abs().max()).item()
+                    err = f" relerr={e:.2e}"
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / reps
+                print(f"{mname:5s} {name:12s} {ms:7.3f} ms  {2.0 * D * D * T / ms / 1e9:6.1f} TF{err}", flush=True)
+        finally:
+            L.lib().iddgcn_set_gemm_precision(old)
 
 
 if __name__ == "__main__":
-    for p in sys.argv[1:] or [L.LIB_PATH]:
-        run(p)
+    run(*(int(a) for a in sys.argv[1:2]))
