@@ -38,7 +38,54 @@ from iddgcn_amd.parallel import GradAllReduce  # noqa: E402
 from iddgcn_amd.utils import synthetic_graph  # noqa: E402
 
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md, f32-input MFMA dense peak
+MFMA_F16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md, bf16/f16 MFMA dense peak (16x the f32 rate)
 HBM_PEAK_GBS = 8000.0
+GEMM_NOTE = {
+    "split": "D=256 GEMM operands split hi+lo fp16 (22 significant bits, power-of-two row/column scales), "
+             "3 f16 MFMAs per k-step, fp32 accumulation; every other kernel exact f32 "
+             "(include/iddgcn.h iddgcn_set_gemm_precision)",
+    "exact": "exact f32 MFMA (v_mfma_f32_32x32x2_f32, bitwise an fmaf chain) everywhere",
+}
+
+
+def kernel_roofline(name, N, R, D, T, gemm, avg_ms):
+    """Roofline of one edge-level GEMM launch.
+
+    flops: 2*D^2*T algorithmic (x3 f16 MFMA instructions on the f16 peak in split mode);
+    bytes (algorithmic, fp32): fwd reads x^{l-1}, writes x^l, reads W[h_e] (R per edge), t_e and the
+    distinct P_r rows (R*N*D once); bwd reads do and the sigma' operand x, writes do'; dS reads x and
+    do.  bound = whichever roofline time is larger."""
+    flops = 2.0 * D * D * T
+    nbytes = {"tail_fwd_gemm": 8.0 * D * T + 4.0 * R * T + 4.0 * T + 4.0 * R * N * D,
+              "tail_bwd_gemm": 12.0 * D * T,
+              "tail_dS_tn": 8.0 * D * T}[name]
+    hw_flops, peak_f = (3 * flops, MFMA_F16_PEAK_TFLOPS) if gemm == "split" else (flops, MFMA_F32_PEAK_TFLOPS)
+    t_mfma = hw_flops / (peak_f * 1e12)
+    t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
+    s = avg_ms * 1e-3
+    if t_hbm >= t_mfma:
+        out = {"kernel": name, "bound": "hbm", "achieved": nbytes / s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    else:
+        out = {"kernel": name, "bound": "mfma", "achieved": hw_flops / s / 1e12, "peak": peak_f,
+               "unit": "TFLOP/s"}
+    out["frac"] = out["achieved"] / out["peak"]
+    out.update({"avg_launch_ms": avg_ms, "bytes_per_launch": nbytes, "flops_per_launch": flops,
+                "mfma_frac": hw_flops / s / 1e12 / peak_f, "hbm_frac": nbytes / s / 1e9 / HBM_PEAK_GBS})
+    return out
+
+
+def pmc_traffic(kernel, gemm, workload, world):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same bench
+    command (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x2 per the
+    gfx950 correction + WRITE_SIZE, separate --pmc passes), or None when no such profile exists."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        with open(path) as f:
+            rec = json.load(f)
+        key = f"{workload}/{gemm}/n{world}/{kernel}"
+        if key in rec:
+            return rec[key]["bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 CONFIGS = {
     3: dict(name="synthetic-3", N=100_000, R=2, M=2_000_000, D=256),
@@ -107,6 +154,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gemm", default="split", choices=["split", "exact"],
+                    help="operand precision of the D=256 MFMA GEMMs (the other mode is timed too)")
+    ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,47 +178,60 @@ def main():
     tri = np.concatenate([pos, neg])[lo:hi]
     lab = np.concatenate([np.ones(len(pos), np.float32), np.zeros(len(neg), np.float32)])[lo:hi]
 
-    eng = Engine(N, R, D, dev)
+    eng = Engine(N, R, D, dev, gemm=args.gemm)
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
-    P.load(reference_init(N, R, D, 89))
-    opt = KerasAdam(P)
+    init = reference_init(N, R, D, 89)
     adj = eng.adjacency(adj_mats)
     ed = eng.edges(tri, lab)
     allreduce = GradAllReduce(G.flat) if world > 1 else None
     del pos, neg, tri, lab
 
-    def step():
-        return eng.train_step(P, G, opt, adj, ed, t_global=T, allreduce=allreduce)
+    def timed_run(mode, probe):
+        """W warm-up steps, then K timed steps between barriers + synchronize; max over ranks."""
+        eng.gemm = mode
+        P.load(init)                       # every mode starts from the same parameters
+        opt = KerasAdam(P)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    eng.probe = {}
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    probe, eng.probe = eng.probe, None
-    loss_val = float(loss.item()) / T
+        def step():
+            return eng.train_step(P, G, opt, adj, ed, t_global=T, allreduce=allreduce)
 
-    # dominant kernel: largest total event time inside the timed steps
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        eng.probe = {} if probe else None
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        probe_out, eng.probe = eng.probe, None
+        return elapsed, float(loss.item()) / T, probe_out
+
+    elapsed, loss_val, probe = timed_run(args.gemm, True)
+    other = None
+    if not args.no_other_mode:
+        mode2 = "exact" if args.gemm == "split" else "split"
+        el2, loss2, _ = timed_run(mode2, False)
+        other = {"gemm": mode2, "value": M / (el2 / args.steps), "ms_per_step": el2 / args.steps * 1e3,
+                 "loss": loss2}
+
+    # dominant kernel: largest total event time inside the timed steps; its roofline is the larger
+    # of the MFMA time (hardware MFMA work on the mode's peak) and the HBM time (algorithmic bytes)
     T_local = ed.T
-    flops_per_launch = {"tail_fwd_gemm": 2.0 * D * D * T_local, "tail_bwd_gemm": 2.0 * D * D * T_local,
-                        "tail_dS_tn": 2.0 * D * D * T_local}
     kt = {k: [a.elapsed_time(b) for a, b in v] for k, v in probe.items()}
     dom = max(kt, key=lambda k: sum(kt[k]))
     avg_ms = statistics.mean(kt[dom])
-    achieved = flops_per_launch[dom] / (avg_ms * 1e-3) / 1e12
+    rl = kernel_roofline(dom, N, R, D, T_local, args.gemm, avg_ms)
+    rl["traffic"], rl["traffic_source"] = pmc_traffic(dom, args.gemm, cfg["name"], world)
 
     ms = elapsed / args.steps * 1e3
     result = {
@@ -181,17 +244,18 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "gemm_operands": GEMM_NOTE[args.gemm],
         "data": "synthetic (seeded mutation-drug graph, reference-distribution random init)",
         "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
                    "scored_edges": T, "scored_edges_per_gpu": T_local, "feat_dim": D,
-                   "parallelism": f"edge-dp{world}"},
+                   "parallelism": f"edge-dp{world}", "gemm": args.gemm},
         "scored_edges_per_s": T / (elapsed / args.steps),
         "loss": loss_val,
         "kernel_ms_per_step": {k: sum(v) / args.steps for k, v in kt.items()},
-        "roofline": {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS, "traffic": None,
-                     "avg_launch_ms": avg_ms, "flops_per_launch": flops_per_launch[dom]},
+        "roofline": rl,
     }
+    if other is not None:
+        result["other_gemm_mode"] = other
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:

@@ -1135,6 +1135,165 @@ __global__ __launch_bounds__(512) void gemm_tn256_dma_kernel(long long M, long l
         }
 }
 
+// ---------------------------------------------------------------------------
+// TN reduction GEMM, D = 256, split-fp16 operands.  Same partial-slab contract as
+// gemm_tn256_dma_kernel.  Per 32-row tile, wave w converts column block w (32 columns x 32 rows)
+// of A and of B IN PLACE from the DMA'd fp32 rows (1040-B padded) into k-contiguous planes:
+// segment i of block w (row i's bytes [128w, 128w+128)) becomes column 32w+i as
+// [hi: 32 rows fp16 | lo: 32 rows fp16], so an MFMA fragment (8 consecutive rows of one column)
+// is one ds_read_b128.  The reduction runs over rows, so scales cannot be per row: each block has
+// a running power-of-two scale that only decreases (first tile: max*s in [2^14, 2^15); a later
+// tile whose max would overflow lowers it and the accumulators that used it are rescaled
+// exactly).  A block w is private to wave w; B block cj's scale is published in LDS with its
+// planes and every wave rescales acc[cj] when it changes.  One accumulator per tile:
+// hi*hi + hi*lo + lo*hi with lo = fp16(x*s - hi) (same units; a lo below the fp16 normal range
+// only loses bits below 2^-38 of the block max).
+// ---------------------------------------------------------------------------
+namespace tn3 {
+constexpr int D = 256, TK = 32, LDR = D + 4, TILE = TK * LDR;
+constexpr float S_INIT = 0x1p126f;                       // pow2_scale(0): "no data yet"
+}
+
+__device__ __forceinline__ void split16_same(float xs, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)xs;
+    lo = (_Float16)(xs - (float)hi);
+}
+
+__global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long long rows_per_block,
+                                                            const float* __restrict__ A,
+                                                            const float* __restrict__ B,
+                                                            float* __restrict__ slab) {
+    using namespace tn3;
+    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * TILE + 2 * 8];   // [buf][A|B][TK][LDR], sB[buf][8]
+    float* sBpub = lds + 2 * 2 * TILE;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int i = lane & 31, h = lane >> 5;
+
+    f32x16 acc[8];
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[cj][j] = 0.f;
+    float sA = S_INIT, sBrun = S_INIT;       // running scales of the blocks this wave converts
+    float curB[8];                           // scale acc[cj] is currently expressed in (B side)
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj) curB[cj] = S_INIT;
+
+    const long long r_beg = (long long)blockIdx.x * rows_per_block;
+    long long r_end = r_beg + rows_per_block;
+    if (r_end > M) r_end = M;
+    const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
+
+    auto stage = [&](long long t, int b) {
+        float* As = lds + (b * 2 + 0) * TILE;
+        float* Bs = lds + (b * 2 + 1) * TILE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = wave * 4 + j;
+            const long long e = r_beg + t * TK + r;
+            if (e < r_end) {
+                dma_row_1k(A + e * D, As + r * LDR, lane);
+                dma_row_1k(B + e * D, Bs + r * LDR, lane);
+            } else {
+                st4(As + r * LDR + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                st4(Bs + r * LDR + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+            }
+        }
+    };
+    // convert column block `wave` of one operand tile in place; returns the block scale used
+    auto convert_block = [&](float* T, float& srun, bool is_a) {
+        float v[16];
+        float m = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            v[r] = T[(16 * h + r) * LDR + 32 * wave + i];
+            m = fmaxf(m, fabsf(v[r]));
+        }
+        m = wave_max(m);
+        if (m * srun >= 32768.0f) {                      // lower the running scale (exact rescale)
+            const float s_new = pow2_scale(m);
+            if (is_a) {
+                const float f = s_new * pow2_inv(srun);
+#pragma unroll
+                for (int cj = 0; cj < 8; ++cj) acc[cj] *= f;
+            }
+            srun = s_new;
+        }
+        f16x8 hv[2], lv[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            _Float16 hi, lo;
+            split16_same(v[r] * srun, hi, lo);
+            hv[r >> 3][r & 7] = hi;
+            lv[r >> 3][r & 7] = lo;
+        }
+        char* seg = reinterpret_cast<char*>(T + i * LDR + 32 * wave);
+        *reinterpret_cast<f16x8*>(seg + 32 * h) = hv[0];
+        *reinterpret_cast<f16x8*>(seg + 32 * h + 16) = hv[1];
+        *reinterpret_cast<f16x8*>(seg + 64 + 32 * h) = lv[0];
+        *reinterpret_cast<f16x8*>(seg + 64 + 32 * h + 16) = lv[1];
+    };
+    auto convert = [&](int b) {
+        convert_block(lds + (b * 2 + 0) * TILE, sA, true);
+        convert_block(lds + (b * 2 + 1) * TILE, sBrun, false);
+        if (lane == 0) sBpub[b * 8 + wave] = sBrun;
+    };
+
+    if (nt > 0) {
+        stage(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        convert(0);
+        __syncthreads();
+    }
+    int b = 0;
+    for (long long t = 0; t < nt; ++t, b ^= 1) {
+        if (t + 1 < nt) stage(t + 1, b ^ 1);
+        // B-side scales of this tile: rescale the accumulators whose block scale dropped
+#pragma unroll
+        for (int cj = 0; cj < 8; ++cj) {
+            const float s = sBpub[b * 8 + cj];
+            if (s != curB[cj]) {
+                acc[cj] *= s * pow2_inv(curB[cj]);
+                curB[cj] = s;
+            }
+        }
+        const char* Aseg = reinterpret_cast<const char*>(lds + (b * 2 + 0) * TILE + i * LDR + 32 * wave);
+        const char* Bseg = reinterpret_cast<const char*>(lds + (b * 2 + 1) * TILE + i * LDR);
+#pragma unroll
+        for (int s = 0; s < TK / 16; ++s) {
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(Aseg + 32 * s + 16 * h);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(Aseg + 64 + 32 * s + 16 * h);
+#pragma unroll
+            for (int cj = 0; cj < 8; ++cj) {
+                const f16x8 bh = *reinterpret_cast<const f16x8*>(Bseg + 128 * cj + 32 * s + 16 * h);
+                const f16x8 bl = *reinterpret_cast<const f16x8*>(Bseg + 128 * cj + 64 + 32 * s + 16 * h);
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[cj], 0, 0, 0);
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[cj], 0, 0, 0);
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[cj], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t + 1 < nt) {
+            convert(b ^ 1);
+            __syncthreads();
+        }
+    }
+    float* out = slab + (long long)blockIdx.x * D * D;
+    const float ia = pow2_inv(sA);
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj) {
+        const float ib = pow2_inv(curB[cj]);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int row = 32 * wave + (j & 3) + 8 * (j >> 2) + 4 * h;
+            out[row * D + 32 * cj + i] = (acc[cj][j] * ia) * ib;
+        }
+    }
+}
+
 // out[D][R] partial of A^T dz and colsum(dz) per block; slab row layout [(D+1)][R]
 template <int D>
 __global__ __launch_bounds__(D) void gemm_tn_narrow_kernel(long long M, long long rows_per_block, int R,
@@ -1985,7 +2144,9 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
-    if (d == 256 && g_rowgemm_path != 1) {
+    if (d == 256 && g_gemm_split) {
+        hipLaunchKernelGGL(gemm_tn256_x3_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
+    } else if (d == 256 && g_rowgemm_path != 1) {
         hipLaunchKernelGGL(gemm_tn256_dma_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
     } else switch (d) {
         case 32: TNK(32); break;

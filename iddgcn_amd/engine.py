@@ -129,21 +129,42 @@ class Workspace:
         self.narrow_slab = e((ops.tn_narrow_blocks(N) + 1) * (D + 1) * R)
 
 
-class Engine:
-    """Runs forward / backward / Adam for one (graph, scored-edge batch)."""
+GEMM_MODES = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16}
 
-    def __init__(self, num_entities, num_relations, dim, device=None):
+
+class Engine:
+    """Runs forward / backward / Adam for one (graph, scored-edge batch).
+
+    ``gemm`` selects the operand precision of the D=256 MFMA GEMMs (include/iddgcn.h,
+    iddgcn_set_gemm_precision): "split" (default) splits every fp32 operand into two fp16
+    halves with power-of-two row/column scales and accumulates in fp32 (fp32-class error, 3 f16
+    MFMAs per k-step); "exact" runs v_mfma_f32_32x32x2_f32, bitwise an fmaf chain.  Other widths
+    and all non-GEMM kernels are exact f32 in both modes.
+    """
+
+    def __init__(self, num_entities, num_relations, dim, device=None, gemm="split"):
         if dim not in (32, 64, 128, 256):
             raise L.IddgcnError("embedding dim must be one of 32, 64, 128, 256")
         if not 1 <= num_relations <= 8:
             raise L.IddgcnError("num_relations must be in [1, 8]")
+        if gemm not in GEMM_MODES:
+            raise L.IddgcnError(f"gemm must be one of {sorted(GEMM_MODES)}")
         self.N, self.R, self.D = num_entities, num_relations, dim
+        self.gemm = gemm
         self.device = torch.device("cuda") if device is None else torch.device(device)
         if self.device.type != "cuda":
             raise L.IddgcnError("IDDGCN engine runs on the GPU only (no CPU fallback)")
         L.lib()  # fail loudly now if the HIP library is missing
         self._ws = {}
         self.probe = None      # {name: [(start_event, end_event), ...]} when timing kernels
+
+    @contextlib.contextmanager
+    def _precision(self):
+        old = L.lib().iddgcn_set_gemm_precision(GEMM_MODES[self.gemm])
+        try:
+            yield
+        finally:
+            L.lib().iddgcn_set_gemm_precision(old)
 
     @contextlib.contextmanager
     def _mark(self, name):
@@ -261,8 +282,9 @@ class Engine:
         sum of per-edge BCE terms of this rank (divide by T for the mean)."""
         ws = self.workspace(ed.T, True)
         self._t_global = t_global
-        self.forward(params, adj, ed, ws, True)
-        self.backward(params, grads, adj, ed, ws)
+        with self._precision():
+            self.forward(params, adj, ed, ws, True)
+            self.backward(params, grads, adj, ed, ws)
         if allreduce is not None:
             allreduce(grads.flat, ws.loss)
         opt.apply(params, grads)
@@ -270,7 +292,8 @@ class Engine:
 
     def predict(self, params, adj, ed):
         ws = self.workspace(ed.T, False)
-        self.forward(params, adj, ed, ws, False)
+        with self._precision():
+            self.forward(params, adj, ed, ws, False)
         return ed.unsort(ws.p)
 
     def loss_and_grads(self, params, grads, adj, ed, t_global=None):
@@ -278,10 +301,12 @@ class Engine:
         self._t_global = t_global
         self._want_p = True
         try:
-            self.forward(params, adj, ed, ws, True)
+            with self._precision():
+                self.forward(params, adj, ed, ws, True)
         finally:
             self._want_p = False
-        self.backward(params, grads, adj, ed, ws)
+        with self._precision():
+            self.backward(params, grads, adj, ed, ws)
         return ws.loss, ed.unsort(ws.p)
 
 

@@ -406,6 +406,125 @@ def test_rowgemm_dma_path_bitwise_equals_register_path(mode, cuda):
     assert torch.equal(out[0], out[2])
 
 
+class _gemm_mode:
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        self.old = L.lib().iddgcn_set_gemm_precision(self.mode)
+
+    def __exit__(self, *a):
+        L.lib().iddgcn_set_gemm_precision(self.old)
+
+
+def _maxrel(got, ref):
+    return ((got.double() - ref).abs().max() / ref.abs().max()).item()
+
+
+@pytest.mark.parametrize("mode", ["plain", "trans", "combine", "combine_r1", "dsig", "rank_bcast", "accumulate",
+                                  "gatherA", "small_M", "row_decades", "zero_rows"])
+def test_rowgemm_split_f16_vs_fp64(mode, cuda):
+    """Split-fp16 operand mode (D=256): error vs an fp64 torch reference no larger than twice the
+    exact-f32 MFMA path's (floor 1e-6 of max|ref|), on every epilogue form, ragged tiles, rows whose
+    magnitudes span 12 decades (per-row scales) and all-zero rows; deterministic run to run."""
+    g = torch.Generator().manual_seed(sum(map(ord, mode)))
+    D, N, R = 256, 700, (1 if mode == "combine_r1" else 2)
+    M = 77 if mode == "small_M" else 20_000 + 17
+    A = torch.rand(M, D, generator=g, dtype=torch.float64)
+    if mode == "row_decades":
+        A = torch.randn(M, D, generator=g, dtype=torch.float64) * 10 ** (12 * torch.rand(M, 1, generator=g,
+                                                                                        dtype=torch.float64) - 6)
+    if mode == "zero_rows":
+        A[::3] = 0
+    S = torch.randn(D, D, generator=g, dtype=torch.float64)
+    A, S = A.to(cuda), S.to(cuda)
+    kw, C0 = {}, None
+    Af, Sf = A.float(), S.float()
+    if mode in ("combine", "combine_r1"):
+        W = torch.rand(N, R, generator=g, dtype=torch.float64).to(cuda)
+        P = (torch.randn(R, N, D, generator=g, dtype=torch.float64) * 4).to(cuda)
+        h = torch.randint(0, N, (M,), generator=g).to(cuda)
+        t = torch.randint(0, N, (M,), generator=g).sort().values.to(cuda)
+        kw = dict(coef=W.float(), coef_idx=h.int(), V=P.float(), v_idx=t.int(), v_rel_stride=N * D,
+                  act=L.ACT_SIGMOID)
+        ref = torch.sigmoid(A @ S + sum(W[h, r:r + 1] * P[r][t] for r in range(R)))
+    elif mode == "dsig":
+        X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
+        kw = dict(b_trans=True, act=L.ACT_DSIGMOID, aux=X.float())
+        ref = (A @ S.t()) * X * (1 - X)
+    elif mode == "rank_bcast":
+        X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
+        dz = torch.randn(M, R, generator=g, dtype=torch.float64).to(cuda)
+        Wa = torch.randn(D, R, generator=g, dtype=torch.float64).to(cuda)
+        kw = dict(b_trans=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D, v_row_stride=0,
+                  act=L.ACT_DSIGMOID, aux=X.float())
+        ref = (A @ S.t() + dz @ Wa.t()) * X * (1 - X)
+    elif mode == "accumulate":
+        C0 = torch.randn(M, D, generator=g, dtype=torch.float64).to(cuda)
+        kw = dict(accumulate=True)
+        ref = C0 + A @ S
+    elif mode == "gatherA":
+        ai = torch.randint(0, M, (M,), generator=g).to(cuda)
+        kw = dict(a_idx=ai.int())
+        ref = A[ai] @ S
+    elif mode == "trans":
+        kw = dict(b_trans=True)
+        ref = A @ S.t()
+    else:
+        ref = A @ S
+    errs, outs = {}, {}
+    for gm in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16):
+        with _gemm_mode(gm):
+            C = C0.float().clone() if C0 is not None else torch.full((M, D), 7.0, device=cuda)
+            ops.rowgemm(Af, Sf, C, **kw)
+            if gm == L.GEMM_SPLIT_F16:
+                C2 = C0.float().clone() if C0 is not None else torch.empty(M, D, device=cuda)
+                ops.rowgemm(Af, Sf, C2, **kw)
+                assert torch.equal(C, C2)
+        outs[gm], errs[gm] = C, _maxrel(C, ref)
+    split = outs[L.GEMM_SPLIT_F16]
+    if mode == "zero_rows":
+        assert torch.equal(split[::3], torch.zeros_like(split[::3]))
+    if mode == "row_decades":   # per-row relative error, every row (per-row scales)
+        rel = ((split.double() - ref).abs().amax(1) / ref.abs().amax(1)).max().item()
+        assert rel <= 1e-5, rel
+    assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
+
+
+@pytest.mark.parametrize("M,kind", [(31, "plain"), (5003, "plain"), (300_017, "decades"), (70_001, "zero_blocks"),
+                                    (40_000, "growing")])
+def test_gemm_tn_split_f16_vs_fp64(M, kind, cuda):
+    """Split-fp16 TN GEMM (running per-block power-of-two scales): error vs fp64 within 2x the exact
+    path's (floor 1e-6), with row magnitudes spanning decades, all-zero stretches, and magnitudes that
+    change along the rows (block scales lowered many times); deterministic run to run."""
+    g = torch.Generator().manual_seed(M)
+    D = 256
+    A = torch.rand(M, D, generator=g, dtype=torch.float64)
+    B = torch.randn(M, D, generator=g, dtype=torch.float64) * 1e-12
+    if kind == "decades":
+        B = B * 10 ** (6 * torch.rand(M, 1, generator=g, dtype=torch.float64) - 3)
+    elif kind == "zero_blocks":
+        B[: M // 2] = 0
+        A[M // 3: M // 2] = 0
+    elif kind == "growing":
+        B = B * torch.logspace(-4, 4, M, dtype=torch.float64)[:, None]
+        A = A * torch.logspace(3, -3, M, dtype=torch.float64)[:, None]
+    A, B = A.to(cuda), B.to(cuda)
+    ref = A.t() @ B
+    slab = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
+    errs = {}
+    for gm in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16):
+        with _gemm_mode(gm):
+            C = torch.empty(D, D, device=cuda)
+            ops.gemm_tn(A.float(), B.float(), C, slab)
+            errs[gm] = _maxrel(C, ref)
+            if gm == L.GEMM_SPLIT_F16:
+                C2 = torch.empty(D, D, device=cuda)
+                ops.gemm_tn(A.float(), B.float(), C2, slab)
+                assert torch.equal(C, C2)
+    assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
+
+
 @pytest.mark.parametrize("M", [31, 5003, 300_017])
 def test_gemm_tn_dma_path_bitwise_equals_register_path(M, cuda):
     """D=256 LDS-DMA TN kernel == register-staged TN kernel, bit for bit (same MFMA order,

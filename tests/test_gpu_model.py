@@ -24,8 +24,8 @@ pytestmark = pytest.mark.gpu
 N_ENT, N_REL = 845, 4
 
 
-def run_step(params, pos, neg, N, R, D, dev, adam=False):
-    eng = Engine(N, R, D, dev)
+def run_step(params, pos, neg, N, R, D, dev, adam=False, gemm="split"):
+    eng = Engine(N, R, D, dev, gemm=gemm)
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
     P.load(params)
     adj = eng.adjacency(get_adj_mats(pos, N, R))
@@ -103,9 +103,10 @@ def test_synth_small_step_parity(golden, cuda):
             assert np.abs((out["params"][name] - params[name]) - (v - params[name])).max() <= 2e-5, name
 
 
-@pytest.mark.parametrize("D,R", [(256, 2), (128, 3)])
-def test_wide_step_parity_vs_oracle(D, R, cuda):
-    """The headline width (D=256) on a mutation–drug graph, non-saturating init, vs float64 oracle."""
+@pytest.mark.parametrize("D,R,gemm", [(256, 2, "split"), (256, 2, "exact"), (128, 3, "exact")])
+def test_wide_step_parity_vs_oracle(D, R, gemm, cuda):
+    """The headline width (D=256) on a mutation–drug graph, non-saturating init, vs float64 oracle,
+    in both GEMM operand modes (same bars)."""
     N = 3000
     pos, neg = synthetic_graph(N, R, 12000, seed=5)
     rng = np.random.default_rng(1)
@@ -120,24 +121,76 @@ def test_wide_step_parity_vs_oracle(D, R, cuda):
     params = {k: v.astype(np.float32) for k, v in params.items()}
     neg = neg[:6000]
     loss, scores, grads = train_step_grads(params, pos, neg, get_adj_coo(pos, N, R), N)
-    out = run_step(params, pos, neg, N, R, D, cuda)
+    out = run_step(params, pos, neg, N, R, D, cuda, gemm=gemm)
     assert abs(out["loss"] - loss) <= 1e-5 * loss
     np.testing.assert_allclose(out["scores"], scores, rtol=0, atol=1e-5)
     grad_check(out["grads"], grads, 2e-4)
 
 
-def test_reference_init_distribution_step_finite(cuda):
+@pytest.mark.parametrize("gemm", ["split", "exact"])
+def test_reference_init_distribution_step_finite(gemm, cuda):
     """Reference-distribution init (E~U[0,1), K,S~N(0,1)) saturates the sigmoids exactly as
     TF does; the step must stay finite and match the oracle's loss."""
     N, R, D = 2000, 2, 256
     pos, neg = synthetic_graph(N, R, 8000, seed=2)
     params = init_params(N, R, D, seed=89)
     loss, scores, grads = train_step_grads(params, pos, neg[:4000], get_adj_coo(pos, N, R), N)
-    out = run_step(params, pos, neg[:4000], N, R, D, cuda)
+    out = run_step(params, pos, neg[:4000], N, R, D, cuda, gemm=gemm)
     assert np.isfinite(out["loss"])
     assert abs(out["loss"] - loss) <= 1e-3 * loss
     for v in out["grads"].values():
         assert np.all(np.isfinite(v))
+
+
+@pytest.mark.parametrize("gemm", ["split", "exact"])
+def test_headline_width_saturating_step_vs_fp32_oracle(gemm, cuda):
+    """D=256, E ~ U[0,1) as in the reference, S ~ N(0, 9/D) (layer pre-activations up to ~8, the
+    sigmoids partly saturated), K ~ N(0, 1/(64 D)): fp32 itself deviates from fp64 here by ~3e-7 of
+    max|g|.  Bar, for the split-fp16 GEMM mode and the exact one alike: loss and every gradient within
+    4x the deviation of the reference formulation run in fp32 (floors 1e-6 rel. loss, 1e-5 of max|g|),
+    scores 1e-5."""
+    N, R, D = 2500, 2, 256
+    pos, neg = synthetic_graph(N, R, 10000, seed=8)
+    neg = neg[:5000]
+    rng = np.random.default_rng(3)
+    params = {"E": rng.random((N, D))}
+    for l in (1, 2, 3):
+        params[f"K{l}"] = rng.standard_normal((R, D, D)) / np.sqrt(D) / 8
+        params[f"S{l}"] = rng.standard_normal((D, D)) * 3 / np.sqrt(D)
+        params[f"relw{l}"] = rng.uniform(-.05, .05, R)
+        params[f"Wa{l}"] = rng.standard_normal((D, R)) / np.sqrt(D)
+        params[f"ba{l}"] = np.zeros(R)
+    params["rel"] = rng.standard_normal((R, D)) * 0.2
+    params = {k: v.astype(np.float32) for k, v in params.items()}
+    adj = get_adj_coo(pos, N, R)
+    loss, scores, g64 = train_step_grads(params, pos, neg, adj, N)
+    loss32, _, g32 = train_step_grads(params, pos, neg, adj, N, dtype=torch.float32)
+    out = run_step(params, pos, neg, N, R, D, cuda, gemm=gemm)
+    assert abs(out["loss"] - loss) <= max(4 * abs(loss32 - loss), 1e-6 * loss)
+    np.testing.assert_allclose(out["scores"], scores, rtol=0, atol=1e-5)
+    for k, v in g64.items():
+        scale = np.abs(v).max()
+        fp32_dev = np.abs(g32[k] - v).max() / scale
+        ours = np.abs(out["grads"][k].astype(np.float64) - v).max() / scale
+        assert ours <= max(4.0 * fp32_dev, 1e-5), f"grad {k}: {ours:.2e} vs fp32-oracle {fp32_dev:.2e}"
+
+
+def test_split_and_exact_gemm_modes_agree_at_scale(cuda):
+    """Config-3-shaped step (D=256, R=2, N=20k, 40k scored edges) at the reference-distribution
+    init the bench uses (E~U[0,1), K,S~N(0,1): pre-activations ~|800|, sigmoids saturated): the two
+    GEMM operand modes give the same loss to 1e-6 and the same scores to 1e-5, and finite gradients.
+    (In saturated regimes gradients move a lot under any rounding change — on a milder init with
+    loss ~3.2 the fp32 reference formulation already differs from fp64 by 5-33% of max|g| — so
+    gradient agreement is tested where it is meaningful, by the two tests above.)"""
+    N, R, D = 20000, 2, 256
+    pos, neg = synthetic_graph(N, R, 20000, seed=4)
+    params = init_params(N, R, D, seed=89)
+    a = run_step(params, pos, neg, N, R, D, cuda, gemm="split")
+    b = run_step(params, pos, neg, N, R, D, cuda, gemm="exact")
+    assert abs(a["loss"] - b["loss"]) <= 1e-6 * abs(b["loss"])
+    np.testing.assert_allclose(a["scores"], b["scores"], rtol=0, atol=1e-5)
+    for k in a["grads"]:
+        assert np.all(np.isfinite(a["grads"][k])), k
 
 
 def test_bitwise_determinism(golden, cuda):

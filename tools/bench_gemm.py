@@ -25,7 +25,8 @@ def run(T=4_000_000, N=100_000, D=256, R=2, reps=5, check=20_000):
     t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
     h = torch.randint(0, N, (T,), device=dev, generator=g).int()
     aux = torch.rand(T, D, device=dev, generator=g)
-    dO = torch.randn(T, D, device=dev, generator=g) * 1e-12
+    # gradient-like rows: tiny, spanning 6 decades from row to row (exercises the running scales)
+    dO = torch.randn(T, D, device=dev, generator=g) * 1e-12 * 10 ** (6 * torch.rand(T, 1, device=dev, generator=g) - 3)
     C = torch.empty(T, D, device=dev)
     slab = torch.empty(ops.tn_blocks(T, D) * D * D, device=dev)
     dS = torch.empty(D, D, device=dev)
@@ -42,8 +43,9 @@ def run(T=4_000_000, N=100_000, D=256, R=2, reps=5, check=20_000):
                                            act=L.ACT_SIGMOID),
         "bwd_dsig": lambda: ops.rowgemm(dO, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux),
         "plain": lambda: ops.rowgemm(A, S, C),
-        "tn": lambda: ops.gemm_tn(A, aux, dS, slab),
+        "tn": lambda: ops.gemm_tn(A, dO, dS, slab),
     }
+    tn_ref = A.double().t() @ dO.double()
     for mode, mname in ((L.GEMM_EXACT_F32, "exact"), (L.GEMM_SPLIT_F16, "split")):
         old = L.lib().iddgcn_set_gemm_precision(mode)
         try:
@@ -54,6 +56,9 @@ def run(T=4_000_000, N=100_000, D=256, R=2, reps=5, check=20_000):
                 if name in refs:
                     ref = refs[name]
                     e = ((C[:n].double() - ref).abs().max() / ref.abs().max()).item()
+                    err = f" relerr={e:.2e}"
+                elif name == "tn":
+                    e = ((dS.double() - tn_ref).abs().max() / tn_ref.abs().max()).item()
                     err = f" relerr={e:.2e}"
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()

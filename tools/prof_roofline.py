@@ -31,7 +31,11 @@ def main(trace, bench, name="rowgemm256_v3_kernel<2, false, true>", frac=0.5):
     print(f"edge launches     : {len(big)} ({per_step}/step), timed {len(timed)}")
     print(f"rocprof avg (ms)  : {avg:.4f}  min {timed['ms'].min():.4f}  max {timed['ms'].max():.4f}")
     print(f"bench avg (ms)    : {rl['avg_launch_ms']:.4f}  (HIP events, bench.py --no-cpu-baseline run)")
-    print(f"rocprof TFLOP/s   : {rl['flops_per_launch'] / avg / 1e9:.1f}  vs bench {rl['achieved']:.1f}")
+    if rl.get("unit") == "GB/s":
+        print(f"rocprof GB/s      : {rl['bytes_per_launch'] / avg / 1e6:.1f}  vs bench {rl['achieved']:.1f} "
+              f"(algorithmic {rl['bytes_per_launch'] / 1e9:.3f} GB per launch)")
+    else:
+        print(f"rocprof TFLOP/s   : {rl['flops_per_launch'] / avg / 1e9:.1f}  vs bench {rl['achieved']:.1f}")
 
 
 if __name__ == "__main__":
