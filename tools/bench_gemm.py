@@ -4,7 +4,8 @@ in both operand-precision modes (exact f32 MFMA, split-fp16 MFMA).
 For each case it prints the time per launch, the algorithmic TFLOP/s, and the max error of each
 mode against an fp64 torch reference on the first `check` rows (absolute, over max |ref|).
 
-usage: python tools/bench_gemm.py [T]
+usage: python tools/bench_gemm.py [T] [modes=exact,split] [lib.so ...]
+  (each library is loaded in turn on the same inputs: build-flag variants of the same source)
 """
 import sys
 
@@ -15,7 +16,15 @@ from iddgcn_amd import _lib as L  # noqa: E402
 from iddgcn_amd import ops  # noqa: E402
 
 
-def run(T=4_000_000, N=100_000, D=256, R=2, reps=5, check=20_000):
+def run(T=4_000_000, N=100_000, D=256, R=2, reps=5, check=20_000, modes=("exact", "split"), libs=()):
+    for lp in libs or [None]:
+        if lp:
+            L._lib = L.load(lp)
+            print(f"--- {lp}", flush=True)
+        run1(T, N, D, R, reps, check, modes)
+
+
+def run1(T, N, D, R, reps, check, modes):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     A = torch.rand(T, D, device=dev, generator=g)
@@ -47,6 +56,8 @@ def run(T=4_000_000, N=100_000, D=256, R=2, reps=5, check=20_000):
     }
     tn_ref = A.double().t() @ dO.double()
     for mode, mname in ((L.GEMM_EXACT_F32, "exact"), (L.GEMM_SPLIT_F16, "split")):
+        if mname not in modes:
+            continue
         old = L.lib().iddgcn_set_gemm_precision(mode)
         try:
             for name, fn in cases.items():
@@ -73,4 +84,6 @@ def run(T=4_000_000, N=100_000, D=256, R=2, reps=5, check=20_000):
 
 
 if __name__ == "__main__":
-    run(*(int(a) for a in sys.argv[1:2]))
+    a = sys.argv[1:]
+    run(T=int(a[0]) if a else 4_000_000, modes=tuple(a[1].split(",")) if len(a) > 1 else ("exact", "split"),
+        libs=a[2:])
