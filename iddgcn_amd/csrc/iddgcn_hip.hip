@@ -538,6 +538,7 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
 namespace r3 {
 constexpr int D = 256, NW = 8, TR = 32;
 constexpr int ROWS_PER_WAVE = TR / NW;                 // A rows each wave stages
+static_assert(ROWS_PER_WAVE == 4, "the early-wave s_waitcnt vmcnt(4) counts the A-row DMAs");
 constexpr int LDA = D + 4;                             // padded rows: conflict-free ds_read_b128
 constexpr int A_FLOATS = TR * LDA;                     // 33,280 B
 constexpr int SLAB = TR * 32;                          // 32 rows x 32 cols
@@ -772,11 +773,15 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     // rewrites exactly the slots it read), then re-read row-major for 4 buffer_store_dwordx4
     // per wave through a per-tile buffer resource whose range check drops rows past M.
     const int sw = (i >> 1) & 7;
-    auto epilogue = [&](long long t, const f32x16& acc) {
+    auto out_rsrc = [&](long long t) {
         const long long row0 = t * TR;
         const long long left = (long long)p.M - row0;
         const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
-        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.C + row0 * D, (short)0, nbytes, 0x00020000);
+        return __builtin_amdgcn_make_buffer_rsrc(p.C + row0 * D, (short)0, nbytes, 0x00020000);
+    };
+    // stage phase: combine + activation into slab 0 (LDS only, plus the C loads of `accumulate`)
+    auto epi_stage = [&](long long t, const f32x16& acc) {
+        const __amdgpu_buffer_rsrc_t rc = out_rsrc(t);
         float cf[NS_MAX] = {0.f, 0.f};
         if (HAS_COEF) {
             if (NV == 2 || (NV == 0 && R == 2)) {
@@ -819,6 +824,10 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             }
             st4(slabw + off, v);
         }
+    };
+    // store phase: row-major re-read of slab 0, 4 buffer_store_dwordx4 per wave
+    auto epi_store = [&](long long t) {
+        const __amdgpu_buffer_rsrc_t rc = out_rsrc(t);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -830,6 +839,10 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             }
             __builtin_amdgcn_raw_buffer_store_b128(o, rc, (row * D + c0 + cg * 4) * 4, 0, 0);
         }
+    };
+    auto epilogue = [&](long long t, const f32x16& acc) {
+        epi_stage(t, acc);
+        epi_store(t);
     };
 
     // ---- prologue: A(t_beg), indices and epilogue slabs of t_beg, indices of t_beg+1 ------
@@ -861,6 +874,8 @@ _Pragma("unroll") \
         for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
         int b = 0; \
         for (long long t = t_beg; t < t_end; ++t, b ^= 1) { \
+            /* A(t+1) first: buffer b^1 held tile t-1, whose MFMAs ended before the last barrier */ \
+            if (t + 1 < t_end) dma_A(t + 1, b ^ 1); \
             if (LATE && t > t_beg) { \
                 epilogue(t - 1, acc); \
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
@@ -868,7 +883,6 @@ _Pragma("unroll") \
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
                 dma_idx(t + 1); \
             } \
-            if (t + 1 < t_end) dma_A(t + 1, b ^ 1); \
             const int an = load_aidx(t + 2); \
             if constexpr (!X3) { \
 _Pragma("unroll") \
@@ -886,7 +900,7 @@ _Pragma("unroll") \
                     __builtin_amdgcn_sched_barrier(0); \
                     a_cur = a_nxt; \
                 } \
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+                if (LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
             } else { \
                 f32x16 acc_hi, acc_lo; \
 _Pragma("unroll") \
@@ -917,11 +931,19 @@ _Pragma("unroll") \
                     for (int q = 0; q < 4; ++q) \
                         acc[4 * j + q] = (fmaf(acc_lo[4 * j + q], 0x1p-11f, acc_hi[4 * j + q]) * ri) * cv[q]; \
                 } \
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
-                if (t + 1 < t_end) convert_rows(b ^ 1); \
+                if (LATE) { \
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+                    if (t + 1 < t_end) convert_rows(b ^ 1); \
+                } \
             } \
             if (!LATE) { \
-                epilogue(t, acc); \
+                /* slabs(t) landed; A(t+1) (the last ROWS_PER_WAVE loads issued) may still fly */ \
+                if (t + 1 < t_end && !p.a_idx) asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); \
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+                epi_stage(t, acc); \
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+                if (X3 && t + 1 < t_end) convert_rows(b ^ 1); \
+                epi_store(t); \
                 if (t + 1 < t_end) { \
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
                     dma_slabs(t + 1); \
