@@ -12,3 +12,4 @@ from .graph import get_adj_mats  # noqa: F401
 from .model import (Adam, BinaryCrossentropy, DistMult, IDDGCN_Layer, IDDGCN_Model,  # noqa: F401
                     SaveWeightsCallback, get_IDDGCN_Model)
 from .utils import generate_reverse_triplets, get_y_true  # noqa: F401
+from . import explain  # noqa: F401,E402  (explaiNE / GNNExplainer / IDDGCN explainer on the HIP path)

@@ -38,6 +38,7 @@ class RowGemmArgs(ctypes.Structure):
 SIGNATURES = {
     "iddgcn_abi_version": (ci, []),
     "iddgcn_spmm_csr_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, ci]),
+    "iddgcn_sddmm_csr_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
     "iddgcn_rowgemm_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
     "iddgcn_set_rowgemm_path": (ci, [ci]),
     "iddgcn_set_gemm_precision": (ci, [ci]),

@@ -214,6 +214,49 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(int n_seg, int n_rows, co
 }
 
 // ---------------------------------------------------------------------------
+// CSR SDDMM (gradient of A·X w.r.t. A's stored values): out[k] = <G[seg row], X[col[k]]>.
+// One row per group of D/4 lanes; the G row stays in registers, two X rows in flight, each dot
+// reduced across the group.  Output in CSR order.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void sddmm_csr_kernel(int n_seg, int n_rows, const int* __restrict__ ptr,
+                                                        const int* __restrict__ col, const float* __restrict__ G,
+                                                        const float* __restrict__ X, float* __restrict__ out) {
+    constexpr int LPR = D / 4;
+    const long long grow = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
+    // groups of one wave may hold different rows: every lane runs the wave's longest row
+    const bool live = grow < (long long)n_seg * n_rows;
+    int beg = 0, end = 0;
+    f32x4 g = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        const int s = (int)(grow / n_rows);
+        const int n = (int)(grow % n_rows);
+        const int* p = ptr + (long long)s * (n_rows + 1);
+        beg = p[n];
+        end = p[n + 1];
+        g = ld4(G + grow * D + sub * 4);
+    }
+    int len = end - beg, maxlen = len;
+    if (LPR < 64) {
+#pragma unroll
+        for (int m = 32; m >= LPR; m >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, m, 64));
+    }
+    for (int k = 0; k < maxlen; k += 2) {
+        const bool ok0 = k < len, ok1 = k + 1 < len;
+        const f32x4 x0 = ok0 ? ld4(X + (long long)col[beg + k] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 x1 = ok1 ? ld4(X + (long long)col[beg + k + 1] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 p0 = g * x0, p1 = g * x1;
+        const float d0 = group_sum<LPR>((p0[0] + p0[1]) + (p0[2] + p0[3]));
+        const float d1 = group_sum<LPR>((p1[0] + p1[1]) + (p1[2] + p1[3]));
+        if (sub == 0) {
+            if (ok0) out[beg + k] = d0;
+            if (ok1) out[beg + k + 1] = d1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Row GEMM with fused epilogue on v_mfma_f32_32x32x2_f32.
 //   wave w: column slab cs = w % CS (32 output columns), row group rg = w / CS.
 //   B slab resident in VGPRs: breg[s] = B[kk(s,h)][c0+i],  kk(s,h) = 8(s/4) + 4h + s%4,
@@ -1742,7 +1785,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
             for (int u = 0; u < U; ++u) {
                 const bool ok = e[u] >= 0;
                 rr[u] = ok ? r_idx[e[u]] : 0;
-                yy[u] = ok ? y[e[u]] : 0.f;
+                yy[u] = (ok && y) ? y[e[u]] : 0.f;
                 b[u] = ok ? ld4(Xt + e[u] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
 #pragma unroll
@@ -1758,14 +1801,20 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 if (e[u] < 0) continue;
                 const float p = sigmoidf_(sc[u]);
                 if (p_out && sub == 0) p_out[e[u]] = p;
-                const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
-                const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
-                const float g =
-                    pass ? scale * (-(yy[u] / (pc + EPS_BCE)) + (1.0f - yy[u]) / (1.0f - pc + EPS_BCE)) : 0.f;
+                float g, lterm;
+                if (y) {        // Keras BCE seed
+                    const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
+                    const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
+                    g = pass ? scale * (-(yy[u] / (pc + EPS_BCE)) + (1.0f - yy[u]) / (1.0f - pc + EPS_BCE)) : 0.f;
+                    lterm = -(yy[u] * logf(pc + EPS_BCE) + (1.0f - yy[u]) * logf(1.0f - pc + EPS_BCE));
+                } else {        // prediction seed: gradient of scale * sum_e p_e
+                    g = scale;
+                    lterm = p;
+                }
                 const float ds = g * p * (1.0f - p);
                 if (sub == 0) {
                     if (ds_out) ds_out[e[u]] = ds;
-                    lacc += -(yy[u] * logf(pc + EPS_BCE) + (1.0f - yy[u]) * logf(1.0f - pc + EPS_BCE));
+                    lacc += lterm;
                 }
                 f32x4 dx = (ds * rho[u]) * a;
                 dx = dx * (b[u] * (1.0f - b[u]));
@@ -2081,6 +2130,25 @@ int iddgcn_spmm_csr_f32(void* stream, int n_seg, int n_rows, int d, const int* r
     return launch_status();
 }
 
+int iddgcn_sddmm_csr_f32(void* stream, int n_seg, int n_rows, int d, const int* row_ptr, const int* col,
+                         const float* G, const float* X, float* out) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (n_seg < 0 || n_rows < 0 || !row_ptr || !col || !G || !X || !out) return IDDGCN_E_BAD_ARG;
+    const long long rows = (long long)n_seg * n_rows;
+    if (rows == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = grid_for(rows, d / 4);
+#define SDK(DD) hipLaunchKernelGGL(sddmm_csr_kernel<DD>, dim3(grid), dim3(256), 0, st, n_seg, n_rows, row_ptr, col, G, X, out)
+    switch (d) {
+        case 32: SDK(32); break;
+        case 64: SDK(64); break;
+        case 128: SDK(128); break;
+        default: SDK(256); break;
+    }
+#undef SDK
+    return launch_status();
+}
+
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     if (!a) return IDDGCN_E_BAD_ARG;
     if (!dim_ok(a->D)) return IDDGCN_E_BAD_DIM;
@@ -2325,7 +2393,7 @@ int iddgcn_distmult_bce_heads_f32(void* stream, int n_nodes, int d, int R, const
                                   float* dXh, float* drel_slab, float* loss_slab, int n_blocks) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
-    if (n_nodes < 0 || n_blocks < 1 || !seg_ptr || !perm || !Xh || !Xt || !r_idx || !rel || !y || !do_out ||
+    if (n_nodes < 0 || n_blocks < 1 || !seg_ptr || !perm || !Xh || !Xt || !r_idx || !rel || !do_out ||
         !dXh || !drel_slab || !loss_slab)
         return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;

@@ -223,14 +223,18 @@ class Engine:
         if train:
             # one pass over head segments: p / loss / drel partials, the tail seed do^3 (per edge)
             # and the head seed dO^3[n] = X3(1-X3) * sum_{h_e=n} ds_e rel[r_e] * x3_e
-            scale = 1.0 / (float(self._t_global or T) * float(N))
-            ops.distmult_bce_heads(ed.hptr, ed.hperm, ws.X[2], ws.xt[2], ed.r, P["rel"], ed.y, ws.dE_a, ws.dOn_a,
+            if self._pred_seed is None:        # Keras BCE, x 1/num_entities (IDDGCN.py:161-168)
+                scale, y = 1.0 / (float(self._t_global or T) * float(N)), ed.y
+            else:                              # d(scale * sum_e p_e): the explainers' seed
+                scale, y = float(self._pred_seed), None
+            ops.distmult_bce_heads(ed.hptr, ed.hperm, ws.X[2], ws.xt[2], ed.r, P["rel"], y, ws.dE_a, ws.dOn_a,
                                    ws.drel_slab, ws.loss_slab, scale=scale, p_out=ws.p if self._want_p else None)
         else:
             ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], p_out=ws.p)
 
     _t_global = None
     _want_p = False        # per-edge probabilities are only materialised for loss_and_grads
+    _pred_seed = None      # None: BCE seed; a float: gradient of pred_seed * sum_e p_e
 
     # -- backward -----------------------------------------------------------
     def backward(self, P, G, adj, ed, ws):
@@ -308,6 +312,35 @@ class Engine:
         with self._precision():
             self.backward(params, grads, adj, ed, ws)
         return ws.loss, ed.unsort(ws.p)
+
+
+    def value_grads(self, params, adj, ed, scale=1.0, grads=None):
+        """Gradient of ``scale * sum_e p_e`` (p = the model's predicted probabilities of the scored
+        edges ``ed``) w.r.t. every stored adjacency value, and p.
+
+        This is ``tape.gradient(pred, adj_mat.values)`` of the explainers (explaiNE.py:85-94,
+        GnnExplainer.py:31-51): AE_r = A_r·E enters every layer, so with dAE_r the total gradient
+        w.r.t. AE_r (summed over the 3 layers by the backward), d/dA_r[i,j] = <dAE_r[i], E[j]>, one
+        SDDMM over the adjacency.  Returns (list of per-relation GPU tensors in the adjacency's
+        entry order, p in the caller's edge order).  ``grads``: optional FlatParams that receives
+        the parameter gradients of the same quantity (a scratch buffer is used otherwise).
+        """
+        N, R, D = self.N, self.R, self.D
+        ws = self.workspace(ed.T, True)
+        if grads is None:
+            if getattr(self, "_scratch_grads", None) is None:
+                self._scratch_grads = FlatParams(N, R, D, self.device)
+            grads = self._scratch_grads
+        self._pred_seed, self._want_p = float(scale), True
+        try:
+            with self._precision():
+                self.forward(params, adj, ed, ws, True)
+                self.backward(params, grads, adj, ed, ws)
+        finally:
+            self._pred_seed, self._want_p = None, False
+        dv = torch.empty(adj.total_nnz, dtype=torch.float32, device=self.device)
+        ops.sddmm_csr(adj.fwd_ptr, adj.fwd_col, ws.dAE, params["E"], dv, R, N)
+        return adj.to_entry_order(dv), ed.unsort(ws.p)
 
 
 def step_flops(N, R, D, T, M):

@@ -91,11 +91,12 @@ class DeviceAdjacency:
         N = num_entities
         self.num_entities = N
         self.num_relations = len(adj_mats)
-        fptr, fcol, fval = [], [], []
+        fptr, fcol, fval, fsrc = [], [], [], []
         bc, bm, bv = [], [], []
         off_f = 0
         any_val = False
         self.nnz = []
+        self.rows, self.cols = [], []          # host copies, per relation, in the caller's entry order
         for r, a in enumerate(adj_mats):
             rows = np.asarray(a.rows, dtype=np.int64)
             cols = np.asarray(a.cols, dtype=np.int64)
@@ -107,11 +108,14 @@ class DeviceAdjacency:
             fptr.append(p + off_f)
             fcol.append(c)
             fval.append(vals[o])
+            fsrc.append(o + off_f)
             off_f += c.size
             bc.append(cols)
             bm.append(rows + r * N)
             bv.append(vals)
             self.nnz.append(int(rows.size))
+            self.rows.append(rows)
+            self.cols.append(cols)
         if off_f > INT32_MAX or N * len(adj_mats) > INT32_MAX:
             raise IddgcnError("adjacency too large for int32 offsets")
         # Backward: dE[c] += sum_r sum_{m: (m,c) in A_r} dAE[r][m].  One merged CSR of
@@ -126,6 +130,29 @@ class DeviceAdjacency:
         self.fwd_val = t(np.concatenate(fval), np.float32) if any_val else None
         self.bwd_val = t(bv[border], np.float32) if any_val else None
         self.total_nnz = off_f
+        # entry k of the concatenated per-relation value lists (caller order) sits at CSR position
+        # fwd_pos[k] of the forward CSR; the merged backward CSR reads value bwd_src[j]
+        self.base_values = t(bv, np.float32)
+        self.fwd_src = t(np.concatenate(fsrc), np.int64)
+        self.fwd_pos = torch.empty_like(self.fwd_src)
+        self.fwd_pos[self.fwd_src] = torch.arange(off_f, device=device)
+        self.bwd_src = t(border, np.int64)
+        self.rel_offsets = np.concatenate([[0], np.cumsum(self.nnz)]).astype(np.int64)
+        self.device = device
+
+    def set_values(self, values):
+        """Replace the stored values (a (total_nnz,) GPU tensor in the caller's entry order, relation
+        after relation) without rebuilding the CSR: ``adj * sigmoid(mask)`` of the explainers."""
+        if values.shape != (self.total_nnz,):
+            raise IddgcnError(f"values must have shape ({self.total_nnz},)")
+        v = values.to(device=self.fwd_src.device, dtype=torch.float32)
+        self.fwd_val = v[self.fwd_src].contiguous()
+        self.bwd_val = v[self.bwd_src].contiguous()
+
+    def to_entry_order(self, csr_vals):
+        """Per-entry quantity in forward-CSR order -> list of per-relation tensors in entry order."""
+        flat = csr_vals[self.fwd_pos]
+        return [flat[self.rel_offsets[r]:self.rel_offsets[r + 1]] for r in range(self.num_relations)]
 
 
 class ScoredEdges:

@@ -52,6 +52,18 @@ def spmm_csr(row_ptr, col, vals, X, Y, n_seg, n_rows, accumulate=False):
                                         _ptr(X), _ptr(Y), int(accumulate)), "spmm_csr")
 
 
+def sddmm_csr(row_ptr, col, G, X, out, n_seg, n_rows):
+    """out[k] = <G[s][row(k)], X[col[k]]> over the batched CSR (gradient w.r.t. adjacency values)."""
+    D = X.shape[1]
+    _req(row_ptr, _I32, (n_seg * (n_rows + 1),), "row_ptr")
+    _req(col, _I32, None, "col")
+    _req(G, _F32, (n_seg, n_rows, D), "G")
+    _req(X, _F32, None, "X")
+    _req(out, _F32, (col.shape[0],), "out")
+    L.check(L.lib().iddgcn_sddmm_csr_f32(_stream(), n_seg, n_rows, D, _ptr(row_ptr), _ptr(col), _ptr(G), _ptr(X),
+                                         _ptr(out)), "sddmm_csr")
+
+
 def rowgemm(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, coef_idx=None, V=None,
             v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None):
     D = B.shape[0]
@@ -170,7 +182,8 @@ def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_
 
 def distmult_bce_heads(seg_ptr, perm, Xh, Xt, r_idx, rel, y, do_out, dXh, drel_slab, loss_slab, *, scale=1.0,
                       p_out=None, ds_out=None):
-    """Training DistMult + BCE + tail seed (do_out) + head seed (dXh) in one pass over head segments."""
+    """Training DistMult + BCE + tail seed (do_out) + head seed (dXh) in one pass over head segments.
+    y=None selects the prediction seed (gradient of scale * sum_e p_e; loss slabs sum p_e)."""
     T = r_idx.shape[0]
     n_nodes, D = dXh.shape
     R = rel.shape[0]

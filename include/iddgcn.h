@@ -47,6 +47,16 @@ int iddgcn_spmm_csr_f32(void* stream, int n_seg, int n_rows, int d,
                         const int* row_ptr, const int* col, const float* vals,
                         const float* X, float* Y, int accumulate);
 
+/* out[k] = sum_c G[s*n_rows + n][c] * X[col[k]][c]   for every stored entry k of row n of
+ * segment s (same batched CSR as iddgcn_spmm_csr_f32; out in CSR order).  With G = dAE_r (the
+ * gradient w.r.t. A_r·E) and X = E this is the gradient w.r.t. the adjacency VALUES that the
+ * explainers take: tape.gradient(pred, adj_mat.values) (explanation/explaiNE.py:17) and the
+ * mask gradients of adj*sigmoid(mask) (explanation/GnnExplainer.py:33,51,
+ * explanation/IDDGCN_explain.py:52,80). */
+int iddgcn_sddmm_csr_f32(void* stream, int n_seg, int n_rows, int d,
+                         const int* row_ptr, const int* col,
+                         const float* G, const float* X, float* out);
+
 /* Row GEMM on f32 MFMA with a fused epilogue.  For e in [0, M), c in [0, D):
  *   v  = sum_k A[a_idx ? a_idx[e] : e][k] * (b_trans ? B[c][k] : B[k][c])
  *   v += accumulate ? C[e][c] : 0
@@ -141,6 +151,9 @@ int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R,
  * which is iddgcn_seg_gather_reduce_f32(seg_ptr, perm, ds, r_idx, rel, Xt, Xh).  Rows of nodes with
  * no edge get zeros.  n_blocks from iddgcn_distmult_blocks(); the drel / loss partials are
  * per block, as for iddgcn_distmult_bce_f32.
+ * y == NULL selects the PREDICTION seed: g = scale for every edge (the gradient of
+ * scale * sum_e p_e, no clipping) and loss_slab accumulates sum_e p_e — the seed of the
+ * explainers' tape.gradient(pred, ...) (explanation/explaiNE.py:85-94).
  * Replaces IDDGCN.py:103-109 + the loss of 161-168 and the head-side gradient of
  * DistMult's embedding lookup, one launch. */
 int iddgcn_distmult_bce_heads_f32(void* stream, int n_nodes, int d, int R, const int* seg_ptr,

@@ -62,6 +62,35 @@ def test_spmm_csr(D, cuda):
 
 
 @pytest.mark.parametrize("D", DIMS)
+def test_sddmm_csr(D, cuda):
+    """out[k] = <G[s][row_k], X[col_k]> over a batched CSR with empty rows and one long row."""
+    g = torch.Generator().manual_seed(100 + D)
+    N, R = 301, 3
+    ptrs, cols, rows_all, off = [], [], [], 0
+    for r in range(R):
+        rows = torch.randint(0, N, (2000,), generator=g)
+        rows[:300] = 5                                  # one long row
+        rows = rows[rows % 7 != 3]                      # some empty rows
+        c = torch.randint(0, N, (rows.numel(),), generator=g)
+        key = torch.unique(rows * N + c)
+        rr, cc = key // N, key % N
+        ptr = torch.zeros(N + 1, dtype=torch.int64)
+        ptr[1:] = torch.cumsum(torch.bincount(rr, minlength=N), 0)
+        ptrs.append(ptr + off)
+        cols.append(cc)
+        rows_all.append(rr + r * N)
+        off += cc.numel()
+    ptr = torch.cat(ptrs).to(torch.int32).to(cuda)
+    col = torch.cat(cols).to(torch.int32).to(cuda)
+    Gm, Xm = rnd(R, N, D, dev=cuda, gen=g), rnd(N, D, dev=cuda, gen=g)
+    out = torch.full((off,), 7.0, device=cuda)
+    ops.sddmm_csr(ptr, col, Gm.float(), Xm.float(), out, R, N)
+    rows = torch.cat(rows_all).to(cuda)
+    ref = (Gm.view(R * N, D)[rows] * Xm[torch.cat(cols).to(cuda)]).sum(-1)
+    close(out, ref, 1e-5 * np.sqrt(D))
+
+
+@pytest.mark.parametrize("D", DIMS)
 @pytest.mark.parametrize("trans", [False, True])
 def test_rowgemm_plain(D, trans, cuda):
     g = torch.Generator().manual_seed(7 * D + trans)
