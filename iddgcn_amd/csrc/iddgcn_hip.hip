@@ -616,6 +616,23 @@ __device__ __forceinline__ void split16(float xs, _Float16& hi, _Float16& lo) {
     hi = (_Float16)xs;
     lo = (_Float16)((xs - (float)hi) * 2048.0f);
 }
+// maxima over the 64 lanes of four values at once (halving butterfly: 2 + 1 swaps, 4 DPP steps);
+// on return m[j] is wave-uniform
+__device__ __forceinline__ void wave_max4(float (&m)[4]) {
+    float a0 = m[0], b0 = m[2], a1 = m[1], b1 = m[3];
+    pl_swap32(a0, b0);                 // lanes < 32: value 0 / 1, lanes >= 32: value 2 / 3
+    pl_swap32(a1, b1);
+    float v0 = fmaxf(a0, b0), v1 = fmaxf(a1, b1);
+    pl_swap16(v0, v1);                 // 16-lane row k holds value k
+    float v = fmaxf(v0, v1);
+    v = fmaxf(v, xpartner_dpp<8>(v));
+    v = fmaxf(v, xpartner_dpp<4>(v));
+    v = fmaxf(v, xpartner_dpp<2>(v));
+    v = fmaxf(v, xpartner_dpp<1>(v));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        m[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16 * j));
+}
 __device__ __forceinline__ float wave_max(float v) {             // max over the 64 lanes
     float a = v, b = v;
     pl_swap32(a, b);
@@ -634,17 +651,25 @@ template <int NV, bool AUX, bool HAS_COEF, bool X3>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     using namespace r3;
     constexpr int NS = NV + (AUX ? 1 : 0);
-    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+    // A-tile pipeline depth: three buffers (A(t+2) in flight while A(t) feeds the MFMAs) when the
+    // wave slabs leave room for them (NS <= 1), two otherwise
+    constexpr int NBUF = NS >= 2 ? 2 : 3;
+    constexpr int PD = NBUF - 1;                       // prefetch distance in tiles
+    constexpr int NSL = NS > 1 ? NS : 1;               // slabs per wave (slab 0 also stages C)
+    constexpr int WF = NSL * SLAB + COEF + IDX + CMP + CINV;
+    constexpr int LDSF = NBUF * A_FLOATS + NW * WF + NBUF * TR;
+    static_assert(LDSF * 4 <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) float lds[LDSF];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool late = V3_STAGGER && wave >= 4;         // staggered half
     const int i = lane & 31, h = lane >> 5;
     const int c0 = wave * 32;
     float* bufA = lds;
-    float* slabw = lds + 2 * A_FLOATS + wave * WAVE_FLOATS;   // [NS][32][32]
-    float* coefw = slabw + NS_MAX * SLAB;                     // [32][R]
-    float* cinvw = slabw + WAVE_FLOATS - CINV;                 // [32] (X3)
-    float* rowinv = lds + 2 * A_FLOATS + NW * WAVE_FLOATS;     // [2][TR] (X3)
+    float* slabw = lds + NBUF * A_FLOATS + wave * WF;          // [NSL][32][32]
+    float* coefw = slabw + NSL * SLAB;                         // [32][R]
+    float* cinvw = slabw + WF - CINV;                          // [32] (X3)
+    float* rowinv = lds + NBUF * A_FLOATS + NW * WF;           // [NBUF][TR] (X3)
     const int R = p.R;
 
     // weights: exact f32 (breg, B[kk][c0+i] for 4 k-steps of 32x32x2 per ds_read) or, X3, the
@@ -688,8 +713,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
                 x[j] = ld4(base + (wave * ROWS_PER_WAVE + j) * LDA + lane * 4);
                 m[j] = fmaxf(fmaxf(fabsf(x[j][0]), fabsf(x[j][1])), fmaxf(fabsf(x[j][2]), fabsf(x[j][3])));
             }
-#pragma unroll
-            for (int j = 0; j < ROWS_PER_WAVE; ++j) m[j] = wave_max(m[j]);
+            wave_max4(m);
 #pragma unroll
             for (int j = 0; j < ROWS_PER_WAVE; ++j) {
                 const int r = wave * ROWS_PER_WAVE + j;
@@ -895,15 +919,29 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         to_sgpr(a0);
         dma_A(t_beg, 0);
-        const int a1 = load_aidx(t_beg + 1);
+        if constexpr (PD == 2) {
+            const int a1 = load_aidx(t_beg + 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            to_sgpr(a1);
+            dma_A(t_beg + 1, 1);
+        }
+        const int an0 = load_aidx(t_beg + PD);
         dma_slabs(t_beg);
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         convert_rows(0);
         dma_idx(t_beg + 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        to_sgpr(a1);
+        to_sgpr(an0);
         __syncthreads();
     }
+    // s_waitcnt vmcnt(n): everything but the n youngest vector-memory ops of this wave has landed
+    // (LDS-DMA, loads and stores count together, in issue order)
+    auto wait_newest = [&](int n) {
+        if (n >= 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
 
     // ---- main loop, specialised per half: LATE waves run epilogue(t-1) before MFMA(t),
     // early waves epilogue(t) after it.  Branching once per wave into two compile-time copies
@@ -915,18 +953,22 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
         f32x16 acc; \
 _Pragma("unroll") \
         for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
-        int b = 0; \
-        for (long long t = t_beg; t < t_end; ++t, b ^= 1) { \
-            /* A(t+1) first: buffer b^1 held tile t-1, whose MFMAs ended before the last barrier */ \
-            if (t + 1 < t_end) dma_A(t + 1, b ^ 1); \
+        int b = 0, b1 = 1, b2 = 2 % NBUF;     /* buffers of tiles t, t+1, t+2 */ \
+        for (long long t = t_beg; t < t_end; ++t) { \
+            /* A(t+PD) into the buffer of tile t-1 (its MFMAs ended before the last barrier) */ \
+            const bool more = t + PD < t_end; \
+            if (more) dma_A(t + PD, PD == 2 ? b2 : b1); \
+            const int an = load_aidx(t + PD + 1); \
+            /* ops issued so far this iteration (the youngest): A(t+PD) rows, the a_idx load */ \
+            const int n_new = (more ? ROWS_PER_WAVE : 0) + ((p.a_idx && t + PD + 1 < t_end) ? 1 : 0); \
             if (LATE && t > t_beg) { \
+                wait_newest(n_new);          /* slabs(t-1), idx(t) and every older op */ \
                 epilogue(t - 1, acc); \
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
                 dma_slabs(t); \
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
                 dma_idx(t + 1); \
             } \
-            const int an = load_aidx(t + 2); \
             if constexpr (!X3) { \
 _Pragma("unroll") \
                 for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
@@ -943,27 +985,26 @@ _Pragma("unroll") \
                     __builtin_amdgcn_sched_barrier(0); \
                     a_cur = a_nxt; \
                 } \
-                if (LATE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
             } else { \
                 f32x16 acc_hi, acc_lo; \
 _Pragma("unroll") \
                 for (int j = 0; j < 16; ++j) acc_hi[j] = acc_lo[j] = 0.f; \
                 const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
-                f16x8 ah = __builtin_bit_cast(f16x8, ld4(arow)); \
-                f16x8 al = __builtin_bit_cast(f16x8, ld4(arow + 128)); \
+                /* fragments of k-steps q and q+1 in alternating registers (no copies) */ \
+                f16x8 ah[2], al[2]; \
+                ah[0] = __builtin_bit_cast(f16x8, ld4(arow)); \
+                al[0] = __builtin_bit_cast(f16x8, ld4(arow + 128)); \
 _Pragma("unroll") \
                 for (int q = 0; q < D / 16; ++q) { \
-                    f16x8 ah_n = ah, al_n = al; \
+                    const int cu = q & 1; \
                     if (q + 1 < D / 16) { \
-                        ah_n = __builtin_bit_cast(f16x8, ld4(arow + 8 * (q + 1))); \
-                        al_n = __builtin_bit_cast(f16x8, ld4(arow + 128 + 8 * (q + 1))); \
+                        ah[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + 8 * (q + 1))); \
+                        al[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + 128 + 8 * (q + 1))); \
                     } \
-                    acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], ah, acc_hi, 0, 0, 0); \
-                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], al, acc_lo, 0, 0, 0); \
-                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(blo[q], ah, acc_lo, 0, 0, 0); \
+                    acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], ah[cu], acc_hi, 0, 0, 0); \
+                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], al[cu], acc_lo, 0, 0, 0); \
+                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(blo[q], ah[cu], acc_lo, 0, 0, 0); \
                     __builtin_amdgcn_sched_barrier(0); \
-                    ah = ah_n; \
-                    al = al_n; \
                 } \
                 /* unscale: row i (1/s_row of this buffer), columns c0+8j+4h+q (1/s_col) */ \
                 const float ri = rowinv[b * TR + i]; \
@@ -974,18 +1015,16 @@ _Pragma("unroll") \
                     for (int q = 0; q < 4; ++q) \
                         acc[4 * j + q] = (fmaf(acc_lo[4 * j + q], 0x1p-11f, acc_hi[4 * j + q]) * ri) * cv[q]; \
                 } \
-                if (LATE) { \
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
-                    if (t + 1 < t_end) convert_rows(b ^ 1); \
-                } \
             } \
-            if (!LATE) { \
-                /* slabs(t) landed; A(t+1) (the last ROWS_PER_WAVE loads issued) may still fly */ \
-                if (t + 1 < t_end && !p.a_idx) asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); \
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+            if (LATE) { \
+                /* A(t+1): issued this iteration (PD 1) or before slabs(t-1) (PD 2, landed) */ \
+                if (PD == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+                if (t + 1 < t_end) convert_rows(b1); \
+            } else { \
+                wait_newest(n_new);              /* slabs(t), idx(t+1) (and A(t+1) when PD 2) */ \
                 epi_stage(t, acc); \
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
-                if (X3 && t + 1 < t_end) convert_rows(b ^ 1); \
+                if (PD == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+                if (X3 && t + 1 < t_end) convert_rows(b1); \
                 epi_store(t); \
                 if (t + 1 < t_end) { \
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
@@ -998,8 +1037,12 @@ _Pragma("unroll") \
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
             __builtin_amdgcn_s_barrier(); \
             asm volatile("" ::: "memory"); \
+            const int bt = b; b = b1; b1 = (PD == 2) ? b2 : bt; b2 = bt; \
         } \
-        if (LATE) epilogue(t_end - 1, acc); \
+        if (LATE) { \
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+            epilogue(t_end - 1, acc); \
+        } \
     }
     if (V3_PRIO && late) __builtin_amdgcn_s_setprio(1);
     if (late) V3_MAIN_LOOP(true) else V3_MAIN_LOOP(false)
