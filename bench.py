@@ -74,6 +74,29 @@ def kernel_roofline(name, N, R, D, T, gemm, avg_ms):
     return out
 
 
+def stream_probe(dev, T, D, reps=3):
+    """What this box's HBM sustains for the access mixes of the edge kernels, measured in the same
+    run on one edge table (T x D fp32): write-only (fill), read+write 1:1 (copy), read-only
+    (sum).  Context for roofline.frac, whose peak is the 8 TB/s vendor figure."""
+    a = torch.empty(T, D, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    out = {}
+    for name, fn, nbytes in (("fill", lambda: a.fill_(1.0), a.numel() * 4),
+                             ("copy", lambda: b.copy_(a), 2 * a.numel() * 4),
+                             ("read", lambda: a.sum(), a.numel() * 4)):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        out[name] = nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9
+    del a, b
+    return out
+
+
 def pmc_traffic(kernel, gemm, workload, world):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same bench
     command (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x2 per the
@@ -232,6 +255,7 @@ def main():
     avg_ms = statistics.mean(kt[dom])
     rl = kernel_roofline(dom, N, R, D, T_local, args.gemm, avg_ms)
     rl["traffic"], rl["traffic_source"] = pmc_traffic(dom, args.gemm, cfg["name"], world)
+    rl["box_stream_GBs"] = stream_probe(dev, ed.T, D)
 
     ms = elapsed / args.steps * 1e3
     result = {
