@@ -87,6 +87,16 @@ def test_explaine_matches_oracle(golden, cuda):
         _check_topk(ours_p[k], ours_s[k], ref_p[k], ref_s[k], 2e-4 * np.abs(ref_s[k]).max())
 
 
+def test_explaine_graph_replay_equals_eager(golden, cuda):
+    """The HIP-graph path (device-side single-edge layout + torch.sort ranking, replayed per triple)
+    returns bitwise the eager path's scores and the same triples, over 12 consecutive triples."""
+    model, w, adjacency, test = _setup(golden)
+    ge_p, ge_s = X.explaine(model, adjacency, test[:12], top_k=10, graph=False)
+    gr_p, gr_s = X.explaine(model, adjacency, test[:12], top_k=10, graph=True)
+    assert np.array_equal(gr_s, ge_s)
+    assert np.array_equal(gr_p, ge_p)
+
+
 @pytest.mark.parametrize("kind", ["gnnexplainer", "iddgcn"])
 def test_mask_explainers_match_oracle(kind, golden, cuda):
     """GnnExplainer.py (5 epochs, thr .2) and IDDGCN_explain.py (10 epochs, thr .15, ratio loss), three
