@@ -308,18 +308,14 @@ class IDDGCN_Model:
         return dadj
 
     def save_weights(self, filepath):
+        """Keras-h5 for a ``.h5`` path (IDDGCN.py:181-199; h5py or the built-in writer), else .npz."""
         self._sync_to_host()
         d = self._named()
-        if filepath.endswith(".h5"):
-            try:
-                import h5py  # noqa: F401
-            except ImportError:
-                filepath = filepath[:-3] + ".npz"
+        os.makedirs(os.path.dirname(os.path.abspath(filepath)), exist_ok=True)
         if filepath.endswith(".h5"):
             from .weights_io import save_h5
             save_h5(filepath, self)
         else:
-            os.makedirs(os.path.dirname(os.path.abspath(filepath)), exist_ok=True)
             np.savez(filepath, **d)
 
     def load_weights(self, filepath):
