@@ -1,4 +1,4 @@
-"""ctypes binding of libiddgcn_hip.so (C-ABI declared in include/iddgcn.h).
+"""ctypes binding of libiddgcn_hip.so (C-ABI declared in include/iddgcn.h and include/iddgcn_graph.h).
 
 The product path has no CPU fallback: if the shared library is missing or was
 built for another ABI version, :func:`lib` raises immediately.
@@ -58,6 +58,13 @@ SIGNATURES = {
     "iddgcn_gather_rows_f32": (ci, [vp, cll, ci, vp, vp, vp]),
     "iddgcn_reduce_slabs_f32": (ci, [vp, ci, cll, vp, vp, ci, cf]),
     "iddgcn_adam_f32": (ci, [vp, cll, vp, vp, vp, vp, cf, cf, cf, cf, ci]),
+    # include/iddgcn_graph.h
+    "iddgcn_radix_sort_workspace": (cll, [cll, ci]),
+    "iddgcn_radix_sort_pairs": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, cll]),
+    "iddgcn_adjacency_workspace": (cll, [cll, ci, ci]),
+    "iddgcn_build_adjacency": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cll]),
+    "iddgcn_scored_edges_workspace": (cll, [cll, ci]),
+    "iddgcn_build_scored_edges": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cll]),
 }
 
 _lib = None
@@ -72,7 +79,7 @@ def exported_symbols():
 
 
 def load(path=LIB_PATH):
-    """Load the library and bind every symbol of include/iddgcn.h (no GPU call)."""
+    """Load the library and bind every symbol of include/*.h (no GPU call)."""
     if not os.path.exists(path):
         raise IddgcnError(
             f"libiddgcn_hip.so not found at {path}: build it with "

@@ -180,10 +180,13 @@ class Engine:
 
     # -- setup --------------------------------------------------------------
     def adjacency(self, adj_mats):
+        if isinstance(adj_mats, DeviceAdjacency):
+            return adj_mats
         return DeviceAdjacency(adj_mats, self.N, self.device)
 
     def edges(self, triples, labels=None):
-        return ScoredEdges(triples, labels, self.N, self.R, self.device)
+        """Scored-edge layout, built on the GPU (iddgcn_build_scored_edges)."""
+        return ScoredEdges.from_triples(triples, labels, self.N, self.R, self.device)
 
     def workspace(self, T, train):
         key = (T, train)

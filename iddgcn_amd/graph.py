@@ -13,6 +13,10 @@
   contiguous segments, and adds a head-sorted permutation for the head-side
   reductions.  All indices are validated here (int32, in range) so no kernel
   ever sees an out-of-range index.
+* ``DeviceAdjacency.from_triples`` / ``ScoredEdges.from_triples`` build the same
+  layouts on the GPU (include/iddgcn_graph.h: radix sorts, compaction, CSR
+  pointers), bit-identical to the host build above; ``get_adj_mats(...,
+  device=cuda)`` returns the device-built adjacency directly.
 """
 import numpy as np
 import torch
@@ -54,8 +58,12 @@ def _as_triples(data):
     return data.astype(np.int64)
 
 
-def get_adj_mats(data, num_entities, num_relations):
-    """utils1.get_adj_mats (utils1.py:420-451) without TensorFlow."""
+def get_adj_mats(data, num_entities, num_relations, device=None):
+    """utils1.get_adj_mats (utils1.py:420-451) without TensorFlow.  With a GPU ``device`` the
+    graph is built on the GPU and a DeviceAdjacency is returned (fit/predict take it in place of
+    the list of SparseAdj)."""
+    if device is not None and torch.device(device).type == "cuda":
+        return DeviceAdjacency.from_triples(data, num_entities, num_relations, device)
     data = _as_triples(data)
     if data.size and (data[:, [0, 2]].min() < 0 or data[:, [0, 2]].max() >= num_entities):
         raise IddgcnError("entity index out of range [0, num_entities)")
@@ -96,7 +104,7 @@ class DeviceAdjacency:
         off_f = 0
         any_val = False
         self.nnz = []
-        self.rows, self.cols = [], []          # host copies, per relation, in the caller's entry order
+        self._rows, self._cols = [], []        # host copies, per relation, in the caller's entry order
         for r, a in enumerate(adj_mats):
             rows = np.asarray(a.rows, dtype=np.int64)
             cols = np.asarray(a.cols, dtype=np.int64)
@@ -114,8 +122,8 @@ class DeviceAdjacency:
             bm.append(rows + r * N)
             bv.append(vals)
             self.nnz.append(int(rows.size))
-            self.rows.append(rows)
-            self.cols.append(cols)
+            self._rows.append(rows)
+            self._cols.append(cols)
         if off_f > INT32_MAX or N * len(adj_mats) > INT32_MAX:
             raise IddgcnError("adjacency too large for int32 offsets")
         # Backward: dE[c] += sum_r sum_{m: (m,c) in A_r} dAE[r][m].  One merged CSR of
@@ -140,6 +148,55 @@ class DeviceAdjacency:
         self.rel_offsets = np.concatenate([[0], np.cumsum(self.nnz)]).astype(np.int64)
         self.device = device
 
+    @classmethod
+    def from_triples(cls, data, num_entities, num_relations, device):
+        """get_adj_mats + __init__ on the GPU (iddgcn_build_adjacency): the entry order is the CSR
+        order, so fwd_src / fwd_pos are the identity.  One host synchronisation (the counts)."""
+        from . import ops
+        tr = _device_triples(data, device)
+        N, R = num_entities, num_relations
+        out, nnz, nph, err = ops.build_adjacency(tr, N, R)
+        if err:
+            raise IddgcnError("entity index out of range [0, num_entities)")
+        self = cls.__new__(cls)
+        self.num_entities, self.num_relations, self.device = N, R, device
+        self.fwd_ptr, self.bwd_ptr = out["fwd_ptr"], out["bwd_ptr"]
+        self.fwd_col, self.bwd_col = out["fwd_col"][:nnz], out["bwd_col"][:nnz]
+        self.fwd_val = out["fwd_val"][:nnz] if nph else None
+        self.bwd_val = out["bwd_val"][:nnz] if nph else None
+        self.total_nnz = nnz
+        ends = self.fwd_ptr.view(R, N + 1)[:, [0, N]].cpu().numpy().astype(np.int64)
+        self.nnz = [int(b - a) for a, b in ends]
+        self.rel_offsets = np.concatenate([[0], np.cumsum(self.nnz)]).astype(np.int64)
+        self.base_values = out["fwd_val"][:nnz]
+        self.fwd_src = torch.arange(nnz, dtype=torch.int64, device=tr.device)
+        self.fwd_pos = self.fwd_src
+        self.bwd_src = out["bwd_src"][:nnz].long()
+        self._rows = self._cols = None
+        return self
+
+    def _host_coo(self):
+        ptr = self.fwd_ptr.view(self.num_relations, self.num_entities + 1).cpu().numpy().astype(np.int64)
+        col = self.fwd_col.cpu().numpy().astype(np.int64)
+        self._rows, self._cols = [], []
+        for r in range(self.num_relations):
+            deg = np.diff(ptr[r])
+            self._rows.append(np.repeat(np.arange(self.num_entities, dtype=np.int64), deg))
+            self._cols.append(col[ptr[r, 0]:ptr[r, -1]])
+
+    @property
+    def rows(self):
+        """Per-relation row (obj) indices, host int64, entry order."""
+        if self._rows is None:
+            self._host_coo()
+        return self._rows
+
+    @property
+    def cols(self):
+        if self._cols is None:
+            self._host_coo()
+        return self._cols
+
     def set_values(self, values):
         """Replace the stored values (a (total_nnz,) GPU tensor in the caller's entry order, relation
         after relation) without rebuilding the CSR: ``adj * sigmoid(mask)`` of the explainers."""
@@ -153,6 +210,15 @@ class DeviceAdjacency:
         """Per-entry quantity in forward-CSR order -> list of per-relation tensors in entry order."""
         flat = csr_vals[self.fwd_pos]
         return [flat[self.rel_offsets[r]:self.rel_offsets[r + 1]] for r in range(self.num_relations)]
+
+
+def _device_triples(data, device):
+    if isinstance(data, torch.Tensor) and data.is_cuda:
+        t = data[0] if data.dim() == 3 and data.shape[0] == 1 else data
+        if t.dim() != 2 or t.shape[1] != 3:
+            raise IddgcnError(f"triples must be (B, 3), got {tuple(t.shape)}")
+        return t.to(device=device, dtype=torch.int64).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(_as_triples(data)), device=device)
 
 
 class ScoredEdges:
@@ -184,6 +250,31 @@ class ScoredEdges:
         self.tptr, self.hperm, self.hptr = g(tptr, np.int32), g(hperm, np.int32), g(hptr, np.int32)
         self.y = None if labels is None else g(np.asarray(labels, dtype=np.float32)[order], np.float32)
         self.inv = g(np.argsort(order, kind="stable"), np.int64)
+
+    @classmethod
+    def from_triples(cls, triples, labels, num_entities, num_relations, device):
+        """__init__ on the GPU (iddgcn_build_scored_edges): same arrays, bit-identical; ``order``
+        is a GPU int32 tensor here.  One host synchronisation (the error flag)."""
+        from . import ops
+        tr = _device_triples(triples, device)
+        if tr.shape[0] > INT32_MAX:
+            raise IddgcnError("too many scored edges for int32 indexing")
+        lab = None
+        if labels is not None:
+            lab = torch.as_tensor(np.asarray(labels, dtype=np.float32) if not isinstance(labels, torch.Tensor)
+                                  else labels, device=device).to(torch.float32).reshape(-1).contiguous()
+        o, err = ops.build_scored_edges(tr, lab, num_entities, num_relations)
+        if err & 1:
+            raise IddgcnError("scored entity index out of range [0, num_entities)")
+        if err & 2:
+            raise IddgcnError("scored relation index out of range [0, num_relations)")
+        self = cls.__new__(cls)
+        self.T = tr.shape[0]
+        self.h, self.r, self.t = o["h"], o["r"], o["t"]
+        self.tptr, self.hperm, self.hptr = o["tptr"], o["hperm"], o["hptr"]
+        self.y, self.inv = o["y"], o["inv"]
+        self.order = None
+        return self
 
     def unsort(self, x):
         """Sorted-order per-edge tensor -> caller's order."""

@@ -299,6 +299,8 @@ class IDDGCN_Model:
             self._params.load(self._named())
 
     def _adjacency(self, adj_mats):
+        if isinstance(adj_mats, DeviceAdjacency):       # get_adj_mats(..., device=cuda)
+            return adj_mats
         key = id(adj_mats)
         hit = self._graph_cache.get(key)
         if hit is not None and hit[0] is adj_mats:

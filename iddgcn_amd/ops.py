@@ -266,3 +266,83 @@ def adam(var, m, v, g, alpha, b1, b2, eps, sparse_form):
             raise L.IddgcnError(f"adam: {nm} size mismatch")
     L.check(L.lib().iddgcn_adam_f32(_stream(), n, _ptr(var), _ptr(m), _ptr(v), _ptr(g), float(alpha), float(b1),
                                     float(b2), float(eps), int(sparse_form)), "adam")
+
+
+# -- device graph build (include/iddgcn_graph.h) ------------------------------------------------
+_I64 = torch.int64
+_U8 = torch.uint8
+
+
+def _workspace(nbytes, device):
+    if nbytes < 0:
+        raise L.IddgcnError("graph build: sizes out of range")
+    return torch.empty(max(int(nbytes), 1), dtype=_U8, device=device)
+
+
+def radix_sort(keys, vals=None, *, end_bit=None, argsort=False):
+    """Stable LSD radix sort of int32/int64 keys (non-negative; bits [0, end_bit)).  Returns
+    (sorted keys, sorted vals) where vals is `vals` permuted, the stable argsort if argsort=True,
+    or None."""
+    if keys.dtype not in (_I32, _I64):
+        raise L.IddgcnError("radix_sort: keys must be int32 or int64")
+    _req(keys, keys.dtype, None, "keys")
+    _req(vals, _I32, (keys.shape[0],), "vals")
+    kb = keys.element_size()
+    n = keys.shape[0]
+    end_bit = 8 * kb if end_bit is None else int(end_bit)
+    ko = torch.empty_like(keys)
+    vo = torch.empty(n, dtype=_I32, device=keys.device) if (vals is not None or argsort) else None
+    ws = _workspace(L.lib().iddgcn_radix_sort_workspace(n, kb), keys.device)
+    L.check(L.lib().iddgcn_radix_sort_pairs(_stream(), n, kb, end_bit, _ptr(keys), _ptr(vals), _ptr(ko), _ptr(vo),
+                                            _ptr(ws), ws.numel()), "radix_sort")
+    return ko, vo
+
+
+def build_adjacency(triples, N, R):
+    """utils1.get_adj_mats + DeviceAdjacency's CSR layouts on the GPU.  triples: (M, 3) int64 GPU
+    tensor.  Returns a dict of GPU tensors (capacity M + R) and the host counts
+    (nnz, placeholders, error)."""
+    _req(triples, _I64, None, "triples")
+    if triples.dim() != 2 or triples.shape[1] != 3:
+        raise L.IddgcnError(f"triples must be (M, 3), got {tuple(triples.shape)}")
+    M = triples.shape[0]
+    dev = triples.device
+    need = L.lib().iddgcn_adjacency_workspace(M, N, R)
+    ws = _workspace(need, dev)
+    C = M + R
+    out = {"fwd_ptr": torch.empty(R * (N + 1), dtype=_I32, device=dev),
+           "fwd_col": torch.empty(C, dtype=_I32, device=dev), "fwd_val": torch.empty(C, dtype=_F32, device=dev),
+           "bwd_ptr": torch.empty(N + 1, dtype=_I32, device=dev),
+           "bwd_col": torch.empty(C, dtype=_I32, device=dev), "bwd_src": torch.empty(C, dtype=_I32, device=dev),
+           "bwd_val": torch.empty(C, dtype=_F32, device=dev)}
+    counts = torch.empty(3, dtype=_I32, device=dev)
+    o = out
+    L.check(L.lib().iddgcn_build_adjacency(_stream(), M, N, R, _ptr(triples), _ptr(o["fwd_ptr"]), _ptr(o["fwd_col"]),
+                                           _ptr(o["fwd_val"]), _ptr(o["bwd_ptr"]), _ptr(o["bwd_col"]),
+                                           _ptr(o["bwd_src"]), _ptr(o["bwd_val"]), _ptr(counts), _ptr(ws),
+                                           ws.numel()), "build_adjacency")
+    nnz, nph, err = (int(x) for x in counts.cpu())     # the one host synchronisation of the build
+    return out, nnz, nph, err
+
+
+def build_scored_edges(triples, labels, N, R):
+    """graph.ScoredEdges on the GPU: tail-sorted (stable) h/r/t, gathered labels, tptr, hperm, hptr,
+    inv.  Returns (dict of GPU tensors, error flag)."""
+    _req(triples, _I64, None, "triples")
+    if triples.dim() != 2 or triples.shape[1] != 3:
+        raise L.IddgcnError(f"triples must be (T, 3), got {tuple(triples.shape)}")
+    T = triples.shape[0]
+    dev = triples.device
+    _req(labels, _F32, (T,), "labels")
+    ws = _workspace(L.lib().iddgcn_scored_edges_workspace(T, N), dev)
+    o = {k: torch.empty(T, dtype=_I32, device=dev) for k in ("h", "r", "t", "hperm")}
+    o["y"] = torch.empty(T, dtype=_F32, device=dev) if labels is not None else None
+    o["tptr"] = torch.empty(N + 1, dtype=_I32, device=dev)
+    o["hptr"] = torch.empty(N + 1, dtype=_I32, device=dev)
+    o["inv"] = torch.empty(T, dtype=_I64, device=dev)
+    err = torch.empty(1, dtype=_I32, device=dev)
+    L.check(L.lib().iddgcn_build_scored_edges(_stream(), T, N, R, _ptr(triples), _ptr(labels), _ptr(o["h"]),
+                                              _ptr(o["r"]), _ptr(o["t"]), _ptr(o["y"]), _ptr(o["tptr"]),
+                                              _ptr(o["hperm"]), _ptr(o["hptr"]), _ptr(o["inv"]), _ptr(err), _ptr(ws),
+                                              ws.numel()), "build_scored_edges")
+    return o, int(err.item())

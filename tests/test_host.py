@@ -14,8 +14,8 @@ from tests.conftest import ROOT
 
 
 def header_symbols():
-    src = open(os.path.join(ROOT, "include", "iddgcn.h")).read()
-    return sorted(set(re.findall(r"^\s*int\s+(iddgcn_\w+)\s*\(", src, flags=re.M)))
+    src = "".join(open(os.path.join(ROOT, "include", f)).read() for f in ("iddgcn.h", "iddgcn_graph.h"))
+    return sorted(set(re.findall(r"^\s*(?:int|long long)\s+(iddgcn_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_library_exports_every_header_symbol():
@@ -163,3 +163,20 @@ def test_load_npz_weights(golden, tmp_path):
     m2.load_weights(p)
     for a, b in zip(m.get_weights(), m2.get_weights()):
         assert np.array_equal(a, b)
+
+
+def test_graph_build_workspace_queries_are_pure_host():
+    lib = _lib.lib()
+    assert lib.iddgcn_radix_sort_workspace(1000, 4) > 1000 * 8
+    assert lib.iddgcn_radix_sort_workspace(1000, 8) > lib.iddgcn_radix_sort_workspace(1000, 4)
+    assert lib.iddgcn_radix_sort_workspace(1000, 3) < 0
+    assert lib.iddgcn_radix_sort_workspace(1 << 31, 4) < 0
+    assert lib.iddgcn_adjacency_workspace(37510, 845, 4) > 0
+    assert lib.iddgcn_adjacency_workspace(10, 0, 4) < 0
+    assert lib.iddgcn_adjacency_workspace(10, 1 << 30, 2) < 0          # R*N >= 2^31
+    assert lib.iddgcn_scored_edges_workspace(40316, 845) > 0
+    assert lib.iddgcn_scored_edges_workspace(-1, 845) < 0
+    # invalid arguments are rejected before any launch (no GPU needed)
+    assert lib.iddgcn_radix_sort_pairs(None, 10, 4, 40, None, None, None, None, None, 0) == -3
+    assert lib.iddgcn_build_adjacency(None, 10, 0, 4, None, None, None, None, None, None, None, None, None,
+                                      None, 0) == -3
