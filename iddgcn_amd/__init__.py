@@ -13,3 +13,4 @@ from .model import (Adam, BinaryCrossentropy, DistMult, IDDGCN_Layer, IDDGCN_Mod
                     SaveWeightsCallback, get_IDDGCN_Model)
 from .utils import generate_reverse_triplets, get_y_true  # noqa: F401
 from . import explain  # noqa: F401,E402  (explaiNE / GNNExplainer / IDDGCN explainer on the HIP path)
+from . import similarity  # noqa: F401,E402  (feat_similarity.py similarity graph on MFMA)

@@ -65,6 +65,10 @@ SIGNATURES = {
     "iddgcn_build_adjacency": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cll]),
     "iddgcn_scored_edges_workspace": (cll, [cll, ci]),
     "iddgcn_build_scored_edges": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cll]),
+    # include/iddgcn_similarity.h
+    "iddgcn_similarity_workspace": (cll, [ci, ci]),
+    "iddgcn_similarity_pairs": (ci, [vp, ci, ci, vp, ctypes.c_double, vp, cll, vp, cll, vp, vp, cll]),
+    "iddgcn_similarity_triples": (ci, [vp, cll, ci, ci, cll, vp, vp]),
 }
 
 _lib = None

@@ -346,3 +346,38 @@ def build_scored_edges(triples, labels, N, R):
                                               _ptr(o["hperm"]), _ptr(o["hptr"]), _ptr(o["inv"]), _ptr(err), _ptr(ws),
                                               ws.numel()), "build_scored_edges")
     return o, int(err.item())
+
+
+# -- similarity graph (include/iddgcn_similarity.h) ---------------------------------------------
+def similarity_pairs(X, threshold, capacity=None, band_capacity=None):
+    """Keys i*N + j (unordered, int64 GPU tensor) of every i < j with cosine(X_i, X_j) > threshold.
+    X: (N, F) float64 GPU tensor.  Reruns once with exact buffer sizes if a capacity was short."""
+    _req(X, torch.float64, None, "X")
+    if X.dim() != 2:
+        raise L.IddgcnError("X must be (N, F)")
+    N, F = X.shape
+    dev = X.device
+    ws = _workspace(L.lib().iddgcn_similarity_workspace(N, F), dev)
+    cap = int(capacity) if capacity is not None else max(1 << 16, 64 * N)
+    bcap = int(band_capacity) if band_capacity is not None else max(1 << 14, 4 * N)
+    counts = torch.empty(2, dtype=_I64, device=dev)
+    for _ in range(2):
+        keys = torch.empty(max(cap, 1), dtype=_I64, device=dev)
+        band = torch.empty(max(bcap, 1), dtype=_I64, device=dev)
+        L.check(L.lib().iddgcn_similarity_pairs(_stream(), N, F, _ptr(X), float(threshold), _ptr(keys), cap,
+                                                _ptr(band), bcap, _ptr(counts), _ptr(ws), ws.numel()),
+                "similarity_pairs")
+        n_acc, n_band = (int(v) for v in counts.cpu())
+        if n_acc <= cap and n_band <= bcap:
+            return keys[:n_acc]
+        cap, bcap = max(cap, n_acc), max(bcap, n_band)
+    raise L.IddgcnError("similarity_pairs: capacity retry failed")
+
+
+def similarity_triples(sorted_keys, N, relation, start):
+    _req(sorted_keys, _I64, None, "sorted_keys")
+    n = sorted_keys.shape[0]
+    out = torch.empty((n, 3), dtype=_I64, device=sorted_keys.device)
+    L.check(L.lib().iddgcn_similarity_triples(_stream(), n, N, int(relation), int(start), _ptr(sorted_keys),
+                                              _ptr(out)), "similarity_triples")
+    return out

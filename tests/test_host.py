@@ -14,7 +14,7 @@ from tests.conftest import ROOT
 
 
 def header_symbols():
-    src = "".join(open(os.path.join(ROOT, "include", f)).read() for f in ("iddgcn.h", "iddgcn_graph.h"))
+    src = "".join(open(os.path.join(ROOT, "include", f)).read() for f in ("iddgcn.h", "iddgcn_graph.h", "iddgcn_similarity.h"))
     return sorted(set(re.findall(r"^\s*(?:int|long long)\s+(iddgcn_\w+)\s*\(", src, flags=re.M)))
 
 

@@ -85,3 +85,18 @@ def test_synth_fixture_grads_torch_consistency(golden):
     assert abs(loss - float(s["loss"])) < 1e-12
     for k, v in grads.items():
         np.testing.assert_allclose(v, s[f"grad_{k}"], rtol=1e-10, atol=1e-15)
+
+
+def test_similarity_oracle_reproduces_reference_outputs(golden):
+    """oracle/ref_similarity.py against the reference's own mu_similar0.97.csv / drug_similar0.78.csv
+    (as committed in tests/golden/similarity.npz; re-read from /root/reference when present)."""
+    import pandas as pd
+
+    from oracle.ref_similarity import similar_triples
+    g = golden("similarity.npz")
+    assert np.array_equal(similar_triples(g["mu_feat"], 0.97, 3, 0), g["mu_triples"])
+    assert np.array_equal(similar_triples(g["drug_feat"], 0.78, 2, 661), g["drug_triples"])
+    ref = "/root/reference/datasets/prediction_datasets"
+    if os.path.isdir(ref):
+        assert np.array_equal(pd.read_csv(f"{ref}/mu_similar0.97.csv", header=None).to_numpy(), g["mu_triples"])
+        assert np.array_equal(pd.read_csv(f"{ref}/drug_similar0.78.csv", header=None).to_numpy(), g["drug_triples"])
