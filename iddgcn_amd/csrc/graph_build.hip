@@ -36,11 +36,11 @@ __device__ __forceinline__ unsigned mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-// lanes of this wave that are valid and hold the same digit as this lane (0 for invalid lanes)
-__device__ __forceinline__ uint64_t peers_of(unsigned d, bool valid) {
+// lanes of this wave that are valid and hold the same digit as this lane (0 for invalid lanes);
+// digits have `nb` (<= RB) bits
+__device__ __forceinline__ uint64_t peers_of(unsigned d, bool valid, int nb) {
     uint64_t m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < RB; ++b) {
+    for (int b = 0; b < nb; ++b) {
         const bool bit = (d >> b) & 1u;
         const uint64_t bb = __ballot(bit);
         m &= bit ? bb : ~bb;
@@ -58,6 +58,17 @@ __device__ __forceinline__ unsigned wave_incl_scan(unsigned x) {
     return x;
 }
 
+// XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8), so give XCD x
+// one contiguous range of tiles.  Consecutive tiles of one XCD then write adjacent hist entries and
+// adjacent digit runs, and the partial lines at run boundaries merge in that XCD's L2 instead of
+// being written from two XCDs.
+__device__ __forceinline__ int tile_index(int ntiles) {
+    const int b = blockIdx.x, x = b & 7;
+    int start = 0;
+    for (int y = 0; y < x; ++y) start += (ntiles - y + 7) >> 3;
+    return start + (b >> 3);
+}
+
 template <typename K>
 __device__ __forceinline__ unsigned digit_of(K k, int shift, unsigned mask) {
     return (unsigned)(k >> shift) & mask;
@@ -70,7 +81,8 @@ __global__ __launch_bounds__(NT) void radix_hist_kernel(const K* __restrict__ ke
     __shared__ unsigned wcnt[NW][RADIX];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     for (int i = tid; i < NW * RADIX; i += NT) (&wcnt[0][0])[i] = 0;
-    const long long base = (long long)blockIdx.x * TILE + wave * WAVE_KEYS + lane;
+    const int tile = tile_index(ntiles);
+    const long long base = (long long)tile * TILE + wave * WAVE_KEYS + lane;
     K k[IPT];
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
@@ -78,20 +90,16 @@ __global__ __launch_bounds__(NT) void radix_hist_kernel(const K* __restrict__ ke
         k[j] = i < n ? keys[i] : (K)0;
     }
     __syncthreads();
+    // wave-private bins, LDS integer atomics (no return value): the counts do not depend on the order
 #pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-        const bool v = base + j * 64 < n;
-        const unsigned d = digit_of(k[j], shift, mask);
-        const uint64_t p = peers_of(d, v);
-        // the highest lane of each peer group adds the group's size; wave-private bins, no atomics
-        if (v && mbcnt(p) + 1 == (unsigned)__popcll(p)) wcnt[wave][d] += (unsigned)__popcll(p);
-    }
+    for (int j = 0; j < IPT; ++j)
+        if (base + j * 64 < n) atomicAdd(&wcnt[wave][digit_of(k[j], shift, mask)], 1u);
     __syncthreads();
     if (tid < RADIX) {
         unsigned s = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) s += wcnt[w][tid];
-        hist[(size_t)tid * ntiles + blockIdx.x] = s;
+        hist[(size_t)tid * ntiles + tile] = s;
     }
 }
 
@@ -126,7 +134,7 @@ __global__ __launch_bounds__(1024) void scan_rows_kernel(unsigned* __restrict__ 
 template <typename K, int VMODE>
 __global__ __launch_bounds__(NT) void radix_scatter_kernel(const K* __restrict__ kin, const unsigned* __restrict__ vin,
                                                            K* __restrict__ kout, unsigned* __restrict__ vout,
-                                                           long long n, int shift, unsigned mask,
+                                                           long long n, int shift, unsigned mask, int nbits,
                                                            const unsigned* __restrict__ hist,
                                                            const unsigned* __restrict__ dtotal, int ntiles) {
     __shared__ K skey[TILE];
@@ -136,7 +144,8 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(const K* __restrict__
     __shared__ unsigned gbase[RADIX];
     __shared__ unsigned part[2][RADIX / 64];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const long long tile0 = (long long)blockIdx.x * TILE;
+    const int tile = tile_index(ntiles);
+    const long long tile0 = (long long)tile * TILE;
     const long long base = tile0 + wave * WAVE_KEYS + lane;
     for (int i = tid; i < NW * RADIX; i += NT) (&wcnt[0][0])[i] = 0;
     K k[IPT];
@@ -154,7 +163,7 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(const K* __restrict__
     for (int j = 0; j < IPT; ++j) {
         const bool ok = base + j * 64 < n;
         const unsigned d = digit_of(k[j], shift, mask);
-        const uint64_t p = peers_of(d, ok);
+        const uint64_t p = peers_of(d, ok, nbits);
         const unsigned below = mbcnt(p);
         unsigned before = 0;
         if (ok) before = wcnt[wave][d];
@@ -192,7 +201,7 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(const K* __restrict__
         const unsigned ds = pa + a - tc;                 // this tile's first slot of digit tid
         const unsigned db = pb + b - dt;                 // global first slot of digit tid
         dstart[tid] = ds;
-        gbase[tid] = db + hist[(size_t)tid * ntiles + blockIdx.x] - ds;   // mod 2^32; n < 2^31
+        gbase[tid] = db + hist[(size_t)tid * ntiles + tile] - ds;   // mod 2^32; n < 2^31
     }
     __syncthreads();
 #pragma unroll
@@ -399,7 +408,10 @@ int radix_sort(hipStream_t st, long long n, int end_bit, const K* kin, const uns
     unsigned* valt = (unsigned*)(ws + al((size_t)n * sizeof(K)));
     unsigned* hist = (unsigned*)((char*)valt + al((size_t)n * 4));
     unsigned* dtot = (unsigned*)((char*)hist + al((size_t)nt * RADIX * 4));
+    // as few passes as 8-bit digits need, with the digits as narrow as that allows: fewer buckets
+    // mean longer digit runs per tile (fuller written lines) and fewer ballots per key
     const int passes = (end_bit + RB - 1) / RB;
+    const int dbits = passes ? (end_bit + passes - 1) / passes : 0;
     if (passes == 0) {
         GB_CHECK(hipMemcpyAsync(kout, kin, (size_t)n * sizeof(K), hipMemcpyDeviceToDevice, st));
         if (vout) {
@@ -411,8 +423,8 @@ int radix_sort(hipStream_t st, long long n, int end_bit, const K* kin, const uns
     const K* ksrc = kin;
     const unsigned* vsrc = vin;
     for (int p = 0; p < passes; ++p) {
-        const int shift = p * RB;
-        const int nb = end_bit - shift < RB ? end_bit - shift : RB;
+        const int shift = p * dbits;
+        const int nb = end_bit - shift < dbits ? end_bit - shift : dbits;
         const unsigned mask = (1u << nb) - 1u;
         const bool last_dst = ((passes - 1 - p) & 1) == 0;
         K* kdst = last_dst ? kout : kalt;
@@ -422,13 +434,13 @@ int radix_sort(hipStream_t st, long long n, int end_bit, const K* kin, const uns
         hipLaunchKernelGGL(scan_rows_kernel, dim3(RADIX), dim3(1024), 0, st, hist, (int)nt, dtot);
         if (!vout)
             hipLaunchKernelGGL((radix_scatter_kernel<K, 0>), dim3((unsigned)nt), dim3(NT), 0, st, ksrc, vsrc, kdst,
-                               vdst, n, shift, mask, hist, dtot, (int)nt);
+                               vdst, n, shift, mask, nb, hist, dtot, (int)nt);
         else if (p == 0 && !vin)
             hipLaunchKernelGGL((radix_scatter_kernel<K, 2>), dim3((unsigned)nt), dim3(NT), 0, st, ksrc, vsrc, kdst,
-                               vdst, n, shift, mask, hist, dtot, (int)nt);
+                               vdst, n, shift, mask, nb, hist, dtot, (int)nt);
         else
             hipLaunchKernelGGL((radix_scatter_kernel<K, 1>), dim3((unsigned)nt), dim3(NT), 0, st, ksrc, vsrc, kdst,
-                               vdst, n, shift, mask, hist, dtot, (int)nt);
+                               vdst, n, shift, mask, nb, hist, dtot, (int)nt);
         ksrc = kdst;
         vsrc = vdst;
     }
