@@ -53,11 +53,13 @@ def kernel_roofline(name, N, R, D, T, gemm, avg_ms):
 
     flops: 2*D^2*T algorithmic (x3 f16 MFMA instructions on the f16 peak in split mode);
     bytes (algorithmic, fp32): fwd reads x^{l-1}, writes x^l, reads W[h_e] (R per edge), t_e and the
-    distinct P_r rows (R*N*D once); bwd reads do and the sigma' operand x, writes do'; dS reads x and
-    do.  bound = whichever roofline time is larger."""
+    distinct P_r rows (R*N*D once); bwd reads do and the sigma' operand x, writes do' (the layer-2 bwd,
+    "rec", rebuilds x^1 from the distinct ES1 / P^1 rows and W^1[h_e] instead of reading it); dS reads
+    x and do.  bound = whichever roofline time is larger."""
     flops = 2.0 * D * D * T
     nbytes = {"tail_fwd_gemm": 8.0 * D * T + 4.0 * R * T + 4.0 * T + 4.0 * R * N * D,
               "tail_bwd_gemm": 12.0 * D * T,
+              "tail_bwd_rec_gemm": 8.0 * D * T + 4.0 * R * T + 4.0 * T + 4.0 * (R + 1) * N * D,
               "tail_dS_tn": 8.0 * D * T}[name]
     hw_flops, peak_f = (3 * flops, MFMA_F16_PEAK_TFLOPS) if gemm == "split" else (flops, MFMA_F32_PEAK_TFLOPS)
     t_mfma = hw_flops / (peak_f * 1e12)
@@ -180,6 +182,8 @@ def main():
     ap.add_argument("--gemm", default="split", choices=["split", "exact"],
                     help="operand precision of the D=256 MFMA GEMMs (the other mode is timed too)")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")
+    ap.add_argument("--recompute-x1", action="store_true",
+                    help="layer-2 backward rebuilds x^1 on chip instead of re-reading it (A/B)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -201,7 +205,7 @@ def main():
     tri = np.concatenate([pos, neg])[lo:hi]
     lab = np.concatenate([np.ones(len(pos), np.float32), np.zeros(len(neg), np.float32)])[lo:hi]
 
-    eng = Engine(N, R, D, dev, gemm=args.gemm)
+    eng = Engine(N, R, D, dev, gemm=args.gemm, recompute_x1=args.recompute_x1)
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
     init = reference_init(N, R, D, 89)
     adj = eng.adjacency(adj_mats)

@@ -8,9 +8,12 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
-ABI_VERSION = 1
+# a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
+if os.environ.get("IDDGCN_LIB"):
+    LIB_PATH = os.environ["IDDGCN_LIB"]
+ABI_VERSION = 2
 
-ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
+ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID, ACT_DSIGMOID_COMBINE = 0, 1, 2, 3
 GEMM_EXACT_F32, GEMM_SPLIT_F16 = 0, 1
 
 vp = ctypes.c_void_p
@@ -31,6 +34,7 @@ class RowGemmArgs(ctypes.Structure):
         ("V", vp), ("v_idx", vp),
         ("v_rel_stride", cll), ("v_row_stride", cll),
         ("act", ci), ("aux", vp),
+        ("v_runs_max", ci),
     ]
 
 

@@ -281,6 +281,7 @@ struct RowGemmP {
     const float* V; const int* v_idx;
     long long v_rel_stride, v_row_stride;
     int act; const float* aux;
+    int v_runs_max;
     int tiles_per_block;
 };
 
@@ -352,7 +353,15 @@ __global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmP p) {
                 const long long ci = p.coef_idx ? (long long)p.coef_idx[e] : e;
                 const long long vi = p.v_idx ? (long long)p.v_idx[e] : e;
                 const float* vb = p.V + vi * p.v_row_stride + c;
-                for (int r = 0; r < p.R; ++r) v = fmaf(p.coef[ci * p.R + r], vb[r * p.v_rel_stride], v);
+                if (p.act == IDDGCN_ACT_DSIGMOID_COMBINE) {
+                    // x = sigmoid(V_0 + sum_r coef_r V_{r+1}): the same arithmetic as combine_kernel
+                    float xs = vb[0];
+                    for (int r = 0; r < p.R; ++r) xs = fmaf(p.coef[ci * p.R + r], vb[(r + 1) * p.v_rel_stride], xs);
+                    const float x = sigmoid_fast(xs);
+                    v = v * (x * (1.0f - x));
+                } else {
+                    for (int r = 0; r < p.R; ++r) v = fmaf(p.coef[ci * p.R + r], vb[r * p.v_rel_stride], v);
+                }
             }
             if (p.act == IDDGCN_ACT_SIGMOID) {
                 v = sigmoid_fast(v);
@@ -647,18 +656,29 @@ __device__ __forceinline__ float wave_max(float v) {             // max over the
     return v;
 }
 
-template <int NV, bool AUX, bool HAS_COEF, bool X3>
+// REC (IDDGCN_ACT_DSIGMOID_COMBINE): the sigma' operand is not read from memory but recomputed,
+// x = sigmoid(V_0[v] + sum_r coef_r V_{r+1}[v]) from the tile's distinct V rows (NV = R + 1), so
+// the tail activation x^1 of layer 1 never has to be re-read by the backward.  The caller
+// guarantees at most REC_CAP runs of equal v_idx per 32-row tile (tail-sorted edges: 1-4).
+constexpr int REC_CAP = 8;
+template <int NV, bool AUX, bool HAS_COEF, bool X3, bool REC = false>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     using namespace r3;
+    static_assert(!REC || (NV >= 2 && !AUX && HAS_COEF), "REC: V_0 + coefficient-weighted V_1.., no aux");
     constexpr int NS = NV + (AUX ? 1 : 0);
-    // A-tile pipeline depth: three buffers (A(t+2) in flight while A(t) feeds the MFMAs) when the
-    // wave slabs leave room for them (NS <= 1), two otherwise
-    constexpr int NBUF = NS >= 2 ? 2 : 3;
-    constexpr int PD = NBUF - 1;                       // prefetch distance in tiles
     constexpr int NSL = NS > 1 ? NS : 1;               // slabs per wave (slab 0 also stages C)
-    constexpr int WF = NSL * SLAB + COEF + IDX + CMP + CINV;
+    // Slab 0 holds 32 rows (it also stages the C tile); REC slabs r >= 1 hold REC_CAP rows.
+    constexpr int CAPV = REC ? REC_CAP : 32;
+    constexpr int SLABC = CAPV * 32;
+    constexpr int SLABS = SLAB + (NSL - 1) * SLABC;    // floats of all slabs of one wave
+    constexpr int WF = SLABS + COEF + IDX + CMP + CINV;
+    // A-tile pipeline depth: three buffers (A(t+2) in flight while A(t) feeds the MFMAs) when the
+    // LDS budget allows, two otherwise
+    constexpr int NBUF = (3 * A_FLOATS + NW * WF + 3 * TR) * 4 <= 160 * 1024 ? 3 : 2;
+    constexpr int PD = NBUF - 1;                       // prefetch distance in tiles
     constexpr int LDSF = NBUF * A_FLOATS + NW * WF + NBUF * TR;
     static_assert(LDSF * 4 <= 160 * 1024, "LDS budget");
+    auto soff = [](int r) { return r == 0 ? 0 : SLAB + (r - 1) * SLABC; };   // slab r of a wave
     __shared__ __attribute__((aligned(16))) float lds[LDSF];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -666,8 +686,8 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     const int i = lane & 31, h = lane >> 5;
     const int c0 = wave * 32;
     float* bufA = lds;
-    float* slabw = lds + NBUF * A_FLOATS + wave * WF;          // [NSL][32][32]
-    float* coefw = slabw + NSL * SLAB;                         // [32][R]
+    float* slabw = lds + NBUF * A_FLOATS + wave * WF;          // slab 0 [32][32], slabs r >= 1 [CAPV][32]
+    float* coefw = slabw + SLABS;                              // [32][R]
     float* cinvw = slabw + WF - CINV;                          // [32] (X3)
     float* rowinv = lds + NBUF * A_FLOATS + NW * WF;           // [NBUF][TR] (X3)
     const int R = p.R;
@@ -808,8 +828,11 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
                 const long long v = cmpw[row < u ? row : u - 1];
 #pragma unroll
                 for (int r = 0; r < NV; ++r) {
+                    if constexpr (REC) {
+                        if (r > 0 && kb >= CAPV) continue;   // (precondition broken: stay in bounds)
+                    }
                     const float* gp = p.V + r * p.v_rel_stride + v * D + c0 + g * 4;
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + r * SLAB + kb * 32), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + soff(r) + kb * 32), 16, 0, 0);
                 }
             }
         }
@@ -820,7 +843,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
                 const int g = (lane & 7) ^ ((row >> 1) & 7);
                 const long long e = clampe(t * TR + row);
                 const float* gp = p.aux + e * D + c0 + g * 4;
-                __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + NV * SLAB + k * 256), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + soff(NV) + k * 256), 16, 0, 0);
             }
         }
         if (HAS_COEF) {
@@ -851,7 +874,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
         const __amdgpu_buffer_rsrc_t rc = out_rsrc(t);
         float cf[NS_MAX] = {0.f, 0.f};
         if (HAS_COEF) {
-            if (NV == 2 || (NV == 0 && R == 2)) {
+            if (REC ? R == 2 : (NV == 2 || (NV == 0 && R == 2))) {
                 const float2 c2 = *reinterpret_cast<const float2*>(coefw + i * 2);
                 cf[0] = c2.x;
                 cf[1] = c2.y;
@@ -866,7 +889,21 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             f32x4 v = {acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
             if (p.accumulate)
                 v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (i * D + col) * 4, 0, 0));
-            if (NV > 0 && !(V3_ABL & 2)) {
+            if constexpr (REC) {        // v *= x(1-x), x = sigmoid(V_0 + sum_r cf_r V_{r+1})
+                const int offv = vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
+                f32x4 xs = ld4(slabw + offv);
+#pragma unroll
+                for (int r = 1; r < NV; ++r) {
+                    const f32x4 s = ld4(slabw + soff(r) + offv);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) xs[q] = fmaf(cf[r - 1], s[q], xs[q]);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float x = sigmoid_fast(xs[q]);
+                    v[q] = v[q] * (x * (1.0f - x));
+                }
+            } else if (NV > 0 && !(V3_ABL & 2)) {
                 const int offv = vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
 #pragma unroll
                 for (int r = 0; r < NV; ++r) {
@@ -885,7 +922,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
             } else if (p.act == IDDGCN_ACT_DSIGMOID) {
-                const f32x4 x = ld4(slabw + NV * SLAB + off);
+                const f32x4 x = ld4(slabw + soff(NV) + off);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = v[q] * (x[q] * (1.0f - x[q]));
             }
@@ -2199,12 +2236,15 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     if (a->M < 0 || !a->A || !a->B || !a->C) return IDDGCN_E_BAD_ARG;
     if (a->R > 0 && (!a->coef || !a->V)) return IDDGCN_E_BAD_ARG;
     if (a->act == IDDGCN_ACT_DSIGMOID && !a->aux) return IDDGCN_E_BAD_ARG;
+    if (a->act == IDDGCN_ACT_DSIGMOID_COMBINE && (a->R < 1 || a->R + 1 > MAX_R || a->v_row_stride == 0))
+        return IDDGCN_E_BAD_ARG;
+    if (a->act < IDDGCN_ACT_NONE || a->act > IDDGCN_ACT_DSIGMOID_COMBINE) return IDDGCN_E_BAD_ARG;
     if (a->M == 0) return 0;
     RowGemmP p;
     p.M = a->M; p.A = a->A; p.a_idx = a->a_idx; p.B = a->B; p.b_trans = a->b_trans;
     p.C = a->C; p.accumulate = a->accumulate; p.R = a->R; p.coef = a->coef; p.coef_idx = a->coef_idx;
     p.V = a->V; p.v_idx = a->v_idx; p.v_rel_stride = a->v_rel_stride; p.v_row_stride = a->v_row_stride;
-    p.act = a->act; p.aux = a->aux;
+    p.act = a->act; p.aux = a->aux; p.v_runs_max = a->v_runs_max;
     hipStream_t st = (hipStream_t)stream;
 #define RGEMM(DD, MAXB)                                                                         \
     {                                                                                           \
@@ -2216,6 +2256,33 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     }
     const bool gatherV = p.R > 0 && p.v_row_stride != 0;
     const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
+    if (p.act == IDDGCN_ACT_DSIGMOID_COMBINE) {
+        // fast path: D = 256, R <= 2, dense V rows, the caller's bound on V runs per 32-row tile
+        if (a->D == 256 && p.R <= 2 && p.v_row_stride == 256 && p.v_runs_max >= 1 && p.v_runs_max <= REC_CAP &&
+            (g_rowgemm_path == 0 || g_gemm_split)) {
+            const long long nt = ((long long)p.M + r3::TR - 1) / r3::TR;
+            long long nb = nt < 256 ? nt : 256;
+            p.tiles_per_block = (int)((nt + nb - 1) / nb);
+            nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
+            const dim3 g((unsigned)nb), blk(512);
+#define V3R(NV)                                                                                           \
+            {                                                                                             \
+                if (g_gemm_split) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, false, true, true, true>), g, blk, 0, st, p); \
+                else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, false, true, false, true>), g, blk, 0, st, p);           \
+            }
+            if (p.R == 1) V3R(2)
+            else V3R(3)
+#undef V3R
+            return launch_status();
+        }
+        switch (a->D) {      // any v_idx order: the register-staged kernel
+            case 32: RGEMM(32, 2048); break;
+            case 64: RGEMM(64, 2048); break;
+            case 128: RGEMM(128, 1024); break;
+            default: RGEMM(256, 256); break;
+        }
+        return launch_status();
+    }
     // v3 (staggered, wave-private slabs): D=256, R <= 2
     const bool v3_ok = a->D == 256 && p.R <= 2 && !(gatherV && dsig) && (!gatherV || p.v_row_stride == 256) &&
                        g_rowgemm_path == 0;

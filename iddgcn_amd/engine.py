@@ -99,8 +99,12 @@ class Workspace:
         f = dict(dtype=torch.float32, device=device)
         e = lambda *s: torch.empty(*s, **f)  # noqa: E731
         self.AE = e(R, N, D)
-        self.P = e(NUM_LAYERS, R, N, D)
-        self.ES1 = e(N, D)
+        # [ES1 | P^1_0 .. P^1_{R-1} | P^2 .. | P^3 ..]: ES1 sits right before layer 1's P_r so that
+        # EP1 = (ES1, P^1_0, ...) is one (R+1)-table operand (x^1 recompute in the backward)
+        EP = e(1 + NUM_LAYERS * R, N, D)
+        self.ES1 = EP[0]
+        self.P = EP[1:].view(NUM_LAYERS, R, N, D)
+        self.EP1 = EP[:1 + R]
         self.X = e(NUM_LAYERS, N, D)            # head chain X^1..X^3
         self.Ssm = e(NUM_LAYERS, N, R)
         self.W = e(NUM_LAYERS, N, R)
@@ -142,7 +146,7 @@ class Engine:
     and all non-GEMM kernels are exact f32 in both modes.
     """
 
-    def __init__(self, num_entities, num_relations, dim, device=None, gemm="split"):
+    def __init__(self, num_entities, num_relations, dim, device=None, gemm="split", recompute_x1=False):
         if dim not in (32, 64, 128, 256):
             raise L.IddgcnError("embedding dim must be one of 32, 64, 128, 256")
         if not 1 <= num_relations <= 8:
@@ -151,6 +155,9 @@ class Engine:
             raise L.IddgcnError(f"gemm must be one of {sorted(GEMM_MODES)}")
         self.N, self.R, self.D = num_entities, num_relations, dim
         self.gemm = gemm
+        # layer-2 backward: rebuild sigma'(x^1) from node tables instead of re-reading x^1 (4.1 GB
+        # less HBM traffic per step at config 3, but ~6% slower per launch: off by default)
+        self.recompute_x1 = recompute_x1
         self.device = torch.device("cuda") if device is None else torch.device(device)
         if self.device.type != "cuda":
             raise L.IddgcnError("IDDGCN engine runs on the GPU only (no CPU fallback)")
@@ -252,8 +259,14 @@ class Engine:
                 # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x)
                 with self._mark("tail_dS_tn"):
                     ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab)
-                with self._mark("tail_bwd_gemm"):
-                    ops.rowgemm(do, Sl, do_next, b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1])
+                rec = l == 1 and self._recompute_ok(ed)
+                with self._mark("tail_bwd_rec_gemm" if rec else "tail_bwd_gemm"):
+                    if rec:
+                        # x^1 = sigmoid(ES1[t] + sum_r W^1[h,r] P^1_r[t]) rebuilt on chip (forward, above)
+                        ops.rowgemm(do, Sl, do_next, b_trans=True, act=L.ACT_DSIGMOID_COMBINE, coef=ws.Wedge[0],
+                                    V=ws.EP1, v_idx=ed.t, v_rel_stride=N * D, v_runs_max=ed.tail_runs32)
+                    else:
+                        ops.rowgemm(do, Sl, do_next, b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1])
             # head side (node level)
             ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
                               dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)
@@ -282,6 +295,11 @@ class Engine:
         # DistMult rel grad and the loss
         ops.reduce_slabs(ws.drel_slab, ws.nb_dm, G["rel"])
         ops.reduce_slabs(ws.loss_slab, ws.nb_dm, ws.loss)
+
+    def _recompute_ok(self, ed):
+        """The x^1-recompute GEMM runs when it takes the D=256 on-chip path (<= 8 tail runs per
+        32-edge block); other shapes re-read x^1 (the generic kernel would be slower)."""
+        return self.recompute_x1 and self.D == 256 and 1 <= ed.tail_runs32 <= 8
 
     # -- public steps ---------------------------------------------------------
     def train_step(self, params, grads, opt, adj, ed, t_global=None, allreduce=None):

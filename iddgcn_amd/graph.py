@@ -276,6 +276,26 @@ class ScoredEdges:
         self.order = None
         return self
 
+    _runs32 = None
+
+    @property
+    def tail_runs32(self):
+        """Most runs of equal tail in any aligned 32-edge block (0 for no edges).  The D=256 row
+        GEMM that recomputes the layer-1 tail activation keeps at most 8 distinct tail rows of a
+        block on chip (include/iddgcn.h, IDDGCN_ACT_DSIGMOID_COMBINE)."""
+        if self._runs32 is None:
+            T = self.T
+            if T == 0:
+                self._runs32 = 0
+            else:
+                t = self.t
+                start = torch.zeros((T + 31) // 32 * 32, dtype=torch.int32, device=t.device)
+                start[:T] = 1
+                start[1:T] = (t[1:] != t[:-1]).int()
+                start[0:T:32] = 1
+                self._runs32 = int(start.view(-1, 32).sum(1).max().item())
+        return self._runs32
+
     def unsort(self, x):
         """Sorted-order per-edge tensor -> caller's order."""
         return x[self.inv]

@@ -65,7 +65,10 @@ def sddmm_csr(row_ptr, col, G, X, out, n_seg, n_rows):
 
 
 def rowgemm(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, coef_idx=None, V=None,
-            v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None):
+            v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None, v_runs_max=0):
+    """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32).  act=ACT_DSIGMOID_COMBINE
+    multiplies by x(1-x) with x = sigmoid(V_0[v_idx] + sum_r coef_r V_{r+1}[v_idx]) (V: R+1 tables);
+    v_runs_max bounds the runs of equal v_idx per aligned 32-row block (0 = unknown)."""
     D = B.shape[0]
     M = C.shape[0] if M is None else M
     R = 0 if coef is None else coef.shape[-1]
@@ -84,11 +87,15 @@ def rowgemm(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, 
         _idx_ok(v_idx, M, None, "v_idx")
     if act == L.ACT_DSIGMOID:
         _req(aux, _F32, (M, D), "aux")
+    if act == L.ACT_DSIGMOID_COMBINE:
+        if not R or V is None or V.numel() < (R + 1) * int(v_rel_stride):
+            raise L.IddgcnError("ACT_DSIGMOID_COMBINE needs coef (R columns) and R+1 V tables")
     args = L.RowGemmArgs(
         M=M, D=D, A=_ptr(A), a_idx=_ptr(a_idx), B=_ptr(B), b_trans=int(b_trans), C=_ptr(C),
         accumulate=int(accumulate), R=R, coef=_ptr(coef), coef_idx=_ptr(coef_idx), V=_ptr(V),
         v_idx=_ptr(v_idx), v_rel_stride=int(v_rel_stride),
-        v_row_stride=int(D if v_row_stride is None else v_row_stride), act=int(act), aux=_ptr(aux))
+        v_row_stride=int(D if v_row_stride is None else v_row_stride), act=int(act), aux=_ptr(aux),
+        v_runs_max=int(v_runs_max))
     L.check(L.lib().iddgcn_rowgemm_f32(_stream(), ctypes.byref(args)), "rowgemm")
 
 

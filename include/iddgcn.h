@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 1
+#define IDDGCN_ABI_VERSION 2
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -35,6 +35,12 @@ extern "C" {
 #define IDDGCN_ACT_NONE     0
 #define IDDGCN_ACT_SIGMOID  1
 #define IDDGCN_ACT_DSIGMOID 2     /* v *= aux * (1 - aux)   (sigmoid backward) */
+/* v *= x * (1 - x) with x = sigmoid(V_0[v_idx] + sum_{r<R} coef[r] * V_{r+1}[v_idx]) recomputed
+ * from node tables (the layer-1 tail activation, IDDGCN.py:62-79, without re-reading it):
+ * V holds R + 1 tables of v_rel_stride floats, aux is unused.  v_runs_max > 0 asserts that no
+ * aligned 32-row block of v_idx holds more runs of equal values than that; the D = 256 kernel
+ * needs <= 8 (tail-sorted edges), any other input takes the generic kernel. */
+#define IDDGCN_ACT_DSIGMOID_COMBINE 3
 
 int iddgcn_abi_version(void);
 
@@ -75,6 +81,7 @@ typedef struct {
     const float* V; const int* v_idx;
     long long v_rel_stride, v_row_stride;
     int act; const float* aux;
+    int v_runs_max;       /* ABI 2: bound on runs of equal v_idx per 32-row block, 0 = unknown */
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 

@@ -395,8 +395,24 @@ def test_adam_kernel_matches_keras_forms(cuda):
         close(var2, vd - alpha * mr / (vr.sqrt() + eps), 1e-6)
 
 
-@pytest.mark.parametrize("mode", ["plain", "combine", "combine_r1", "dsig", "rank_bcast", "rank_bcast_nodsig",
-                                  "accumulate", "gatherA", "small_M"])
+def _run_structured_idx(M, N, gen):
+    """Row indices whose 32-row tiles hold 1, 2, 8, 15, 16, 17, 24 and 32 runs of equal values
+    (the D=256 row GEMM keeps at most 16 distinct V rows of a tile in LDS for its second relation
+    and reads the rest of such a tile from global memory)."""
+    idx = torch.empty(M, dtype=torch.int64)
+    run = 0
+    for t0 in range(0, M, 32):
+        rows = min(32, M - t0)
+        u = min([1, 2, 8, 15, 16, 17, 24, 32][(t0 // 32) % 8], rows)
+        cuts = sorted(torch.randperm(rows - 1, generator=gen)[:u - 1].add(1).tolist())
+        for k, (a, b) in enumerate(zip([0] + cuts, cuts + [rows])):
+            idx[t0 + a:t0 + b] = (run + k) % N
+        run += u
+    return idx
+
+
+@pytest.mark.parametrize("mode", ["plain", "combine", "combine_r1", "combine_runs", "dsig", "rank_bcast",
+                                  "rank_bcast_nodsig", "accumulate", "gatherA", "small_M"])
 def test_rowgemm_dma_path_bitwise_equals_register_path(mode, cuda):
     """D=256 LDS-DMA pipelined kernel == register-staged kernel, bit for bit (same MFMA chain,
     same epilogue order), including a ragged last tile and multi-tile persistent blocks."""
@@ -408,6 +424,10 @@ def test_rowgemm_dma_path_bitwise_equals_register_path(mode, cuda):
     if mode in ("combine", "combine_r1"):
         kw = dict(coef=torch.rand(N, R, generator=g).to(cuda), coef_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
                   V=torch.randn(R, N, D, generator=g).to(cuda), v_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
+                  v_rel_stride=N * D, act=L.ACT_SIGMOID)
+    elif mode == "combine_runs":
+        kw = dict(coef=torch.rand(N, R, generator=g).to(cuda), coef_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
+                  V=torch.randn(R, N, D, generator=g).to(cuda), v_idx=_run_structured_idx(M, N, g).int().to(cuda),
                   v_rel_stride=N * D, act=L.ACT_SIGMOID)
     elif mode == "dsig":
         kw = dict(b_trans=True, act=L.ACT_DSIGMOID, aux=torch.rand(M, D, generator=g).to(cuda))
@@ -450,8 +470,64 @@ def _maxrel(got, ref):
     return ((got.double() - ref).abs().max() / ref.abs().max()).item()
 
 
-@pytest.mark.parametrize("mode", ["plain", "trans", "combine", "combine_r1", "dsig", "rank_bcast", "accumulate",
-                                  "gatherA", "small_M", "row_decades", "zero_rows"])
+def _runs32(t):
+    """Most runs of equal values in any aligned 32-row block (graph.ScoredEdges.tail_runs32)."""
+    s = torch.ones(len(t), dtype=torch.int64)
+    s[1:] = (t[1:] != t[:-1]).long()
+    s[::32] = 1
+    s = torch.cat([s, s.new_zeros(-len(t) % 32)])
+    return int(s.view(-1, 32).sum(1).max())
+
+
+@pytest.mark.parametrize("D", DIMS)
+@pytest.mark.parametrize("R", [1, 2])
+def test_rowgemm_dsigmoid_combine(D, R, cuda):
+    """(dO·S^T) * x(1-x) with x = sigmoid(V_0[t] + sum_r W[e,r] V_{r+1}[t]) rebuilt from node tables
+    (IDDGCN_ACT_DSIGMOID_COMBINE, the layer-2 tail backward without re-reading x^1): the generic
+    kernel (any t) and, at D=256 with <= 8 runs per 32 rows, the on-chip kernel, in both GEMM modes,
+    against fp64 (split <= 2x the exact error, floor 1e-6); the on-chip kernel bitwise equal to the
+    generic one in exact mode; equal to ACT_DSIGMOID on the materialised x."""
+    g = torch.Generator().manual_seed(101 + D + R)
+    M, N = 4099, 300
+    dO = torch.randn(M, D, generator=g, dtype=torch.float64) * 1e-3
+    S = torch.randn(D, D, generator=g, dtype=torch.float64) / D ** 0.5
+    W = torch.rand(M, R, generator=g, dtype=torch.float64)
+    V = torch.randn(R + 1, N, D, generator=g, dtype=torch.float64)
+    t = torch.randint(0, N, (M,), generator=g).sort().values
+    runs = _runs32(t)
+    assert 1 <= runs <= 8
+    xs = V[0][t] + sum(W[:, r:r + 1] * V[r + 1][t] for r in range(R))
+    x = torch.sigmoid(xs)
+    ref = ((dO @ S.t()) * x * (1 - x)).to(cuda)
+    dOf, Sf, Wf, Vf, ti = (a.float().contiguous().to(cuda) for a in (dO, S, W, V, t))
+    ti = ti.int()
+
+    def run(v_runs_max, act=L.ACT_DSIGMOID_COMBINE, aux=None):
+        C = torch.full((M, D), 3.0, device=cuda)
+        if act == L.ACT_DSIGMOID_COMBINE:
+            ops.rowgemm(dOf, Sf, C, b_trans=True, act=act, coef=Wf, V=Vf, v_idx=ti, v_rel_stride=N * D,
+                        v_runs_max=v_runs_max)
+        else:
+            ops.rowgemm(dOf, Sf, C, b_trans=True, act=act, aux=aux)
+        return C
+
+    errs = {}
+    for gm in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16):
+        with _gemm_mode(gm):
+            generic, fast = run(0), run(runs)
+            errs[gm] = _maxrel(fast, ref)
+            assert _maxrel(generic, ref) <= 2e-5
+            if gm == L.GEMM_EXACT_F32:
+                assert torch.equal(fast, generic)
+                xm = torch.empty(M, D, device=cuda)             # the materialised x^1 (combine_kernel)
+                ops.combine(Vf[0], Wf, Vf[1:].contiguous(), xm, y_idx=ti, v_idx=ti, v_rel_stride=N * D)
+                assert _maxrel(run(0, L.ACT_DSIGMOID, xm), ref) <= 2e-5
+    assert errs[L.GEMM_EXACT_F32] <= 2e-5
+    assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
+
+
+@pytest.mark.parametrize("mode", ["plain", "trans", "combine", "combine_r1", "combine_runs", "dsig", "rank_bcast",
+                                  "accumulate", "gatherA", "small_M", "row_decades", "zero_rows"])
 def test_rowgemm_split_f16_vs_fp64(mode, cuda):
     """Split-fp16 operand mode (D=256): error vs an fp64 torch reference no larger than twice the
     exact-f32 MFMA path's (floor 1e-6 of max|ref|), on every epilogue form, ragged tiles, rows whose
@@ -469,11 +545,13 @@ def test_rowgemm_split_f16_vs_fp64(mode, cuda):
     A, S = A.to(cuda), S.to(cuda)
     kw, C0 = {}, None
     Af, Sf = A.float(), S.float()
-    if mode in ("combine", "combine_r1"):
+    if mode in ("combine", "combine_r1", "combine_runs"):
         W = torch.rand(N, R, generator=g, dtype=torch.float64).to(cuda)
         P = (torch.randn(R, N, D, generator=g, dtype=torch.float64) * 4).to(cuda)
         h = torch.randint(0, N, (M,), generator=g).to(cuda)
         t = torch.randint(0, N, (M,), generator=g).sort().values.to(cuda)
+        if mode == "combine_runs":
+            t = _run_structured_idx(M, N, g).to(cuda)
         kw = dict(coef=W.float(), coef_idx=h.int(), V=P.float(), v_idx=t.int(), v_rel_stride=N * D,
                   act=L.ACT_SIGMOID)
         ref = torch.sigmoid(A @ S + sum(W[h, r:r + 1] * P[r][t] for r in range(R)))
