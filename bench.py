@@ -182,6 +182,8 @@ def main():
     ap.add_argument("--gemm", default="split", choices=["split", "exact"],
                     help="operand precision of the D=256 MFMA GEMMs (the other mode is timed too)")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")
+    ap.add_argument("--fuse-tail-seg", action="store_true",
+                    help="layers 2-3: tail segmented reduction fused into the dS pass (A/B)")
     ap.add_argument("--recompute-x1", action="store_true",
                     help="layer-2 backward rebuilds x^1 on chip instead of re-reading it (A/B)")
     args = ap.parse_args()
@@ -205,7 +207,8 @@ def main():
     tri = np.concatenate([pos, neg])[lo:hi]
     lab = np.concatenate([np.ones(len(pos), np.float32), np.zeros(len(neg), np.float32)])[lo:hi]
 
-    eng = Engine(N, R, D, dev, gemm=args.gemm, recompute_x1=args.recompute_x1)
+    eng = Engine(N, R, D, dev, gemm=args.gemm, recompute_x1=args.recompute_x1,
+                 fuse_tail_seg=args.fuse_tail_seg)
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
     init = reference_init(N, R, D, 89)
     adj = eng.adjacency(adj_mats)

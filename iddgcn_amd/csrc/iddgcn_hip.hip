@@ -82,11 +82,11 @@ __device__ __forceinline__ float group_sum(float v) {
 // Reduce K values (K a power of two, K <= LPR) over an aligned group of LPR lanes with a
 // butterfly that halves the value set at each level: K-1 + log2(LPR/K) ... shuffles instead of
 // K*log2(LPR).  On return v[0] holds, in every lane, the full sum of value index
-// sub / (LPR/K).  LPR == 64 uses the permlane/DPP exchanges above.
+// sub / (LPR/K).  LPR == 64 and 32 use the permlane/DPP exchanges above (no LDS crossbar).
 template <int LPR, int K>
 __device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
     static_assert((K & (K - 1)) == 0 && K <= LPR, "K must be a power of two <= LPR");
-    if constexpr (LPR == 64) {
+    if constexpr (LPR == 64 || LPR == 32) {
         // levels 32 and 16: one register swap exchanges the kept/sent halves of a value pair
         int kc = K;
         auto swap_level = [&](auto swapper) {
@@ -107,7 +107,7 @@ __device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
                 v[0] = a + b;
             }
         };
-        swap_level([](float& a, float& b) { pl_swap32(a, b); });
+        if constexpr (LPR == 64) swap_level([](float& a, float& b) { pl_swap32(a, b); });
         swap_level([](float& a, float& b) { pl_swap16(a, b); });
         auto dpp_level = [&](auto mtag) {
             constexpr int m = decltype(mtag)::value;
@@ -1304,13 +1304,43 @@ __device__ __forceinline__ void split16_same(float xs, _Float16& hi, _Float16& l
     lo = (_Float16)(xs - (float)hi);
 }
 
+// SEG: the tail-side segmented reduction of the same layer (tail_seg_reduce_kernel) fused into the
+// dS = x^T do pass, so do is read from HBM once instead of twice:
+//   dP_r[t] = sum_{e: t_e = t} W[e][r] do_e      (row order, fmaf chain: = tail_seg_reduce)
+//   dWedge[e][r] = <do_e, P_r[t_e]>
+// Block row ranges (row_beg) start at tail-segment starts, so every segment is summed by one block
+// and written once (no partials, no atomics; the caller zeroes dP for tails without edges).  Per
+// tile, the distinct tails' P rows (<= TNSEG_CAP, the caller's bound) are DMA'd into LDS with the
+// tile; while the fp32 do rows are still in LDS (before the in-place fp16 conversion) lane (i, h)
+// walks column 32w+i of the tile's rows for relation h: the segment sum in a register and the dot
+// partials reduced over the wave's 32 columns, then over the 8 waves (block order) by wave 0.
+struct TnSegP {
+    const int* row_beg;       // [n_blocks + 1]
+    const int* tail;          // [M] tail of each row (sorted)
+    const float* W;           // [M][R]
+    const float* P;           // [R][.][D]
+    long long p_rel_stride;
+    float* dP;                // [R][.][D], same stride as P
+    float* dWedge;            // [M][R]
+    int R;                    // 1 or 2
+};
+constexpr int TNSEG_CAP = 6;
+
+template <bool SEG>
 __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long long rows_per_block,
                                                             const float* __restrict__ A,
                                                             const float* __restrict__ B,
-                                                            float* __restrict__ slab) {
+                                                            float* __restrict__ slab, TnSegP sp) {
     using namespace tn3;
-    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * TILE + 2 * 8];   // [buf][A|B][TK][LDR], sB[buf][8]
+    // SEG region per buffer: tails[32] | run-start mask (+pad)[32] | W[32][2] | P rows [CAP][2][D];
+    // then part[8][32][2]
+    constexpr int SEG_BUF = 32 + 32 + 64 + TNSEG_CAP * 2 * D;
+    constexpr int SEG_F = SEG ? 2 * SEG_BUF + 8 * 32 * 2 : 0;
+    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * TILE + 2 * 8 + SEG_F];   // [buf][A|B][TK][LDR], sB[buf][8]
+    static_assert((2 * 2 * TILE + 2 * 8 + SEG_F) * 4 <= 160 * 1024, "LDS budget");
     float* sBpub = lds + 2 * 2 * TILE;
+    float* segL = lds + 2 * 2 * TILE + 2 * 8;
+    float* partL = segL + 2 * SEG_BUF;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int i = lane & 31, h = lane >> 5;
@@ -1325,10 +1355,112 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
 #pragma unroll
     for (int cj = 0; cj < 8; ++cj) curB[cj] = S_INIT;
 
-    const long long r_beg = (long long)blockIdx.x * rows_per_block;
-    long long r_end = r_beg + rows_per_block;
-    if (r_end > M) r_end = M;
+    long long r_beg, r_end;
+    if constexpr (SEG) {
+        r_beg = sp.row_beg[blockIdx.x];
+        r_end = sp.row_beg[blockIdx.x + 1];
+    } else {
+        r_beg = (long long)blockIdx.x * rows_per_block;
+        r_end = r_beg + rows_per_block;
+        if (r_end > M) r_end = M;
+    }
     const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
+
+    // ---- SEG state and helpers ----
+    const int R = SEG ? sp.R : 0;
+    const bool sact = SEG && h < R;                  // lane (i, h) reduces relation h of column c
+    const int c = 32 * wave + i;
+    int cur_t = -1;                                  // tail of the open segment (uniform)
+    float sacc = 0.f;
+    float* const dPc = SEG ? sp.dP + (sact ? h : 0) * sp.p_rel_stride + c : nullptr;   // dP[h][.][c]
+    auto load_tails = [&](long long t) -> int {      // lane < 32: tail of row `lane` of tile t, or -1
+        const long long e = r_beg + t * TK + lane;
+        return (SEG && lane < 32 && t < nt && e < r_end) ? sp.tail[e] : -1;
+    };
+    auto seg_stage = [&](int tk, long long t, int b) {
+        float* base = segL + b * SEG_BUF;
+        int* tl = reinterpret_cast<int*>(base);
+        float* Wl = base + 64;
+        float* Pl = base + 128;
+        const int tprev = __shfl_up(tk, 1, 64);
+        const bool start = lane < 32 && tk >= 0 && (lane == 0 || tk != tprev);
+        const unsigned long long m = __ballot(start);
+        int u = __popcll(m);
+        if (u > TNSEG_CAP) u = TNSEG_CAP;            // (caller's bound broken: stay in bounds)
+        if (wave == 0 && lane < 32) tl[lane] = tk;
+        if (wave == 0 && lane == 32) tl[32] = (int)(unsigned)m;     // run starts of the tile (bit = row)
+        for (int q = wave; q < u * R; q += 8) {      // P rows of the distinct tails, one 1 KiB DMA each
+            const int sidx = q / R, rr = q - sidx * R;
+            unsigned long long mm = m;
+            for (int z = 0; z < sidx; ++z) mm &= mm - 1;
+            const int ts = __builtin_amdgcn_readlane(tk, __builtin_ctzll(mm));
+            dma_row_1k(sp.P + rr * sp.p_rel_stride + (long long)ts * D, Pl + (sidx * 2 + rr) * D, lane);
+        }
+        if (wave == 1) {                             // the tile's W rows (32 x R floats, contiguous)
+            const long long row0 = r_beg + t * TK;
+            const long long nw = (r_end - row0 < TK ? r_end - row0 : TK) * R;
+            const float* g = lane < nw ? sp.W + row0 * R + lane : sp.W;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)Wl, 4, 0, 0);
+        }
+    };
+    // walk the fp32 do rows of tile t (before convert) for column c, relation h: 8 rows at a time,
+    // their do / W values read up front (independent LDS reads), runs from the tile's start mask
+    // (scalar branches), the P value of the run's tail re-read from LDS at each run start only
+    auto seg_scan = [&](long long t, int b) {
+        const float* base = segL + b * SEG_BUF;
+        const int* tl = reinterpret_cast<const int*>(base);
+        const float* Wl = base + 64;
+        const float* Pl = base + 128;
+        const float* Bf = lds + (b * 2 + 1) * TILE;
+        const long long row0 = r_beg + t * TK;
+        const int nrows = (int)(r_end - row0 < TK ? r_end - row0 : TK);
+        const unsigned mstart = (unsigned)__builtin_amdgcn_readfirstlane(tl[32]);
+        const int hh = sact ? h : 0;
+        int slot = 0;
+        float pcur = 0.f;
+#pragma unroll 1
+        for (int q0 = 0; q0 < TK; q0 += 8) {
+            float d[8], w[8], pv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                d[j] = Bf[(q0 + j) * LDR + c];
+                w[j] = Wl[(q0 + j) * R + hh];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int row = q0 + j;
+                pv[j] = 0.f;
+                if (row < nrows) {
+                    if ((mstart >> row) & 1u) {
+                        const int tr = __builtin_amdgcn_readfirstlane(tl[row]);
+                        if (tr != cur_t) {
+                            if (sact && cur_t >= 0) dPc[cur_t * D] = sacc;
+                            cur_t = tr;
+                            sacc = 0.f;
+                        }
+                        pcur = Pl[(slot * 2 + hh) * D + c];
+                        ++slot;
+                    }
+                    sacc = fmaf(w[j], d[j], sacc);
+                    pv[j] = d[j] * pcur;
+                }
+            }
+            const float tot = multi_reduce<32, 8>(pv, i);
+            if ((i & 3) == 0) partL[(wave * 32 + q0 + (i >> 2)) * 2 + h] = tot;
+        }
+    };
+    // dWedge of tile t = sum of the 8 waves' partials, in wave order; wave w writes rows 4w..4w+3
+    auto seg_dwedge = [&](long long t) {
+        const long long row0 = r_beg + t * TK;
+        const int nrows = (int)(r_end - row0 < TK ? r_end - row0 : TK);
+        const int row = 4 * wave + (lane >> 1), rr = lane & 1;
+        if (lane < 8 && row < nrows && rr < R) {
+            float sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) sum += partL[(w * 32 + row) * 2 + rr];
+            sp.dWedge[(row0 + row) * R + rr] = sum;
+        }
+    };
 
     auto stage = [&](long long t, int b) {
         float* As = lds + (b * 2 + 0) * TILE;
@@ -1385,16 +1517,29 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
         if (lane == 0) sBpub[b * 8 + wave] = sBrun;
     };
 
+    int tnext = -1;
     if (nt > 0) {
         stage(0, 0);
+        if constexpr (SEG) {
+            seg_stage(load_tails(0), 0, 0);
+            tnext = load_tails(1);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if constexpr (SEG) seg_scan(0, 0);
         convert(0);
         __syncthreads();
     }
     int b = 0;
     for (long long t = 0; t < nt; ++t, b ^= 1) {
-        if (t + 1 < nt) stage(t + 1, b ^ 1);
+        if constexpr (SEG) seg_dwedge(t);
+        if (t + 1 < nt) {
+            stage(t + 1, b ^ 1);
+            if constexpr (SEG) {
+                seg_stage(tnext, t + 1, b ^ 1);
+                tnext = load_tails(t + 2);
+            }
+        }
         // B-side scales of this tile: rescale the accumulators whose block scale dropped
 #pragma unroll
         for (int cj = 0; cj < 8; ++cj) {
@@ -1422,10 +1567,12 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t + 1 < nt) {
+            if constexpr (SEG) seg_scan(t + 1, b ^ 1);
             convert(b ^ 1);
             __syncthreads();
         }
     }
+    if (sact && cur_t >= 0) dPc[cur_t * D] = sacc;                 // last segment
     float* out = slab + (long long)blockIdx.x * D * D;
     const float ia = pow2_inv(sA);
 #pragma unroll
@@ -2345,7 +2492,8 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
     if (d == 256 && g_gemm_split) {
-        hipLaunchKernelGGL(gemm_tn256_x3_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
+        hipLaunchKernelGGL(gemm_tn256_x3_kernel<false>, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab,
+                           TnSegP{});
     } else if (d == 256 && g_rowgemm_path != 1) {
         hipLaunchKernelGGL(gemm_tn256_dma_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
     } else switch (d) {
@@ -2355,6 +2503,26 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
         default: TNK(256); break;
     }
 #undef TNK
+    int rc = launch_status();
+    if (rc) return rc;
+    const long long n = (long long)d * d;
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_blocks, n, slab, C,
+                       accumulate, 1.0f);
+    return launch_status();
+}
+
+int iddgcn_gemm_tn_seg_f32(void* stream, long long M, int d, const float* A, const float* B, float* slab,
+                           int n_blocks, float* C, int accumulate, const int* row_beg, const int* tail, int R,
+                           const float* W, const float* P, long long p_rel_stride, float* dP, float* dWedge,
+                           int max_tile_runs) {
+    if (d != 256 || !g_gemm_split) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > 2) return IDDGCN_E_BAD_REL;
+    if (M < 0 || n_blocks < 1 || !A || !B || !slab || !C || !row_beg || !tail || !W || !P || !dP || !dWedge ||
+        max_tile_runs < 1 || max_tile_runs > TNSEG_CAP)
+        return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const TnSegP sp{row_beg, tail, W, P, p_rel_stride, dP, dWedge, R};
+    hipLaunchKernelGGL(gemm_tn256_x3_kernel<true>, dim3(n_blocks), dim3(512), 0, st, M, 0LL, A, B, slab, sp);
     int rc = launch_status();
     if (rc) return rc;
     const long long n = (long long)d * d;

@@ -146,7 +146,8 @@ class Engine:
     and all non-GEMM kernels are exact f32 in both modes.
     """
 
-    def __init__(self, num_entities, num_relations, dim, device=None, gemm="split", recompute_x1=False):
+    def __init__(self, num_entities, num_relations, dim, device=None, gemm="split", recompute_x1=False,
+                 fuse_tail_seg=False):
         if dim not in (32, 64, 128, 256):
             raise L.IddgcnError("embedding dim must be one of 32, 64, 128, 256")
         if not 1 <= num_relations <= 8:
@@ -158,6 +159,10 @@ class Engine:
         # layer-2 backward: rebuild sigma'(x^1) from node tables instead of re-reading x^1 (4.1 GB
         # less HBM traffic per step at config 3, but ~6% slower per launch: off by default)
         self.recompute_x1 = recompute_x1
+        # layers 2-3 backward: tail segmented reduction fused into the dS pass (do read once; 8.2 GB
+        # less HBM traffic per step at config 3, but the per-tile scan is serial with the TN pipeline:
+        # 3.9 ms vs 2.0 + 0.9 ms unfused, so off by default)
+        self.fuse_tail_seg = fuse_tail_seg
         self.device = torch.device("cuda") if device is None else torch.device(device)
         if self.device.type != "cuda":
             raise L.IddgcnError("IDDGCN engine runs on the GPU only (no CPU fallback)")
@@ -253,12 +258,20 @@ class Engine:
         do, do_next = ws.dE_a, ws.dE_b          # tail seed do^3, written by distmult_bce_heads
         for l in (2, 1, 0):                     # layer index l -> reference layer l+1
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
-            # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part
-            ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge, dsum=ws.dES if l == 0 else None)
+            # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part; for layers 2-3 the
+            # fused kernel does it inside the dS pass (do read once)
+            seg = self._tn_seg(ed) if l > 0 else None
+            if seg is None:
+                ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
+                                    dsum=ws.dES if l == 0 else None)
             if l > 0:
                 # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x)
                 with self._mark("tail_dS_tn"):
-                    ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab)
+                    if seg is not None:
+                        ops.gemm_tn_seg(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, seg[0], ed.t, ws.Wedge[l], Pl,
+                                        ws.dP, ws.dWedge, seg[1])
+                    else:
+                        ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab)
                 rec = l == 1 and self._recompute_ok(ed)
                 with self._mark("tail_bwd_rec_gemm" if rec else "tail_bwd_gemm"):
                     if rec:
@@ -295,6 +308,14 @@ class Engine:
         # DistMult rel grad and the loss
         ops.reduce_slabs(ws.drel_slab, ws.nb_dm, G["rel"])
         ops.reduce_slabs(ws.loss_slab, ws.nb_dm, ws.loss)
+
+    def _tn_seg(self, ed):
+        """(row_beg, max tile runs) when the fused dS + tail segmented reduction applies: D=256 in the
+        split-fp16 GEMM mode, R <= 2, at most ops.TN_SEG_CAP distinct tails per tile; else None."""
+        if not (self.fuse_tail_seg and self.D == 256 and self.gemm == "split" and self.R <= 2 and ed.T > 0):
+            return None
+        rb, runs = ed.tn_seg_layout(ops.tn_blocks(ed.T, self.D))
+        return (rb, runs) if 1 <= runs <= ops.TN_SEG_CAP else None
 
     def _recompute_ok(self, ed):
         """The x^1-recompute GEMM runs when it takes the D=256 on-chip path (<= 8 tail runs per

@@ -115,6 +115,36 @@ def gemm_tn(A, B, C, slab, accumulate=False):
                                        int(accumulate)), "gemm_tn")
 
 
+TN_SEG_CAP = 6   # distinct tails per 32-row tile the fused kernel stages on chip (include/iddgcn.h)
+
+
+def gemm_tn_seg(A, B, C, slab, row_beg, tail, W, P, dP, dWedge, max_tile_runs, accumulate=False):
+    """C = A^T B fused with the tail-side segmented reduction of B (iddgcn_gemm_tn_seg_f32):
+    dP[r][t] = sum_{tail[e]=t} W[e,r] B[e], dWedge[e,r] = <B[e], P[r][tail[e]]>.  row_beg: block row
+    ranges aligned to tail-segment starts (graph.ScoredEdges.tn_seg_layout); dP zeroed here."""
+    M, D = A.shape
+    R = W.shape[1]
+    _req(A, _F32, (M, D), "A")
+    _req(B, _F32, (M, D), "B")
+    _req(C, _F32, (D, D), "C")
+    _req(row_beg, _I32, None, "row_beg")
+    _req(tail, _I32, (M,), "tail")
+    _req(W, _F32, (M, R), "W")
+    _req(P, _F32, None, "P")
+    _req(dP, _F32, tuple(P.shape), "dP")
+    _req(dWedge, _F32, (M, R), "dWedge")
+    nb = row_beg.shape[0] - 1
+    if P.dim() != 3 or P.shape[0] != R or P.shape[2] != D:
+        raise L.IddgcnError("gemm_tn_seg: P must be (R, N, D)")
+    if slab.numel() < nb * D * D:
+        raise L.IddgcnError("gemm_tn_seg slab too small")
+    dP.zero_()
+    L.check(L.lib().iddgcn_gemm_tn_seg_f32(_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C),
+                                           int(accumulate), _ptr(row_beg), _ptr(tail), R, _ptr(W), _ptr(P),
+                                           P.shape[1] * D, _ptr(dP), _ptr(dWedge), int(max_tile_runs)),
+            "gemm_tn_seg")
+
+
 def tn_narrow_blocks(M):
     return int(L.lib().iddgcn_gemm_tn_narrow_blocks(int(M)))
 

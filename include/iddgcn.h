@@ -111,6 +111,18 @@ int iddgcn_gemm_tn_blocks(long long M, int d);
 int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const float* B,
                        float* slab, int n_blocks, float* C, int accumulate);
 
+/* dS = A^T B (as iddgcn_gemm_tn_f32, split-fp16 mode, D = 256) fused with the tail-side segmented
+ * reduction of the same layer (iddgcn_tail_seg_reduce_f32 without dsum), reading B (= do) once:
+ * dP[r][t] = sum_{e: tail[e] = t} W[e][r] B[e] and dWedge[e][r] = <B[e], P[r][tail[e]]>.
+ * Replaces the autodiff of IDDGCN.py:62-63 (x_t·S) and :71-77 (gather of A_r·E·K_r, sigma(alpha)
+ * scale) on the tail side.  row_beg[n_blocks + 1]: block row ranges that start at tail-segment
+ * starts; max_tile_runs: the caller's bound (<= 6) on distinct tails in any 32-row tile of those
+ * ranges; dP must be zeroed by the caller (tails without edges); R in {1, 2}. */
+int iddgcn_gemm_tn_seg_f32(void* stream, long long M, int d, const float* A, const float* B, float* slab,
+                           int n_blocks, float* C, int accumulate, const int* row_beg, const int* tail, int R,
+                           const float* W, const float* P, long long p_rel_stride, float* dP, float* dWedge,
+                           int max_tile_runs);
+
 /* out[D][R] (+)= A^T·dz and out_b[R] (+)= colsum(dz) over M rows (dW_alpha, db_alpha).
  * slab holds (n_blocks+1)*(D+1)*R floats; n_blocks from iddgcn_gemm_tn_narrow_blocks(). */
 int iddgcn_gemm_tn_narrow_blocks(long long M);

@@ -470,6 +470,60 @@ def _maxrel(got, ref):
     return ((got.double() - ref).abs().max() / ref.abs().max()).item()
 
 
+@pytest.mark.parametrize("R", [1, 2])
+@pytest.mark.parametrize("case", ["uniform", "hub", "ragged", "tiny"])
+def test_gemm_tn_seg_fused(R, case, cuda):
+    """dS = x^T do fused with the tail-side segmented reduction (iddgcn_gemm_tn_seg_f32, split mode,
+    D=256): dS within the split TN bar of fp64, dP bitwise equal to tail_seg_reduce_kernel (same
+    row-order fmaf chain; zero for tails without edges), dWedge within 1e-6 of fp64; block ranges
+    start at tail-segment starts, including a hub tail longer than a block (that block then
+    accumulates dS over far more rows: bar 4e-6) and empty blocks."""
+    from iddgcn_amd.graph import ScoredEdges
+    g = torch.Generator().manual_seed(7 + R + len(case))
+    D, N = 256, 500
+    M = {"uniform": 20_000, "hub": 20_000, "ragged": 20_011, "tiny": 40}[case]
+    t = torch.randint(0, 6 if case == "tiny" else N, (M,), generator=g)
+    if case == "hub":
+        t[: M // 3] = 17                       # one tail with a third of the edges
+    t[t == 3] = 4                              # a tail without edges
+    h = torch.randint(0, N, (M,), generator=g)
+    r = torch.randint(0, R, (M,), generator=g)
+    ed = ScoredEdges.from_triples(torch.stack([h, r, t], 1), None, N, R, cuda)
+    x = torch.rand(M, D, generator=g, dtype=torch.float64)
+    do = torch.randn(M, D, generator=g, dtype=torch.float64) * 1e-4
+    W = torch.rand(M, R, generator=g, dtype=torch.float64)
+    P = torch.randn(R, N, D, generator=g, dtype=torch.float64)
+    xf, dof, Wf, Pf = (a.float().to(cuda).contiguous() for a in (x, do, W, P))
+    nb = ops.tn_blocks(M, D)
+    rb, runs = ed.tn_seg_layout(nb)
+    assert 1 <= runs <= ops.TN_SEG_CAP
+    rbc = rb.cpu().long()
+    ts = ed.t.cpu().long()
+    assert rbc[0] == 0 and rbc[-1] == M and bool((rbc[1:] >= rbc[:-1]).all())
+    inner = rbc[(rbc > 0) & (rbc < M)]
+    assert bool((ts[inner] != ts[inner - 1]).all())          # every block starts a tail segment
+    slab = torch.empty(nb * D * D, device=cuda)
+    dS, dP, dWe = torch.empty(D, D, device=cuda), torch.full((R, N, D), 5.0, device=cuda), torch.empty(M, R, device=cuda)
+    dS2, dP2, dWe2 = torch.empty(D, D, device=cuda), torch.empty(R, N, D, device=cuda), torch.empty(M, R, device=cuda)
+    with _gemm_mode(L.GEMM_SPLIT_F16):
+        ops.gemm_tn_seg(xf, dof, dS, slab, rb, ed.t, Wf, Pf, dP, dWe, runs)
+        ops.tail_seg_reduce(ed.tptr, None, Wf, dof, Pf, dP2, dWe2)
+        ops.gemm_tn(xf, dof, dS2, slab)
+        again = torch.empty_like(dWe)
+        ops.gemm_tn_seg(xf, dof, torch.empty_like(dS), slab, rb, ed.t, Wf, Pf, torch.empty_like(dP), again, runs)
+    assert torch.equal(again, dWe)                             # deterministic
+    assert torch.equal(dP, dP2)
+    assert torch.equal(dP[:, 3], torch.zeros_like(dP[:, 3]))
+    ref_dS = x.t() @ do
+    # the hub tail puts a third of the rows into one block: one fp32 accumulation chain of ~6.7k rows
+    # (sqrt(6.7k) * 2^-24 ~ 5e-6) instead of ~80 rows per block
+    bar = 4e-6 if case == "hub" else max(2 * _maxrel(dS2, ref_dS.to(cuda)), 1e-6)
+    assert _maxrel(dS, ref_dS.to(cuda)) <= bar
+    tl = ed.t.cpu().long()
+    ref_dw = torch.stack([(do * P[rr][tl]).sum(1) for rr in range(R)], 1)
+    assert _maxrel(dWe, ref_dw.to(cuda)) <= 1e-6
+
+
 def _runs32(t):
     """Most runs of equal values in any aligned 32-row block (graph.ScoredEdges.tail_runs32)."""
     s = torch.ones(len(t), dtype=torch.int64)

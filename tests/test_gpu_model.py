@@ -24,8 +24,8 @@ pytestmark = pytest.mark.gpu
 N_ENT, N_REL = 845, 4
 
 
-def run_step(params, pos, neg, N, R, D, dev, adam=False, gemm="split", recompute_x1=False):
-    eng = Engine(N, R, D, dev, gemm=gemm, recompute_x1=recompute_x1)
+def run_step(params, pos, neg, N, R, D, dev, adam=False, gemm="split", recompute_x1=False, fuse_tail_seg=False):
+    eng = Engine(N, R, D, dev, gemm=gemm, recompute_x1=recompute_x1, fuse_tail_seg=fuse_tail_seg)
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
     P.load(params)
     adj = eng.adjacency(get_adj_mats(pos, N, R))
@@ -34,7 +34,7 @@ def run_step(params, pos, neg, N, R, D, dev, adam=False, gemm="split", recompute
     ed = eng.edges(tri, lab)
     loss_sum, p = eng.loss_and_grads(P, G, adj, ed)
     out = {"loss": loss_sum.item() / len(tri), "scores": p.cpu().numpy(), "grads": G.to_numpy(),
-           "recomputed": eng._recompute_ok(ed)}
+           "recomputed": eng._recompute_ok(ed), "fused": eng._tn_seg(ed) is not None}
     if adam:
         opt = KerasAdam(P)
         opt.apply(P, G)
@@ -158,6 +158,35 @@ def test_x1_recompute_step_vs_oracle(gemm, cuda):
     assert np.array_equal(rec["scores"], old["scores"])
     for k, g in old["grads"].items():
         assert np.abs(rec["grads"][k] - g).max() <= 1e-6 * np.abs(g).max() + 1e-30, k
+
+
+def test_fused_tail_seg_step_vs_oracle(cuda):
+    """D=256 split mode with the layer 2-3 tail segmented reduction fused into the dS pass: same
+    bars against the float64 oracle as the unfused path, and the two paths agree (loss and scores
+    bitwise, gradients to 1e-6 of max|g|)."""
+    N, R, D = 800, 2, 256
+    pos, neg = synthetic_graph(N, R, 16000, seed=12)
+    neg = neg[:8000]
+    rng = np.random.default_rng(5)
+    params = {"E": rng.standard_normal((N, D)) / np.sqrt(D)}
+    for l in (1, 2, 3):
+        params[f"K{l}"] = rng.standard_normal((R, D, D)) / D
+        params[f"S{l}"] = rng.standard_normal((D, D)) / np.sqrt(D)
+        params[f"relw{l}"] = rng.uniform(-.05, .05, R)
+        params[f"Wa{l}"] = rng.standard_normal((D, R)) / np.sqrt(D)
+        params[f"ba{l}"] = rng.standard_normal(R) * 0.1
+    params["rel"] = rng.standard_normal((R, D))
+    params = {k: v.astype(np.float32) for k, v in params.items()}
+    loss, scores, grads = train_step_grads(params, pos, neg, get_adj_coo(pos, N, R), N)
+    fused = run_step(params, pos, neg, N, R, D, cuda, fuse_tail_seg=True)
+    plain = run_step(params, pos, neg, N, R, D, cuda)
+    assert fused["fused"] and not plain["fused"]
+    assert abs(fused["loss"] - loss) <= 1e-5 * loss
+    np.testing.assert_allclose(fused["scores"], scores, rtol=0, atol=1e-5)
+    grad_check(fused["grads"], grads, 2e-4)
+    assert fused["loss"] == plain["loss"] and np.array_equal(fused["scores"], plain["scores"])
+    for k, g in plain["grads"].items():
+        assert np.abs(fused["grads"][k] - g).max() <= 1e-6 * np.abs(g).max() + 1e-30, k
 
 
 @pytest.mark.parametrize("gemm", ["split", "exact"])
