@@ -1390,7 +1390,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
         if (wave == 0 && lane < 32) tl[lane] = tk;
         if (wave == 0 && lane == 32) tl[32] = (int)(unsigned)m;     // run starts of the tile (bit = row)
         for (int q = wave; q < u * R; q += 8) {      // P rows of the distinct tails, one 1 KiB DMA each
-            const int sidx = q / R, rr = q - sidx * R;
+            const int sidx = R > 1 ? q / R : q, rr = q - sidx * R;
             unsigned long long mm = m;
             for (int z = 0; z < sidx; ++z) mm &= mm - 1;
             const int ts = __builtin_amdgcn_readlane(tk, __builtin_ctzll(mm));
