@@ -1982,26 +1982,27 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
     constexpr int U = 4;
     __shared__ __attribute__((aligned(16))) float red[GROUPS * RT * D];
     __shared__ float lred[GROUPS];
+    constexpr int SLOTS = 64 / LPR;      // edge slots per head node (one wave per node)
+    constexpr int NPB = 256 / 64;
     const int grp = threadIdx.x / LPR;
     const int sub = threadIdx.x % LPR;
+    const int slot = (threadIdx.x % 64) / LPR;
     f32x4 dr[RT];
 #pragma unroll
     for (int r = 0; r < RT; ++r) dr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
     float lacc = 0.f;
-    const long long nstride = (long long)gridDim.x * GROUPS;
-    for (long long n0 = (long long)blockIdx.x * GROUPS; n0 < n_nodes; n0 += nstride) {
-        const long long n = n0 + grp;
+    const long long nstride = (long long)gridDim.x * NPB;
+    for (long long n0 = (long long)blockIdx.x * NPB; n0 < n_nodes; n0 += nstride) {
+        const long long n = n0 + threadIdx.x / 64;
         const bool live = n < n_nodes;
         const int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
         const int len = end - beg;
-        int maxlen = len;       // groups of one wave may hold different nodes (D < 256)
-        if (LPR < 64) {
-#pragma unroll
-            for (int m = 32; m >= LPR; m >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, m, 64));
-        }
         const f32x4 a = live ? ld4(Xh + n * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < maxlen; k += U) {
+        // slot s takes edge groups k = (it*SLOTS + s)*U: same trip count for the whole wave
+        const int iters = (len + SLOTS * U - 1) / (SLOTS * U);
+        for (int it = 0; it < iters; ++it) {
+            const int k = (it * SLOTS + slot) * U;
             long long e[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) e[u] = (k + u < len) ? (long long)perm[beg + k + u] : -1;
@@ -2053,7 +2054,11 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 acc = fma4(b[u] * ds, rho[u], acc);     // same explicit fma as seg_gather_reduce
             }
         }
-        if (live) st4(dXh + n * D + sub * 4, acc * (a * (1.0f - a)));
+#pragma unroll
+        for (int m = 1; m < SLOTS; m <<= 1)          // slot partials, fixed order
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] += __shfl_xor(acc[q], LPR * m, 64);
+        if (live && slot == 0) st4(dXh + n * D + sub * 4, acc * (a * (1.0f - a)));
     }
 #pragma unroll
     for (int r = 0; r < RT; ++r) st4(red + (grp * RT + r) * D + sub * 4, dr[r]);
@@ -2121,6 +2126,10 @@ __global__ __launch_bounds__(256) void seg_gather_reduce_kernel(int n_nodes, con
 // walked 4 at a time with all 4 row loads (and their W[h] loads) issued before
 // any use, so each wave keeps 4 KiB in flight.  R is a template parameter so
 // the per-relation state stays in a handful of registers (occupancy 8).
+// D < 256: a node gets the whole wave, 64 / (D/4) edge SLOTS of D/4 lanes each walking every
+// SLOTS-th group of U edges (graphs with few nodes, e.g. the reference's 845, would otherwise
+// leave most of the chip idle behind a few long serial segments); the slot partials are summed
+// in fixed order (xor-shuffles) at the end, so results stay deterministic.
 // ---------------------------------------------------------------------------
 template <int D, int R>
 __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const int* __restrict__ seg_ptr,
@@ -2131,12 +2140,14 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
                                                               float* __restrict__ dP, long long dp_rel_stride,
                                                               float* __restrict__ dsum, float* __restrict__ dWedge) {
     constexpr int LPR = D / 4;
+    constexpr int SLOTS = 64 / LPR;                     // edge slots per node (one wave per node)
 #ifndef TS_U
 #define TS_U 4
 #endif
     constexpr int U = TS_U;
-    const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64;
     const int sub = threadIdx.x % LPR;
+    const int slot = (threadIdx.x % 64) / LPR;
     const bool live = n < n_nodes;
     const int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
     f32x4 pr[R], acc[R];
@@ -2147,13 +2158,11 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     }
     f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
     const int len = end - beg;
-    // groups of one wave may hold different nodes (D < 256): trip count must be wave-uniform
-    int maxlen = len;
-    if (LPR < 64) {
-#pragma unroll
-        for (int m = 32; m >= LPR; m >>= 1) maxlen = max(maxlen, __shfl_xor(maxlen, m, 64));
-    }
-    for (int k = 0; k < maxlen; k += U) {
+    // slot s takes edge groups k = (j*SLOTS + s)*U; the whole wave is one node and every slot runs
+    // the same trip count (wave-uniform)
+    const int iters = (len + SLOTS * U - 1) / (SLOTS * U);
+    for (int it = 0; it < iters; ++it) {
+        const int k = (it * SLOTS + slot) * U;
         f32x4 d[U];
         int hh[U];
 #pragma unroll
@@ -2201,7 +2210,17 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             }
         }
     }
-    if (!live) return;
+    // slot partials, fixed order: pairs (s, s ^ 1), then (s, s ^ 2), ... (lane distance LPR * m)
+#pragma unroll
+    for (int m = 1; m < SLOTS; m <<= 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] += __shfl_xor(acc[r][q], LPR * m, 64);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s4[q] += __shfl_xor(s4[q], LPR * m, 64);
+    }
+    if (!live || slot != 0) return;
 #pragma unroll
     for (int r = 0; r < R; ++r) st4(dP + r * dp_rel_stride + n * D + sub * 4, acc[r]);
     if (dsum) st4(dsum + n * D + sub * 4, s4);
@@ -2295,9 +2314,12 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(int n_slabs, long lon
 
 __global__ __launch_bounds__(256) void adam_kernel(long long n, float* __restrict__ var, float* __restrict__ m,
                                                    float* __restrict__ v, const float* __restrict__ g, float alpha,
-                                                   float b1, float b2, float eps, int sparse_form) {
+                                                   float b1, float b2, float eps, int sparse_form,
+                                                   const float* __restrict__ alpha_table,
+                                                   const int* __restrict__ step) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (alpha_table) alpha = alpha_table[*step];    // graph-replayable form: alpha of this iteration
     const float gi = g[i];
     float mi = m[i], vi = v[i];
     if (sparse_form) {
@@ -2310,6 +2332,15 @@ __global__ __launch_bounds__(256) void adam_kernel(long long n, float* __restric
     m[i] = mi;
     v[i] = vi;
     var[i] = var[i] - (mi * alpha) / (sqrtf(vi) + eps);
+}
+
+// end of a graph-replayed training step: record the step's loss, advance the iteration counter
+__global__ void step_advance_kernel(int* __restrict__ step, float* __restrict__ loss_history,
+                                    const float* __restrict__ loss) {
+    if (threadIdx.x != 0) return;
+    const int s = *step;
+    if (loss_history && loss) loss_history[s] = *loss;
+    *step = s + 1;
 }
 
 inline unsigned grid_for(long long rows, int lpr) {
@@ -2532,7 +2563,7 @@ int iddgcn_gemm_tn_seg_f32(void* stream, long long M, int d, const float* A, con
 }
 
 int iddgcn_gemm_tn_narrow_blocks(long long M) {
-    long long nb = (M + 127) / 128;
+    long long nb = (M + 15) / 16;          // <= 16 rows per block: short serial chains at small M
     if (nb > 1024) nb = 1024;
     return (int)(nb < 1 ? 1 : nb);
 }
@@ -2721,7 +2752,7 @@ int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const in
     if (n_nodes < 0 || !seg_ptr || !W || !dO || !P || !dP || !dWedge) return IDDGCN_E_BAD_ARG;
     if (n_nodes == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const unsigned grid = grid_for(n_nodes, d / 4);
+    const unsigned grid = grid_for(n_nodes, 64);       // one wave per node
 #define TK(DD, RR) hipLaunchKernelGGL((tail_seg_reduce_kernel<DD, RR>), dim3(grid), dim3(256), 0, st, n_nodes, seg_ptr, h_idx, W, dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge)
 #define TKR(DD)                \
     switch (R) {               \
@@ -2790,7 +2821,22 @@ int iddgcn_adam_f32(void* stream, long long n, float* var, float* m, float* v, c
     if (n < 0 || !var || !m || !v || !g) return IDDGCN_E_BAD_ARG;
     if (n == 0) return 0;
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, var, m, v,
-                       g, alpha, b1, b2, eps, sparse_form);
+                       g, alpha, b1, b2, eps, sparse_form, nullptr, nullptr);
+    return launch_status();
+}
+
+int iddgcn_adam_table_f32(void* stream, long long n, float* var, float* m, float* v, const float* g,
+                          const float* alpha_table, const int* step, float b1, float b2, float eps, int sparse_form) {
+    if (n < 0 || !var || !m || !v || !g || !alpha_table || !step) return IDDGCN_E_BAD_ARG;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, var, m, v,
+                       g, 0.0f, b1, b2, eps, sparse_form, alpha_table, step);
+    return launch_status();
+}
+
+int iddgcn_step_advance(void* stream, int* step, float* loss_history, const float* loss) {
+    if (!step) return IDDGCN_E_BAD_ARG;
+    hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, loss_history, loss);
     return launch_status();
 }
 

@@ -81,15 +81,72 @@ class KerasAdam:
         self.v = torch.zeros_like(params.flat)
         self.iterations = 0
 
+    def alpha_at(self, t):
+        """lr_t of iteration t, computed in fp32 as TF does."""
+        f = np.float32
+        t = f(t)
+        b1p, b2p = f(self.b1) ** t, f(self.b2) ** t
+        return f(self.lr) * np.sqrt(f(1) - b2p) / (f(1) - b1p)
+
     def apply(self, params, grads):
         self.iterations += 1
-        f = np.float32
-        t = f(self.iterations)
-        b1p, b2p = f(self.b1) ** t, f(self.b2) ** t          # computed in fp32 as TF does
-        alpha = f(self.lr) * np.sqrt(f(1) - b2p) / (f(1) - b1p)
+        alpha = self.alpha_at(self.iterations)
         ns = params.n_sparse
         ops.adam(params.flat[:ns], self.m[:ns], self.v[:ns], grads.flat[:ns], alpha, self.b1, self.b2, self.eps, 1)
         ops.adam(params.flat[ns:], self.m[ns:], self.v[ns:], grads.flat[ns:], alpha, self.b1, self.b2, self.eps, 0)
+
+
+    def apply_table(self, params, grads, alpha_table, step):
+        """apply() with alpha = alpha_table[step] read on the device (HIP-graph replay); the caller
+        advances ``step`` and, after the replays, ``iterations``."""
+        ns = params.n_sparse
+        ops.adam_table(params.flat[:ns], self.m[:ns], self.v[:ns], grads.flat[:ns], alpha_table, step, self.b1,
+                       self.b2, self.eps, 1)
+        ops.adam_table(params.flat[ns:], self.m[ns:], self.v[ns:], grads.flat[ns:], alpha_table, step, self.b1,
+                       self.b2, self.eps, 0)
+
+
+class GraphedTrainStep:
+    """Engine.train_step + Keras Adam + loss record captured once in a HIP graph and replayed per
+    epoch: one graph launch per step instead of ~61 host-issued launches (fit() on the reference's
+    fold-sized graphs, N=845 / T=40k, is launch-bound).  Bitwise the same step: the Adam alpha of
+    each iteration comes from the host's float32 formula, tabulated for the ``n_steps`` iterations
+    after ``opt.iterations`` and indexed by a device counter.  Single process only (no all-reduce
+    inside the graph).  Needs a prior eager step on the same (engine, edges) so every workspace
+    exists before capture."""
+
+    def __init__(self, eng, params, grads, opt, adj, ed, n_steps, t_global=None):
+        dev = eng.device
+        t0 = opt.iterations
+        self.opt, self.n = opt, n_steps
+        self.alpha = torch.as_tensor(np.array([opt.alpha_at(t0 + k + 1) for k in range(n_steps)], np.float32),
+                                     device=dev)
+        self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.losses = torch.zeros(max(n_steps, 1), dtype=torch.float32, device=dev)
+        self.done = 0
+        ws = eng.workspace(ed.T, True)
+
+        def body():
+            eng._t_global = t_global
+            with eng._precision():
+                eng.forward(params, adj, ed, ws, True)
+                eng.backward(params, grads, adj, ed, ws)
+            opt.apply_table(params, grads, self.alpha, self.step)
+            ops.step_advance(self.step, self.losses, ws.loss)
+
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            body()
+
+    def replay(self):
+        """One training step; returns the device scalar holding its loss sum."""
+        if self.done >= self.n:
+            raise L.IddgcnError("GraphedTrainStep: alpha table exhausted")
+        self.graph.replay()
+        self.done += 1
+        self.opt.iterations += 1
+        return self.losses[self.done - 1]
 
 
 class Workspace:

@@ -22,7 +22,7 @@ import torch
 
 from . import _lib as L
 from . import ops
-from .engine import NUM_LAYERS, Engine, FlatParams, KerasAdam
+from .engine import NUM_LAYERS, Engine, FlatParams, GraphedTrainStep, KerasAdam
 from .graph import DeviceAdjacency, SparseAdj, get_adj_mats  # noqa: F401  (re-export)
 from .parallel import GradAllReduce, shard_triples, world
 
@@ -230,6 +230,8 @@ class IDDGCN_Model:
         self._dev = None
         self._opt_state = None
         self._graph_cache = {}
+        # fit(): after one eager epoch, replay the captured step (HIP graph) for the rest
+        self.use_graph = True
 
     # -- Keras-ish plumbing ----------------------------------------------------
     def get_layer(self, name):
@@ -377,9 +379,23 @@ class IDDGCN_Model:
         for cb in cbs:
             cb.set_model(self)
         T = len(triples)
+        graphed = None
+        # per-epoch host work only when someone looks at it: else the replays run back to back and
+        # the losses are read once at the end
+        lazy = not verbose and all(isinstance(cb, History) for cb in cbs)
+        pending = []
         for epoch in range(epochs):
-            loss_sum = eng.train_step(self._params, self._grads, self._opt_state, dadj, ed, t_global=T,
-                                      allreduce=allreduce)
+            if graphed is None and self.use_graph and ws == 1 and epoch >= 1 and epochs - epoch > 1:
+                graphed = GraphedTrainStep(eng, self._params, self._grads, self._opt_state, dadj, ed,
+                                           epochs - epoch, t_global=T)
+            if graphed is not None:
+                loss_sum = graphed.replay()
+            else:
+                loss_sum = eng.train_step(self._params, self._grads, self._opt_state, dadj, ed, t_global=T,
+                                          allreduce=allreduce)
+            if lazy:
+                pending.append(loss_sum if graphed is not None else loss_sum.clone())
+                continue
             loss = float(loss_sum.item()) / T
             if verbose and rank == 0:
                 print(f"Epoch {epoch + 1}/{epochs} - loss: {loss:.6f}")
@@ -390,6 +406,9 @@ class IDDGCN_Model:
                 cb.on_epoch_end(epoch, logs)
             if self.stop_training:
                 break
+        if pending:
+            for epoch, l in enumerate(torch.cat([x.reshape(1) for x in pending]).cpu().tolist()):
+                history.on_epoch_end(epoch, {"loss": l / T})
         self._sync_to_host()
         return history
 

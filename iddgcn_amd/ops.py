@@ -305,6 +305,25 @@ def adam(var, m, v, g, alpha, b1, b2, eps, sparse_form):
                                     float(b2), float(eps), int(sparse_form)), "adam")
 
 
+def adam_table(var, m, v, g, alpha_table, step, b1, b2, eps, sparse_form):
+    """iddgcn_adam_f32 with alpha = alpha_table[step[0]] read on the device (graph-replayable)."""
+    n = var.numel()
+    for t, nm in ((m, "m"), (v, "v"), (g, "g")):
+        if t.numel() != n:
+            raise L.IddgcnError(f"adam: {nm} size mismatch")
+    _req(alpha_table, _F32, None, "alpha_table")
+    _req(step, _I32, (1,), "step")
+    L.check(L.lib().iddgcn_adam_table_f32(_stream(), n, _ptr(var), _ptr(m), _ptr(v), _ptr(g), _ptr(alpha_table),
+                                          _ptr(step), float(b1), float(b2), float(eps), int(sparse_form)),
+            "adam_table")
+
+
+def step_advance(step, loss_history=None, loss=None):
+    """loss_history[step] = loss; step += 1 (one device thread)."""
+    _req(step, _I32, (1,), "step")
+    L.check(L.lib().iddgcn_step_advance(_stream(), _ptr(step), _ptr(loss_history), _ptr(loss)), "step_advance")
+
+
 # -- device graph build (include/iddgcn_graph.h) ------------------------------------------------
 _I64 = torch.int64
 _U8 = torch.uint8

@@ -225,6 +225,15 @@ int iddgcn_reduce_slabs_f32(void* stream, int n_slabs, long long n, const float*
 int iddgcn_adam_f32(void* stream, long long n, float* var, float* m, float* v, const float* g,
                     float alpha, float b1, float b2, float eps, int sparse_form);
 
+/* The same update with alpha = alpha_table[*step] read on the device, so a captured training step
+ * (HIP graph) can be replayed for successive iterations; iddgcn_step_advance (one thread) then
+ * stores *loss into loss_history[*step] (either may be NULL) and increments *step.  The table
+ * holds the host-computed alphas of the iterations to run (IDDGCN.py:399 fit epochs). */
+int iddgcn_adam_table_f32(void* stream, long long n, float* var, float* m, float* v, const float* g,
+                          const float* alpha_table, const int* step, float b1, float b2, float eps,
+                          int sparse_form);
+int iddgcn_step_advance(void* stream, int* step, float* loss_history, const float* loss);
+
 #ifdef __cplusplus
 }
 #endif

@@ -284,8 +284,9 @@ def test_distmult_bce_matches_autograd(D, cuda):
 @pytest.mark.parametrize("D", DIMS)
 @pytest.mark.parametrize("R,skew", [(1, False), (3, True), (5, False)])
 def test_distmult_bce_heads_fused(D, R, skew, cuda):
-    """One-pass head-grouped form == distmult_bce + seg_gather_reduce: p / ds / do / dXh bitwise,
-    drel / loss to rounding (partial sums visit edges in head order)."""
+    """One-pass head-grouped form == distmult_bce + seg_gather_reduce: p / ds / do bitwise, dXh
+    bitwise at D=256 (one edge slot per head) and to 1e-5 of max|dXh| below (the head's edges are split over
+    64/(D/4) slots), drel / loss to rounding (partial sums visit edges in head order)."""
     g = torch.Generator().manual_seed(41 + D + R)
     N, T = 300, 7001
     Xh = torch.rand(N, D, generator=g).to(cuda)
@@ -323,7 +324,12 @@ def test_distmult_bce_heads_fused(D, R, skew, cuda):
     ops.reduce_slabs(sl_l2, nb, loss2)
     assert torch.equal(p, p2) and torch.equal(ds, ds2)
     assert torch.equal(do, do2)
-    assert torch.equal(dXh, dXh2)           # includes zero rows of heads without edges
+    if D == 256:                            # one edge slot per head: the same sequential sum
+        assert torch.equal(dXh, dXh2)       # includes zero rows of heads without edges
+    else:                                   # 64/(D/4) edge slots per head, partials summed at the end
+        assert (dXh2.double() - dXh.double()).abs().max() <= 1e-5 * dXh.double().abs().max()
+        empty = (hptr[1:] == hptr[:-1]).nonzero().flatten()
+        assert torch.equal(dXh2[empty], torch.zeros_like(dXh2[empty]))
     close(drel2, drel.double(), 1e-5)
     assert abs(loss2.item() - loss.item()) <= 1e-5 * abs(loss.item())
 

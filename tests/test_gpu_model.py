@@ -300,6 +300,31 @@ def test_fit_api_drop_in(golden, cuda, tmp_path):
     assert np.array_equal(emb, saved["E"])
 
 
+def test_fit_graph_replay_bitwise_equals_eager(golden, cuda):
+    """fit(): the HIP-graph replay of the training step (engine.GraphedTrainStep: device-side Adam
+    alpha table and step counter) gives bitwise the eager loss history and weights, with and without
+    per-epoch host callbacks (lazy loss collection)."""
+    from iddgcn_amd import Adam, BinaryCrossentropy, get_IDDGCN_Model
+    d = golden("fold0_data.npz")
+    X = d["X_train"][None]
+    adj = get_adj_mats(d["X_train"], N_ENT, N_REL)
+    out = {}
+    for graph, verbose in ((False, 0), (True, 0), (True, 1)):
+        model = get_IDDGCN_Model(N_ENT, N_REL, 64, 64, 7, None, 0, 0)
+        model.use_graph = graph
+        model.neg_triples = d["X_train_neg"][None]
+        model.compile(loss=BinaryCrossentropy(), optimizer=Adam(learning_rate=0.001))
+        hist = model.fit(x=[np.arange(N_ENT)[None], X[:, :, 0], X[:, :, 1], X[:, :, 2], adj],
+                         y=np.ones((1, X.shape[1])), epochs=12, verbose=verbose)
+        out[(graph, verbose)] = (hist.history["loss"], model.get_weights())
+    ref_loss, ref_w = out[(False, 0)]
+    assert len(ref_loss) == 12
+    for key in ((True, 0), (True, 1)):
+        loss, w = out[key]
+        assert loss == ref_loss, key
+        assert all(np.array_equal(a, b) for a, b in zip(w, ref_w)), key
+
+
 def test_standalone_layer_call_matches_oracle(golden, cuda):
     """IDDGCN_Layer(...)([E, h, E[h], t, E[t], adj]) == IDDGCN.py:60-79 (oracle layer_call)."""
     from iddgcn_amd import IDDGCN_Layer
