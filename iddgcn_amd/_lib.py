@@ -48,6 +48,7 @@ SIGNATURES = {
     "iddgcn_set_gemm_precision": (ci, [ci]),
     "iddgcn_gemm_tn_blocks": (ci, [cll, ci]),
     "iddgcn_gemm_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
+    "iddgcn_rowgemm_batched_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs), ci]),
     "iddgcn_adam_table_f32": (ci, [vp, cll, vp, vp, vp, vp, vp, vp, cf, cf, cf, ci]),
     "iddgcn_step_advance": (ci, [vp, vp, vp, vp]),
     "iddgcn_gemm_tn_seg_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci, vp, vp, ci, vp, vp, cll, vp, vp, ci]),

@@ -285,9 +285,17 @@ struct RowGemmP {
     int tiles_per_block;
 };
 
+// up to ROWGEMM_BATCH independent row GEMMs of one width in one launch (blockIdx.y = entry): the
+// node-level projections of a step are many tiny launches at the reference's 845 nodes
+constexpr int ROWGEMM_BATCH = 16;
+struct RowGemmBatch {
+    RowGemmP p[ROWGEMM_BATCH];
+};
+
 template <int D>
-__global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmP p) {
+__global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmBatch pb) {
     using C = RG<D>;
+    const RowGemmP& p = pb.p[blockIdx.y];
     __shared__ __attribute__((aligned(16))) float As[C::TR * C::LDA];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -2411,6 +2419,7 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     if (!a) return IDDGCN_E_BAD_ARG;
     if (!dim_ok(a->D)) return IDDGCN_E_BAD_DIM;
     if (a->R < 0 || a->R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (a->M == 0) return 0;                 // nothing to do (an empty C may have a null pointer)
     if (a->M < 0 || !a->A || !a->B || !a->C) return IDDGCN_E_BAD_ARG;
     if (a->R > 0 && (!a->coef || !a->V)) return IDDGCN_E_BAD_ARG;
     if (a->act == IDDGCN_ACT_DSIGMOID && !a->aux) return IDDGCN_E_BAD_ARG;
@@ -2430,7 +2439,9 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
         long long nb = nt < (MAXB) ? nt : (MAXB);                                               \
         p.tiles_per_block = (int)((nt + nb - 1) / nb);                                          \
         nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;                                  \
-        hipLaunchKernelGGL(rowgemm_kernel<DD>, dim3((unsigned)nb), dim3(RG<DD>::NW * 64), 0, st, p); \
+        RowGemmBatch pb;                                                                        \
+        pb.p[0] = p;                                                                            \
+        hipLaunchKernelGGL(rowgemm_kernel<DD>, dim3((unsigned)nb), dim3(RG<DD>::NW * 64), 0, st, pb); \
     }
     const bool gatherV = p.R > 0 && p.v_row_stride != 0;
     const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
@@ -2503,6 +2514,56 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
         default: RGEMM(256, 256); break;
     }
 #undef RGEMM
+    return launch_status();
+}
+
+int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
+    if (!a || n < 0 || n > ROWGEMM_BATCH) return IDDGCN_E_BAD_ARG;
+    if (n == 0) return 0;
+    bool one_launch = a[0].D != 256;
+    for (int k = 0; k < n; ++k) {
+        if (!dim_ok(a[k].D) || a[k].D != a[0].D) return IDDGCN_E_BAD_DIM;
+        if (a[k].R < 0 || a[k].R > MAX_R) return IDDGCN_E_BAD_REL;
+        if (a[k].M == 0) continue;
+        if (a[k].M < 0 || !a[k].A || !a[k].B || !a[k].C) return IDDGCN_E_BAD_ARG;
+        if (a[k].R > 0 && (!a[k].coef || !a[k].V)) return IDDGCN_E_BAD_ARG;
+        if (a[k].act == IDDGCN_ACT_DSIGMOID && !a[k].aux) return IDDGCN_E_BAD_ARG;
+        if (a[k].act == IDDGCN_ACT_DSIGMOID_COMBINE && (a[k].R < 1 || a[k].R + 1 > MAX_R || a[k].v_row_stride == 0))
+            return IDDGCN_E_BAD_ARG;
+        if (a[k].act < IDDGCN_ACT_NONE || a[k].act > IDDGCN_ACT_DSIGMOID_COMBINE) return IDDGCN_E_BAD_ARG;
+    }
+    if (!one_launch) {          // D = 256: the pipelined kernels, one launch per entry
+        for (int k = 0; k < n; ++k) {
+            const int rc = iddgcn_rowgemm_f32(stream, a + k);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    RowGemmBatch pb;
+    long long nbmax = 0;
+    const int d = a[0].D;
+    const int tr = d == 32 ? RG<32>::TR : d == 64 ? RG<64>::TR : RG<128>::TR;
+    const long long maxb = d == 128 ? 1024 : 2048;
+    for (int k = 0; k < n; ++k) {
+        RowGemmP& p = pb.p[k];
+        p.M = a[k].M; p.A = a[k].A; p.a_idx = a[k].a_idx; p.B = a[k].B; p.b_trans = a[k].b_trans;
+        p.C = a[k].C; p.accumulate = a[k].accumulate; p.R = a[k].R; p.coef = a[k].coef; p.coef_idx = a[k].coef_idx;
+        p.V = a[k].V; p.v_idx = a[k].v_idx; p.v_rel_stride = a[k].v_rel_stride; p.v_row_stride = a[k].v_row_stride;
+        p.act = a[k].act; p.aux = a[k].aux; p.v_runs_max = a[k].v_runs_max;
+        const long long nt = ((long long)p.M + tr - 1) / tr;
+        long long nb = nt < maxb ? nt : maxb;
+        p.tiles_per_block = nb > 0 ? (int)((nt + nb - 1) / nb) : 1;
+        nb = nb > 0 ? (nt + p.tiles_per_block - 1) / p.tiles_per_block : 0;
+        if (nb > nbmax) nbmax = nb;
+    }
+    if (nbmax == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 g((unsigned)nbmax, (unsigned)n);
+    switch (d) {
+        case 32: hipLaunchKernelGGL(rowgemm_kernel<32>, g, dim3(RG<32>::NW * 64), 0, st, pb); break;
+        case 64: hipLaunchKernelGGL(rowgemm_kernel<64>, g, dim3(RG<64>::NW * 64), 0, st, pb); break;
+        default: hipLaunchKernelGGL(rowgemm_kernel<128>, g, dim3(RG<128>::NW * 64), 0, st, pb); break;
+    }
     return launch_status();
 }
 

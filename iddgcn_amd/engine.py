@@ -270,13 +270,12 @@ class Engine:
         E = P["E"]
         # AE_r = A_r·E, all relations in one launch (IDDGCN.py:69-70)
         ops.spmm_csr(adj.fwd_ptr, adj.fwd_col, adj.fwd_val, E, ws.AE, R, N)
-        # P_r^l = AE_r·K_r^l (node-level form of IDDGCN.py:71-72,76-77)
-        for l in range(NUM_LAYERS):
-            K = P[f"K{l + 1}"]
-            for r in range(R):
-                ops.rowgemm(ws.AE[r], K[r], ws.P[l, r])
-        # layer 1: x·S1 is node-level for both sides (inputs are E[h], E[t])
-        ops.rowgemm(E, P["S1"], ws.ES1)
+        # P_r^l = AE_r·K_r^l (node-level form of IDDGCN.py:71-72,76-77) and, layer 1, x·S1 at node
+        # level for both sides (inputs E[h], E[t]): independent GEMMs, batched (one launch below D=256)
+        proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], {}) for l in range(NUM_LAYERS) for r in range(R)]
+        proj.append((E, P["S1"], ws.ES1, {}))
+        for i in range(0, len(proj), 16):
+            ops.rowgemm_batched(proj[i:i + 16])
         ops.alpha_fwd(E, P["Wa1"], P["ba1"], ws.Ssm[0], ws.W[0])
         ops.gather_rows(ws.W[0], ed.h, ws.Wedge[0])
         ops.combine(ws.ES1, ws.W[0], ws.P[0], ws.X[0])
@@ -356,7 +355,8 @@ class Engine:
             K, dK = P[f"K{l + 1}"], G[f"K{l + 1}"]
             for r in range(R):
                 ops.gemm_tn(ws.AE[r], ws.dP[r], dK[r], ws.tn_slab)
-                ops.rowgemm(ws.dP[r], K[r], ws.dAE[r], b_trans=True, accumulate=(l != 2))
+            ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2)))
+                                 for r in range(R)])
             dOn, dOn_next = dOn_next, dOn
             do, do_next = do_next, do
         # dE += sum_r A_r^T dAE_r  (gradient through all_e -> sparse_dense_matmul)

@@ -64,8 +64,23 @@ def sddmm_csr(row_ptr, col, G, X, out, n_seg, n_rows):
                                          _ptr(out)), "sddmm_csr")
 
 
-def rowgemm(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, coef_idx=None, V=None,
-            v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None, v_runs_max=0):
+def rowgemm(A, B, C, **kw):
+    """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32); see _rowgemm_args."""
+    args = _rowgemm_args(A, B, C, **kw)
+    L.check(L.lib().iddgcn_rowgemm_f32(_stream(), ctypes.byref(args)), "rowgemm")
+
+
+def rowgemm_batched(calls):
+    """Independent row GEMMs of one width in one launch (iddgcn_rowgemm_batched_f32).  calls: list of
+    (A, B, C, kwargs) as for rowgemm; at most 16."""
+    if not calls:
+        return
+    arr = (L.RowGemmArgs * len(calls))(*[_rowgemm_args(A, B, C, **kw) for A, B, C, kw in calls])
+    L.check(L.lib().iddgcn_rowgemm_batched_f32(_stream(), arr, len(calls)), "rowgemm_batched")
+
+
+def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, coef_idx=None, V=None,
+                  v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None, v_runs_max=0):
     """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32).  act=ACT_DSIGMOID_COMBINE
     multiplies by x(1-x) with x = sigmoid(V_0[v_idx] + sum_r coef_r V_{r+1}[v_idx]) (V: R+1 tables);
     v_runs_max bounds the runs of equal v_idx per aligned 32-row block (0 = unknown)."""
@@ -90,13 +105,12 @@ def rowgemm(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, 
     if act == L.ACT_DSIGMOID_COMBINE:
         if not R or V is None or V.numel() < (R + 1) * int(v_rel_stride):
             raise L.IddgcnError("ACT_DSIGMOID_COMBINE needs coef (R columns) and R+1 V tables")
-    args = L.RowGemmArgs(
+    return L.RowGemmArgs(
         M=M, D=D, A=_ptr(A), a_idx=_ptr(a_idx), B=_ptr(B), b_trans=int(b_trans), C=_ptr(C),
         accumulate=int(accumulate), R=R, coef=_ptr(coef), coef_idx=_ptr(coef_idx), V=_ptr(V),
         v_idx=_ptr(v_idx), v_rel_stride=int(v_rel_stride),
         v_row_stride=int(D if v_row_stride is None else v_row_stride), act=int(act), aux=_ptr(aux),
         v_runs_max=int(v_runs_max))
-    L.check(L.lib().iddgcn_rowgemm_f32(_stream(), ctypes.byref(args)), "rowgemm")
 
 
 def tn_blocks(M, D):

@@ -218,6 +218,11 @@ int iddgcn_gather_rows_f32(void* stream, long long M, int width, const float* sr
 int iddgcn_reduce_slabs_f32(void* stream, int n_slabs, long long n, const float* slab,
                             float* out, int accumulate, float scale);
 
+/* Up to 16 independent iddgcn_rowgemm_f32 calls of one width D (e.g. the per-relation, per-layer
+ * node projections A_r·E·K_r of IDDGCN.py:71-77) in ONE launch for D < 256; at D = 256 the entries
+ * run one after another on the pipelined kernels. */
+int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* args, int n);
+
 /* Keras-2.7 Adam, one tensor (IDDGCN.py:174,392).  sparse_form=0: TF ApplyAdam
  *   m += (g-m)(1-b1); v += (g^2-v)(1-b2); var -= alpha m/(sqrt(v)+eps)
  * sparse_form=1 (_resource_apply_sparse, embeddings): m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2.

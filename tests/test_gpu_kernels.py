@@ -476,6 +476,36 @@ def _maxrel(got, ref):
     return ((got.double() - ref).abs().max() / ref.abs().max()).item()
 
 
+@pytest.mark.parametrize("D", DIMS)
+def test_rowgemm_batched_equals_single_calls(D, cuda):
+    """iddgcn_rowgemm_batched_f32 (one launch for D < 256) == the same GEMMs one call at a time,
+    bitwise: different row counts (one empty), plain / transposed-accumulate / combine epilogues."""
+    g = torch.Generator().manual_seed(3 * D)
+    N, R = 120, 2
+    calls = []
+    for k, M in enumerate([845, 77, 0, 4000, 845]):
+        A = torch.randn(max(M, 1), D, generator=g).to(cuda)
+        B = (torch.randn(D, D, generator=g) / D ** 0.5).to(cuda)
+        kw = {}
+        if k == 1:
+            kw = dict(b_trans=True, accumulate=True)
+        elif k == 3:
+            kw = dict(coef=torch.rand(N, R, generator=g).to(cuda), coef_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
+                      V=torch.randn(R, N, D, generator=g).to(cuda), v_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
+                      v_rel_stride=N * D, act=L.ACT_SIGMOID)
+        C0 = torch.randn(M, D, generator=g).to(cuda)
+        calls.append((A, B, C0, kw))
+    single, batched = [], []
+    for A, B, C0, kw in calls:
+        C = C0.clone()
+        ops.rowgemm(A, B, C, M=C.shape[0], **kw)
+        single.append(C)
+    outs = [C0.clone() for _, _, C0, _ in calls]
+    ops.rowgemm_batched([(A, B, C, dict(kw, M=C.shape[0])) for (A, B, _, kw), C in zip(calls, outs)])
+    for a, b in zip(single, outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("R", [1, 2])
 @pytest.mark.parametrize("case", ["uniform", "hub", "ragged", "tiny"])
 def test_gemm_tn_seg_fused(R, case, cuda):
