@@ -1,41 +1,38 @@
 """IDDGCN training-step throughput on MI355X (BASELINE.json).
 
-Metric: adjacency edges/s = M / (wall time of one full training step:
-positive forward + negative forward + backward + Keras Adam), whole job.
+Metric: adjacency edges/s = M / (wall time of one full training step: positive forward + negative
+forward + backward + Keras Adam), whole job.
 
-Workload (default, N=1 GPU): BASELINE.json configs[2] — synthetic mutation–drug
-graph, 100,000 nodes, 2 relations, 2,000,000 directed (reverse-closed) edges,
-feature dim 256, fp32, 1:1 negatives (B_pos = B_neg = 2M, T = 4M scored edges).
-With --gpus N (one process per GPU, torchrun, RCCL) the job is weak-scaled:
-M = 2M x N edges on the same 100k nodes, every rank owns 4M scored edges and
-the ranks meet in ONE all-reduce of the flat gradient buffer per step.
+Workloads (BASELINE.json configs; synthetic seeded mutation–drug graphs, reference-distribution
+random init, inputs resident in HBM before the timed region):
+  --config 3 (default)  100k nodes, 2 relations, 2M directed reverse-closed edges, D=256, 1:1
+                        negatives (T = 4M scored edges).  With --gpus N the job is WEAK-scaled: every
+                        rank owns 4M scored edges of a 2M*N-edge graph on the same 100k nodes.
+  --config 4            1M nodes, 2 relations, 20M edges, D=256, T = 40M scored edges; STRONG-scaled
+                        (the 40M scored edges are split over the N ranks).
+  --config 2            the reference's fold-0 shape (845 nodes, 4 relations, D=64), one GPU.
+Multi-GPU: `--gpus N` starts N ranks itself (torch.distributed.run, one process per GPU, RCCL)
+before anything touches the GPU, or joins the N ranks a launcher already started; the ranks meet in
+one bucketed in-place all-reduce of the flat gradient buffer per step (parallel.BucketedAllReduce).
 
-Also reported, on the same JSON line:
-  roofline      the dominant kernel's achieved FLOP rate (algorithmic flops per
-                launch / its HIP-event duration inside the timed steps) against
-                the f32 MFMA peak;
-  cpu_baseline  the reference formulation (oracle/ref_model.py, torch-CPU fp32,
-                per-edge GEMMs, IDDGCN.py:60-79) on this host's cores, on a
-                bounded sample of the same workload (rank 0, N=1 only).
+Also reported on the same JSON line:
+  roofline      the dominant kernel's achieved HBM rate (algorithmic bytes per launch / its
+                HIP-event duration inside the timed steps, events on the launch stream) vs 8 TB/s;
+  cpu_baseline  the reference formulation (oracle/ref_model.py: torch-CPU fp32, per-edge GEMMs,
+                A_r.E per layer, Keras BCE, Keras Adam) on this host's cores, on a bounded sample
+                of the same workload (rank 0, N=1 only).
 """
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from iddgcn_amd.engine import Engine, FlatParams, KerasAdam  # noqa: E402
-from iddgcn_amd.graph import get_adj_mats  # noqa: E402
-from iddgcn_amd.parallel import GradAllReduce  # noqa: E402
-from iddgcn_amd.utils import synthetic_graph  # noqa: E402
 
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md, f32-input MFMA dense peak
 MFMA_F16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md, bf16/f16 MFMA dense peak (16x the f32 rate)
@@ -46,6 +43,38 @@ GEMM_NOTE = {
              "(include/iddgcn.h iddgcn_set_gemm_precision)",
     "exact": "exact f32 MFMA (v_mfma_f32_32x32x2_f32, bitwise an fmaf chain) everywhere",
 }
+# the arithmetic the path computes in, per GEMM mode (the bench line's "dtype")
+DTYPE = {"split": "f32 (D=256 GEMMs on split-fp16x2 operands, fp32 accumulate)", "exact": "f32"}
+
+CONFIGS = {
+    2: dict(name="synthetic-fold0-shape", N=845, R=4, M=37_510, D=64, scaling="weak"),
+    3: dict(name="synthetic-3", N=100_000, R=2, M=2_000_000, D=256, scaling="weak"),
+    4: dict(name="synthetic-4", N=1_000_000, R=2, M=20_000_000, D=256, scaling="strong"),
+}
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N without a launcher: run N ranks under torch.distributed.run as a CHILD process (nothing
+    has touched the GPU yet) and return its exit code; inside a launcher, check its world size."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None:
+        if args.gpus == 1:
+            return None
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__),
+               *sys.argv[1:]]
+        return subprocess.call(cmd)
+    if int(world_env) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks")
+    return None
 
 
 def kernel_roofline(name, N, R, D, T, gemm, avg_ms):
@@ -76,10 +105,11 @@ def kernel_roofline(name, N, R, D, T, gemm, avg_ms):
     return out
 
 
-def stream_probe(dev, T, D, reps=3):
+def stream_probe(torch, dev, T, D, reps=3):
     """What this box's HBM sustains for the access mixes of the edge kernels, measured in the same
-    run on one edge table (T x D fp32): write-only (fill), read+write 1:1 (copy), read-only
-    (sum).  Context for roofline.frac, whose peak is the 8 TB/s vendor figure."""
+    run on one edge table (T x D fp32, capped at 4M rows): write-only (fill), read+write 1:1 (copy),
+    read-only (sum).  Context for roofline.frac, whose peak is the 8 TB/s vendor figure."""
+    T = min(T, 4_000_000)
     a = torch.empty(T, D, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
     out = {}
@@ -100,9 +130,9 @@ def stream_probe(dev, T, D, reps=3):
 
 
 def pmc_traffic(kernel, gemm, workload, world):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same bench
-    command (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x2 per the
-    gfx950 correction + WRITE_SIZE, separate --pmc passes), or None when no such profile exists."""
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the same bench
+    command (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x2 per the gfx950
+    correction + WRITE_SIZE, separate --pmc passes), or None when no such profile exists."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
         with open(path) as f:
@@ -112,13 +142,8 @@ def pmc_traffic(kernel, gemm, workload, world):
             return rec[key]["bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
-CONFIGS = {
-    3: dict(name="synthetic-3", N=100_000, R=2, M=2_000_000, D=256),
-    2: dict(name="synthetic-fold0-shape", N=845, R=4, M=37_510, D=64),
-}
 
-
-def reference_init(N, R, D, seed):
+def reference_init(np, N, R, D, seed):
     """Reference-distribution init (IDDGCN.py:25-58, 92-101, 221-224)."""
     rng = np.random.default_rng(seed)
     p = {"E": rng.random((N, D), dtype=np.float32)}
@@ -133,18 +158,23 @@ def reference_init(N, R, D, seed):
 
 
 def cpu_baseline(cfg, budget_s=25.0):
-    """Reference formulation on the host cores, bounded sample of the same workload."""
-    from oracle.ref_model import KerasAdam as RefAdam  # noqa: F401  (same step as the reference)
-    from oracle.ref_model import adj_to_torch, keras_bce, model_forward, to_torch_params
+    """The reference formulation on the host cores (one full step: pos + neg forward, autograd backward,
+    Keras Adam), on a bounded sample of the same workload."""
+    import numpy as np
+    import torch
+    from oracle.ref_model import KerasAdam, adj_to_torch, keras_bce, model_forward, to_torch_params
     from oracle.ref_utils import get_adj_coo
+    from iddgcn_amd.utils import synthetic_graph
     N, R, D = cfg["N"], cfg["R"], cfg["D"]
     M_s = 40_000 if cfg["M"] > 40_000 else cfg["M"]
     pos, neg = synthetic_graph(N, R, M_s, seed=11)
-    params = reference_init(N, R, D, 89)
+    params = {k: v for k, v in reference_init(np, N, R, D, 89).items()}
     adj = adj_to_torch(get_adj_coo(pos, N, R), N, torch.float32)
+    opt = KerasAdam()
     threads = torch.get_num_threads()
 
     def step():
+        nonlocal params
         P = to_torch_params(params, torch.float32)
         y_pos = model_forward(P, pos[:, 0], pos[:, 1], pos[:, 2], adj)
         y_neg = model_forward(P, neg[:, 0], neg[:, 1], neg[:, 2], adj)
@@ -152,9 +182,7 @@ def cpu_baseline(cfg, budget_s=25.0):
         loss = keras_bce(torch.cat([torch.ones_like(y_pos), torch.zeros_like(y_neg)]), y) / N
         keys = [k for k in P if P[k].requires_grad]
         grads = torch.autograd.grad(loss, [P[k] for k in keys])
-        with torch.no_grad():  # Adam-sized elementwise update over every parameter
-            for k, g in zip(keys, grads):
-                P[k].sub_(1e-3 * g / (g.abs() + 1e-7))
+        params = opt.step(params, {k: g.numpy() for k, g in zip(keys, grads)}, dtype=np.float32)
 
     t0 = time.perf_counter()
     step()
@@ -167,66 +195,48 @@ def cpu_baseline(cfg, budget_s=25.0):
         times.append(time.perf_counter() - t0)
     t = statistics.median(times)
     return {"value": M_s / t, "unit": "adjacency edges/s", "cores": threads, "kind": "port",
-            "sample": (f"oracle/ref_model.py reference formulation (torch-CPU fp32, per-edge GEMMs, A_r.E per layer), "
-                       f"N={N} D={D} R={R}, M={M_s} edges + {M_s} negatives (bounded sample of the workload); "
-                       f"median of {n} steps after 1 warm-up, {t:.2f} s/step")}
+            "sample": (f"oracle/ref_model.py reference formulation (torch-CPU fp32: per-edge GEMMs, A_r.E per layer, "
+                       f"Keras BCE, autograd backward, Keras Adam), N={N} D={D} R={R}, M={M_s} edges + {M_s} "
+                       f"negatives (bounded sample of the workload); median of {n} steps after 1 warm-up, "
+                       f"{t:.2f} s/step")}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gemm", default="split", choices=["split", "exact"],
-                    help="operand precision of the D=256 MFMA GEMMs (the other mode is timed too)")
-    ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")
-    ap.add_argument("--fuse-tail-seg", action="store_true",
-                    help="layers 2-3: tail segmented reduction fused into the dS pass (A/B)")
-    ap.add_argument("--recompute-x1", action="store_true",
-                    help="layer-2 backward rebuilds x^1 on chip instead of re-reading it (A/B)")
-    args = ap.parse_args()
+def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=True):
+    """Build one workload on the GPU, time W + K training steps, return the bench-line fields."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from iddgcn_amd.engine import Engine, FlatParams, KerasAdam
+    from iddgcn_amd.graph import get_adj_mats
+    from iddgcn_amd.parallel import BucketedAllReduce, shard_range
+    from iddgcn_amd.utils import synthetic_graph
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    cfg = CONFIGS[args.config]
+    cfg = CONFIGS[cid]
     N, R, D = cfg["N"], cfg["R"], cfg["D"]
-    M = cfg["M"] * world                                  # weak scaling: M per GPU fixed
-
+    weak = cfg["scaling"] == "weak"
+    M = cfg["M"] * world if weak else cfg["M"]            # weak: per-GPU work fixed
     pos, neg = synthetic_graph(N, R, M, seed=0)           # identical on every rank (seeded)
-    adj_mats = get_adj_mats(pos, N, R)
     T = len(pos) + len(neg)
-    # this rank's contiguous shard of the scored edges (positives ++ negatives)
-    lo, hi = rank * T // world, (rank + 1) * T // world
-    tri = np.concatenate([pos, neg])[lo:hi]
-    lab = np.concatenate([np.ones(len(pos), np.float32), np.zeros(len(neg), np.float32)])[lo:hi]
-
-    eng = Engine(N, R, D, dev, gemm=args.gemm, recompute_x1=args.recompute_x1,
-                 fuse_tail_seg=args.fuse_tail_seg)
-    P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
-    init = reference_init(N, R, D, 89)
-    adj = eng.adjacency(adj_mats)
+    lo, hi = shard_range(T, rank, world)                  # this rank's contiguous shard (pos ++ neg)
+    npos = len(pos)
+    tri = np.concatenate([pos[lo:min(hi, npos)], neg[max(lo - npos, 0):max(hi - npos, 0)]])
+    lab = np.concatenate([np.ones(max(0, min(hi, npos) - lo), np.float32),
+                          np.zeros(max(0, hi - max(lo, npos)), np.float32)])
+    eng = Engine(N, R, D, dev, gemm=gemm, recompute_x1=args.recompute_x1, fuse_tail_seg=args.fuse_tail_seg)
+    adj = get_adj_mats(pos, N, R, device=dev)            # device graph build (bit-identical to the host's)
     ed = eng.edges(tri, lab)
-    allreduce = GradAllReduce(G.flat) if world > 1 else None
     del pos, neg, tri, lab
+    P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
+    init = reference_init(np, N, R, D, 89)
+    comm = BucketedAllReduce() if world > 1 else None
 
     def timed_run(mode, probe):
         """W warm-up steps, then K timed steps between barriers + synchronize; max over ranks."""
         eng.gemm = mode
         P.load(init)                       # every mode starts from the same parameters
         opt = KerasAdam(P)
-
-        def step():
-            return eng.train_step(P, G, opt, adj, ed, t_global=T, allreduce=allreduce)
-
         for _ in range(args.warmup):
-            step()
+            eng.train_step(P, G, opt, adj, ed, t_global=T, comm=comm)
         torch.cuda.synchronize()
         eng.probe = {} if probe else None
         if world > 1:
@@ -234,7 +244,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            loss = step()
+            loss = eng.train_step(P, G, opt, adj, ed, t_global=T, comm=comm)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -246,49 +256,93 @@ def main():
         probe_out, eng.probe = eng.probe, None
         return elapsed, float(loss.item()) / T, probe_out
 
-    elapsed, loss_val, probe = timed_run(args.gemm, True)
-    other = None
-    if not args.no_other_mode:
-        mode2 = "exact" if args.gemm == "split" else "split"
+    elapsed, loss_val, probe = timed_run(gemm, probe_kernels)
+    out = {"value": M / (elapsed / args.steps), "ms_per_step": elapsed / args.steps * 1e3,
+           "scaling": cfg["scaling"], "dtype": DTYPE[gemm], "gemm_operands": GEMM_NOTE[gemm],
+           "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
+                      "scored_edges": T, "scored_edges_per_gpu": ed.T, "feat_dim": D,
+                      "parallelism": f"edge-dp{world}", "gemm": gemm},
+           "scored_edges_per_s": T / (elapsed / args.steps), "loss": loss_val}
+    if other_mode:
+        mode2 = "exact" if gemm == "split" else "split"
         el2, loss2, _ = timed_run(mode2, False)
-        other = {"gemm": mode2, "value": M / (el2 / args.steps), "ms_per_step": el2 / args.steps * 1e3,
-                 "loss": loss2}
+        out["other_gemm_mode"] = {"gemm": mode2, "dtype": DTYPE[mode2], "value": M / (el2 / args.steps),
+                                  "ms_per_step": el2 / args.steps * 1e3, "loss": loss2}
+    if probe:
+        # dominant kernel: largest total event time inside the timed steps; its roofline is the larger
+        # of the MFMA time (hardware MFMA work on the mode's peak) and the HBM time (algorithmic bytes)
+        kt = {k: [a.elapsed_time(b) for a, b in v] for k, v in probe.items()}
+        dom = max(kt, key=lambda k: sum(kt[k]))
+        rl = kernel_roofline(dom, N, R, D, ed.T, gemm, statistics.mean(kt[dom]))
+        rl["traffic"], rl["traffic_source"] = pmc_traffic(dom, gemm, cfg["name"], world)
+        rl["box_stream_GBs"] = stream_probe(torch, dev, ed.T, D)
+        out["kernel_ms_per_step"] = {k: sum(v) / args.steps for k, v in kt.items()}
+        out["roofline"] = rl
+    del eng, adj, ed, P, G
+    torch.cuda.empty_cache()
+    return out
 
-    # dominant kernel: largest total event time inside the timed steps; its roofline is the larger
-    # of the MFMA time (hardware MFMA work on the mode's peak) and the HBM time (algorithmic bytes)
-    T_local = ed.T
-    kt = {k: [a.elapsed_time(b) for a, b in v] for k, v in probe.items()}
-    dom = max(kt, key=lambda k: sum(kt[k]))
-    avg_ms = statistics.mean(kt[dom])
-    rl = kernel_roofline(dom, N, R, D, T_local, args.gemm, avg_ms)
-    rl["traffic"], rl["traffic_source"] = pmc_traffic(dom, args.gemm, cfg["name"], world)
-    rl["box_stream_GBs"] = stream_probe(dev, ed.T, D)
 
-    ms = elapsed / args.steps * 1e3
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--also", type=int, nargs="*", default=[], choices=sorted(CONFIGS),
+                    help="further workloads timed in the same run, reported under 'also'")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gemm", default="split", choices=["split", "exact"],
+                    help="operand precision of the D=256 MFMA GEMMs (the other mode is timed too)")
+    ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")
+    ap.add_argument("--fuse-tail-seg", action="store_true",
+                    help="layers 2-3: tail segmented reduction fused into the dS pass (A/B)")
+    ap.add_argument("--recompute-x1", action="store_true",
+                    help="layer-2 backward rebuilds x^1 on chip instead of re-reading it (A/B)")
+    args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    main_out = run_workload(args.config, args, world, rank, dev, args.gemm, not args.no_other_mode)
     result = {
         "metric": "adjacency edges/s per IDDGCN training step (pos fwd + neg fwd + bwd + Adam)",
-        "value": M / (elapsed / args.steps),
+        "value": main_out.pop("value"),
         "unit": "edges/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms,
+        "ms_per_step": main_out.pop("ms_per_step"),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": main_out.pop("scaling"),
         "vs_baseline": None,
-        "dtype": "f32",
-        "gemm_operands": GEMM_NOTE[args.gemm],
+        "dtype": main_out.pop("dtype"),
         "data": "synthetic (seeded mutation-drug graph, reference-distribution random init)",
-        "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
-                   "scored_edges": T, "scored_edges_per_gpu": T_local, "feat_dim": D,
-                   "parallelism": f"edge-dp{world}", "gemm": args.gemm},
-        "scored_edges_per_s": T / (elapsed / args.steps),
-        "loss": loss_val,
-        "kernel_ms_per_step": {k: sum(v) / args.steps for k, v in kt.items()},
-        "roofline": rl,
+        "config": main_out.pop("config"),
     }
-    if other is not None:
-        result["other_gemm_mode"] = other
+    result.update(main_out)
+    also = []
+    for cid in args.also:
+        try:
+            o = run_workload(cid, args, world, rank, dev, args.gemm, False)
+        except torch.OutOfMemoryError as e:      # a secondary workload never costs the headline line
+            torch.cuda.empty_cache()
+            o = {"config": {"workload": CONFIGS[cid]["name"]}, "error": f"out of memory: {e}"[:300]}
+        also.append(o)
+    if also:
+        result["also"] = also
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg)
+        result["cpu_baseline"] = cpu_baseline(CONFIGS[args.config])
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

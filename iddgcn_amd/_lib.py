@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID, ACT_DSIGMOID_COMBINE = 0, 1, 2, 3
 GEMM_EXACT_F32, GEMM_SPLIT_F16 = 0, 1
@@ -57,9 +57,9 @@ SIGNATURES = {
     "iddgcn_alpha_fwd_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp]),
     "iddgcn_combine_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cll, vp]),
     "iddgcn_distmult_blocks": (ci, [cll]),
-    "iddgcn_distmult_bce_f32": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, ci]),
+    "iddgcn_distmult_bce_f32": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci]),
     "iddgcn_distmult_bce_heads_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
-                                           ci]),
+                                           vp, ci]),
     "iddgcn_seg_gather_reduce_f32": (ci, [vp, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iddgcn_tail_seg_reduce_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, cll, vp, cll, vp, vp]),
     "iddgcn_head_bwd_node_f32": (ci, [vp, ci, ci, ci, vp, vp, cll, vp, vp, vp, vp, vp, vp, cll, vp, vp]),

@@ -1852,6 +1852,7 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
                                                        const int* __restrict__ t_idx, const int* __restrict__ r_idx,
                                                        const float* __restrict__ rel, const float* __restrict__ y,
                                                        float scale, float* __restrict__ p_out,
+                                                       float* __restrict__ s_out,
                                                        float* __restrict__ ds_out, float* __restrict__ do_out,
                                                        float* __restrict__ drel_slab, float* __restrict__ loss_slab) {
     constexpr int LPR = D / 4;
@@ -1916,7 +1917,10 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
             const long long e = e0 + u * stride;
             if (e >= T) continue;
             const float p = sigmoidf_(sc[u]);
-            if (p_out && sub == 0) p_out[e] = p;
+            if (sub == 0) {
+                if (p_out) p_out[e] = p;
+                if (s_out) s_out[e] = sc[u];
+            }
             if (!train) continue;
             const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
             const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
@@ -1972,17 +1976,20 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
 // dXh[n] = Xh(1-Xh) * sum ds_e rel[r_e] Xt[e] accumulates in registers in perm order.  Per-edge
 // arithmetic is that of distmult_kernel + seg_gather_reduce_kernel, so p / ds / do / dXh are
 // bitwise the same; only the drel / loss partial sums visit edges in another order.
+// do_out may alias Xt (the engine writes do^3 over x^3): each element is read, then written, by
+// the same lane, and every edge is visited once.
 // ---------------------------------------------------------------------------
 template <int D, int RT>
 __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R, const int* __restrict__ seg_ptr,
                                                              const int* __restrict__ perm,
                                                              const float* __restrict__ Xh,
-                                                             const float* __restrict__ Xt,
+                                                             const float* Xt,    // may alias do_out
                                                              const int* __restrict__ r_idx,
                                                              const float* __restrict__ rel,
                                                              const float* __restrict__ y, float scale,
-                                                             float* __restrict__ p_out, float* __restrict__ ds_out,
-                                                             float* __restrict__ do_out, float* __restrict__ dXh,
+                                                             float* __restrict__ p_out, float* __restrict__ s_out,
+                                                             float* __restrict__ ds_out,
+                                                             float* do_out, float* __restrict__ dXh,
                                                              float* __restrict__ drel_slab,
                                                              float* __restrict__ loss_slab) {
     constexpr int LPR = D / 4;
@@ -2036,7 +2043,10 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
             for (int u = 0; u < U; ++u) {
                 if (e[u] < 0) continue;
                 const float p = sigmoidf_(sc[u]);
-                if (p_out && sub == 0) p_out[e[u]] = p;
+                if (sub == 0) {
+                    if (p_out) p_out[e[u]] = p;
+                    if (s_out) s_out[e[u]] = sc[u];
+                }
                 float g, lterm;
                 if (y) {        // Keras BCE seed
                     const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
@@ -2738,15 +2748,15 @@ int iddgcn_distmult_blocks(long long T) {
 
 int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R, const float* Xh, const int* h_idx,
                             const float* Xt, const int* t_idx, const int* r_idx, const float* rel, const float* y,
-                            float scale, float* p_out, float* ds_out, float* do_out, float* drel_slab,
-                            float* loss_slab, int n_blocks) {
+                            float scale, float* p_out, float* s_out, float* ds_out, float* do_out,
+                            float* drel_slab, float* loss_slab, int n_blocks) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
     if (T < 0 || n_blocks < 1 || !Xh || !h_idx || !Xt || !r_idx || !rel) return IDDGCN_E_BAD_ARG;
     if (y && (!ds_out || !do_out || !drel_slab || !loss_slab)) return IDDGCN_E_BAD_ARG;
     if (T == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-#define DK(DD) hipLaunchKernelGGL(distmult_kernel<DD>, dim3(n_blocks), dim3(256), 0, st, T, R, Xh, h_idx, Xt, t_idx, r_idx, rel, y, scale, p_out, ds_out, do_out, drel_slab, loss_slab)
+#define DK(DD) hipLaunchKernelGGL(distmult_kernel<DD>, dim3(n_blocks), dim3(256), 0, st, T, R, Xh, h_idx, Xt, t_idx, r_idx, rel, y, scale, p_out, s_out, ds_out, do_out, drel_slab, loss_slab)
     switch (d) {
         case 32: DK(32); break;
         case 64: DK(64); break;
@@ -2759,15 +2769,15 @@ int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R, const float
 
 int iddgcn_distmult_bce_heads_f32(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* perm,
                                   const float* Xh, const float* Xt, const int* r_idx, const float* rel,
-                                  const float* y, float scale, float* p_out, float* ds_out, float* do_out,
-                                  float* dXh, float* drel_slab, float* loss_slab, int n_blocks) {
+                                  const float* y, float scale, float* p_out, float* s_out, float* ds_out,
+                                  float* do_out, float* dXh, float* drel_slab, float* loss_slab, int n_blocks) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
     if (n_nodes < 0 || n_blocks < 1 || !seg_ptr || !perm || !Xh || !Xt || !r_idx || !rel || !do_out ||
         !dXh || !drel_slab || !loss_slab)
         return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;
-#define HK(DD, RT) hipLaunchKernelGGL((distmult_heads_kernel<DD, RT>), dim3(n_blocks), dim3(256), 0, st, n_nodes, R, seg_ptr, perm, Xh, Xt, r_idx, rel, y, scale, p_out, ds_out, do_out, dXh, drel_slab, loss_slab)
+#define HK(DD, RT) hipLaunchKernelGGL((distmult_heads_kernel<DD, RT>), dim3(n_blocks), dim3(256), 0, st, n_nodes, R, seg_ptr, perm, Xh, Xt, r_idx, rel, y, scale, p_out, s_out, ds_out, do_out, dXh, drel_slab, loss_slab)
 #define HKR(DD)                                            \
     {                                                      \
         if (R <= 1) HK(DD, 1);                             \

@@ -43,13 +43,20 @@ def param_layout(N, R, D):
 
 
 class FlatParams:
-    """A flat fp32 buffer with named views (parameters or their gradients)."""
+    """A flat fp32 buffer with named views (parameters or their gradients).
+
+    ``buf`` is ``[flat | loss]``: one float past the parameters holds the step's loss sum when the
+    buffer carries gradients, so a data-parallel step all-reduces gradients and loss IN PLACE in
+    one buffer (parallel.BucketedAllReduce), no bucket copies.  E comes first, so ``buf[N*D:]`` (all
+    small gradients + the loss) and row ranges of ``E`` are contiguous buckets."""
 
     def __init__(self, N, R, D, device):
         self.N, self.R, self.D = N, R, D
         self.layout = param_layout(N, R, D)
         total = sum(int(np.prod(s)) for _, s, _ in self.layout)
-        self.flat = torch.zeros(total, dtype=torch.float32, device=device)
+        self.buf = torch.zeros(total + 1, dtype=torch.float32, device=device)
+        self.flat = self.buf[:total]
+        self.loss = self.buf[total:]
         self.views, off = {}, 0
         self.n_sparse = 0
         for name, shape, sparse in self.layout:
@@ -125,6 +132,7 @@ class GraphedTrainStep:
         self.losses = torch.zeros(max(n_steps, 1), dtype=torch.float32, device=dev)
         self.done = 0
         ws = eng.workspace(ed.T, True)
+        self.ws = ws        # the captured pointers live as long as the graph (Engine may evict its copy)
 
         def body():
             eng._t_global = t_global
@@ -132,7 +140,7 @@ class GraphedTrainStep:
                 eng.forward(params, adj, ed, ws, True)
                 eng.backward(params, grads, adj, ed, ws)
             opt.apply_table(params, grads, self.alpha, self.step)
-            ops.step_advance(self.step, self.losses, ws.loss)
+            ops.step_advance(self.step, self.losses, grads.loss)
 
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
@@ -150,7 +158,13 @@ class GraphedTrainStep:
 
 
 class Workspace:
-    """Every device buffer one step needs, sized for (N, R, D, T)."""
+    """Every device buffer one step needs, sized for (N, R, D, T).
+
+    Edge tables: only the three tail activations x^1..x^3 (T x D each).  The backward writes the
+    edge-level gradients over them in place: DistMult writes do^3 over x^3, and the layer-l backward
+    GEMM writes do^{l-1} = (do^l S^T) * x^{l-1}(1 - x^{l-1}) over its own sigma' operand x^{l-1}
+    (each element is read before it is written, by the same lanes).  3 T x D tables instead of 5:
+    123 GB instead of 205 GB at config 4 (T = 40M, D = 256)."""
 
     def __init__(self, N, R, D, T, device, train=True):
         f = dict(dtype=torch.float32, device=device)
@@ -165,15 +179,14 @@ class Workspace:
         self.X = e(NUM_LAYERS, N, D)            # head chain X^1..X^3
         self.Ssm = e(NUM_LAYERS, N, R)
         self.W = e(NUM_LAYERS, N, R)
-        self.xt = e(NUM_LAYERS, T, D)           # tail chain x^1..x^3
+        self.xt = e(NUM_LAYERS, T, D)           # tail chain x^1..x^3 (then, training, do^3..do^1)
         self.Wedge = e(NUM_LAYERS, T, R)        # W^l[h_e]: per-edge copy of the dynamic weights
         self.p = e(T)
+        self.s = e(T)                           # pre-sigmoid DistMult logits (IDDGCN.py:108)
         self.nb_dm = ops.distmult_blocks(T)
         self.train = train
         if not train:
             return
-        self.dE_a = e(T, D)                     # edge-level grads, ping-pong
-        self.dE_b = e(T, D)
         self.dWedge = e(T, R)
         self.dOn_a = e(N, D)                    # node-level grads, ping-pong
         self.dOn_b = e(N, D)
@@ -184,7 +197,6 @@ class Workspace:
         self.WaT = e(R, D)
         self.drel_slab = e(self.nb_dm * R * D)
         self.loss_slab = e(self.nb_dm)
-        self.loss = e(1)
         tn = max(ops.tn_blocks(T, D), ops.tn_blocks(N, D))
         self.tn_slab = e(tn * D * D)
         self.narrow_slab = e((ops.tn_narrow_blocks(N) + 1) * (D + 1) * R)
@@ -298,22 +310,28 @@ class Engine:
                 scale, y = 1.0 / (float(self._t_global or T) * float(N)), ed.y
             else:                              # d(scale * sum_e p_e): the explainers' seed
                 scale, y = float(self._pred_seed), None
-            ops.distmult_bce_heads(ed.hptr, ed.hperm, ws.X[2], ws.xt[2], ed.r, P["rel"], y, ws.dE_a, ws.dOn_a,
-                                   ws.drel_slab, ws.loss_slab, scale=scale, p_out=ws.p if self._want_p else None)
+            # do^3 is written over x^3 in place (each edge row is read, then written, by the same lanes)
+            ops.distmult_bce_heads(ed.hptr, ed.hperm, ws.X[2], ws.xt[2], ed.r, P["rel"], y, ws.xt[2], ws.dOn_a,
+                                   ws.drel_slab, ws.loss_slab, scale=scale, p_out=ws.p if self._want_p else None,
+                                   s_out=ws.s if self._want_p else None)
         else:
-            ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], p_out=ws.p)
+            ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], p_out=ws.p, s_out=ws.s)
 
     _t_global = None
     _want_p = False        # per-edge probabilities are only materialised for loss_and_grads
     _pred_seed = None      # None: BCE seed; a float: gradient of pred_seed * sum_e p_e
 
     # -- backward -----------------------------------------------------------
-    def backward(self, P, G, adj, ed, ws):
+    def backward(self, P, G, adj, ed, ws, comm=None):
+        """Gradients of the step into G (and the loss sum into G.loss).  ``comm`` (data parallel,
+        parallel.BucketedAllReduce) gets each contiguous piece of G.buf as soon as it is final: all
+        small gradients + the loss after the layer loop, then row chunks of dE as the transposed SpMM
+        produces them, so the all-reduce of the large dE overlaps the SpMM of the next chunk."""
         N, R, D = self.N, self.R, self.D
         dOn, dOn_next = ws.dOn_a, ws.dOn_b      # head seed dO^3, written by distmult_bce_heads
-        do, do_next = ws.dE_a, ws.dE_b          # tail seed do^3, written by distmult_bce_heads
         for l in (2, 1, 0):                     # layer index l -> reference layer l+1
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
+            do = ws.xt[l]                       # do^{l+1}, written over x^{l+1}
             # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part; for layers 2-3 the
             # fused kernel does it inside the dS pass (do read once)
             seg = self._tn_seg(ed) if l > 0 else None
@@ -321,7 +339,7 @@ class Engine:
                 ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
                                     dsum=ws.dES if l == 0 else None)
             if l > 0:
-                # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x)
+                # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x), written over x^{l}
                 with self._mark("tail_dS_tn"):
                     if seg is not None:
                         ops.gemm_tn_seg(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, seg[0], ed.t, ws.Wedge[l], Pl,
@@ -332,10 +350,11 @@ class Engine:
                 with self._mark("tail_bwd_rec_gemm" if rec else "tail_bwd_gemm"):
                     if rec:
                         # x^1 = sigmoid(ES1[t] + sum_r W^1[h,r] P^1_r[t]) rebuilt on chip (forward, above)
-                        ops.rowgemm(do, Sl, do_next, b_trans=True, act=L.ACT_DSIGMOID_COMBINE, coef=ws.Wedge[0],
-                                    V=ws.EP1, v_idx=ed.t, v_rel_stride=N * D, v_runs_max=ed.tail_runs32)
+                        ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID_COMBINE,
+                                    coef=ws.Wedge[0], V=ws.EP1, v_idx=ed.t, v_rel_stride=N * D,
+                                    v_runs_max=ed.tail_runs32)
                     else:
-                        ops.rowgemm(do, Sl, do_next, b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1])
+                        ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1])
             # head side (node level)
             ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
                               dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)
@@ -358,13 +377,19 @@ class Engine:
             ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2)))
                                  for r in range(R)])
             dOn, dOn_next = dOn_next, dOn
-            do, do_next = do_next, do
-        # dE += sum_r A_r^T dAE_r  (gradient through all_e -> sparse_dense_matmul)
-        ops.spmm_csr(adj.bwd_ptr, adj.bwd_col, adj.bwd_val, ws.dAE.view(R * N, D), G["E"].view(1, N, D), 1, N,
-                     accumulate=True)
-        # DistMult rel grad and the loss
+        # DistMult rel grad and the loss: every gradient past E is final now
         ops.reduce_slabs(ws.drel_slab, ws.nb_dm, G["rel"])
-        ops.reduce_slabs(ws.loss_slab, ws.nb_dm, ws.loss)
+        ops.reduce_slabs(ws.loss_slab, ws.nb_dm, G.loss)
+        if comm is not None:
+            comm.ready(G.buf[N * D:])
+        # dE += sum_r A_r^T dAE_r  (gradient through all_e -> sparse_dense_matmul); per-row sums, so a
+        # row-chunked launch sequence is bitwise the single launch
+        chunks = comm.row_chunks(N) if comm is not None else [(0, N)]
+        for n0, n1 in chunks:
+            ops.spmm_csr(adj.bwd_ptr[n0:n1 + 1], adj.bwd_col, adj.bwd_val, ws.dAE.view(R * N, D),
+                         G["E"][n0:n1].view(1, n1 - n0, D), 1, n1 - n0, accumulate=True)
+            if comm is not None:
+                comm.ready(G["E"][n0:n1].reshape(-1))
 
     def _tn_seg(self, ed):
         """(row_beg, max tile runs) when the fused dS + tail segmented reduction applies: D=256 in the
@@ -380,26 +405,41 @@ class Engine:
         return self.recompute_x1 and self.D == 256 and 1 <= ed.tail_runs32 <= 8
 
     # -- public steps ---------------------------------------------------------
-    def train_step(self, params, grads, opt, adj, ed, t_global=None, allreduce=None):
-        """One full-batch step (IDDGCN.py:123-178).  Returns the device scalar
-        sum of per-edge BCE terms of this rank (divide by T for the mean)."""
+    def train_step(self, params, grads, opt, adj, ed, t_global=None, comm=None):
+        """One full-batch step (IDDGCN.py:123-178).  Returns the device scalar (grads.loss) holding the
+        sum of per-edge BCE terms (divide by the global T for the mean).  ``comm``: the data-parallel
+        all-reduce (parallel.BucketedAllReduce), overlapped with the end of the backward."""
         ws = self.workspace(ed.T, True)
         self._t_global = t_global
         with self._precision():
             self.forward(params, adj, ed, ws, True)
-            self.backward(params, grads, adj, ed, ws)
-        if allreduce is not None:
-            allreduce(grads.flat, ws.loss)
+            self.backward(params, grads, adj, ed, ws, comm)
+        if comm is not None:
+            comm.finish()
         opt.apply(params, grads)
-        return ws.loss
+        return grads.loss
 
-    def predict(self, params, adj, ed):
+    def predict(self, params, adj, ed, logits=False):
+        """Probabilities p = sigmoid(s) of the scored edges (caller's order); with ``logits=True``
+        also the pre-sigmoid DistMult scores s (IDDGCN.py:108)."""
         ws = self.workspace(ed.T, False)
         with self._precision():
             self.forward(params, adj, ed, ws, False)
-        return ed.unsort(ws.p)
+        return (ed.unsort(ws.p), ed.unsort(ws.s)) if logits else ed.unsort(ws.p)
 
-    def loss_and_grads(self, params, grads, adj, ed, t_global=None):
+    def layer_outputs(self, ed, rows=None):
+        """After a predict() forward: the per-edge layer outputs (x_h^l, x_t^l), l = 1..3, of the
+        reference's IDDGCN_Layer calls (IDDGCN.py:238-274), in the caller's edge order (optionally only
+        the caller rows ``rows``): the head chain gathered from the node table X^l, the tail chain
+        un-permuted from the tail-sorted edge table x^l."""
+        ws = self.workspace(ed.T, False)
+        inv = ed.inv if rows is None else ed.inv[torch.as_tensor(rows, device=ed.inv.device)]
+        heads = ed.h.long()[inv]
+        return [(ws.X[l][heads], ws.xt[l][inv]) for l in range(NUM_LAYERS)]
+
+    def loss_and_grads(self, params, grads, adj, ed, t_global=None, logits=False):
+        """Forward + backward without the optimizer step: (loss sum, p) or, with ``logits=True``,
+        (loss sum, p, s) — s the pre-sigmoid DistMult scores — all per edge in the caller's order."""
         ws = self.workspace(ed.T, True)
         self._t_global = t_global
         self._want_p = True
@@ -410,7 +450,9 @@ class Engine:
             self._want_p = False
         with self._precision():
             self.backward(params, grads, adj, ed, ws)
-        return ws.loss, ed.unsort(ws.p)
+        if logits:
+            return grads.loss, ed.unsort(ws.p), ed.unsort(ws.s)
+        return grads.loss, ed.unsort(ws.p)
 
 
     def value_grads(self, params, adj, ed, scale=1.0, grads=None):

@@ -24,7 +24,7 @@ from . import _lib as L
 from . import ops
 from .engine import NUM_LAYERS, Engine, FlatParams, GraphedTrainStep, KerasAdam
 from .graph import DeviceAdjacency, SparseAdj, get_adj_mats  # noqa: F401  (re-export)
-from .parallel import GradAllReduce, shard_triples, world
+from .parallel import BucketedAllReduce, shard_triples, world
 
 LAYER_WEIGHT_NAMES = ("relation_kernels", "self_kernel", "relation_weights", "W_alpha", "b_alpha")
 
@@ -143,7 +143,7 @@ class IDDGCN_Layer(Layer):
         head_e (B,D), tail_idx (B,), tail_e (B,D), adj_mats] with GPU float32 tensors.
         Returns (sigmoid(head_out), sigmoid(tail_out)), each (B, D)."""
         embeddings, head_idx, head_e, tail_idx, tail_e, *adj = inputs
-        adj = adj[0] if len(adj) == 1 and isinstance(adj[0], (list, tuple)) else adj
+        adj = _unwrap_adj(adj)
         dev = embeddings.device
         N, D, R = self.num_entities, self.output_dim, self.num_relations
         K, S, _, Wa, ba = [torch.as_tensor(w, device=dev) for w in self._weights]
@@ -182,7 +182,8 @@ class DistMult(Layer):
         rng = np.random.default_rng(self.seed)
         self._weights = [rng.standard_normal((self.num_relations, embedding_dim)).astype(np.float32)]
 
-    def __call__(self, inputs):
+    def __call__(self, inputs, logits=False):
+        """sigmoid(sum head_e * rel[rel_idx] * tail_e) as (1, B); ``logits=True``: the sum itself."""
         head_e, rel_idx, tail_e = inputs
         dev = head_e.device
         if not self._weights:
@@ -194,13 +195,22 @@ class DistMult(Layer):
             raise L.IddgcnError("relation index out of range")
         ident = torch.arange(B, device=dev, dtype=torch.int32)
         p = torch.empty(B, device=dev)
-        ops.distmult_bce(head_e.contiguous(), ident, tail_e.contiguous(), ri, rel, p_out=p)
-        return p.view(1, B)
+        s = torch.empty(B, device=dev) if logits else None
+        ops.distmult_bce(head_e.contiguous(), ident, tail_e.contiguous(), ri, rel, p_out=p, s_out=s)
+        return (s if logits else p).view(1, B)
 
 
 # ---------------------------------------------------------------------------
 # model
 # ---------------------------------------------------------------------------
+def _unwrap_adj(adj):
+    """The trailing inputs after (all, h, r, t) or (E, h, h_e, t, t_e): one DeviceAdjacency, one
+    nested list/tuple of sparse matrices, or the matrices spliced in."""
+    if len(adj) == 1 and isinstance(adj[0], (list, tuple, DeviceAdjacency)):
+        return adj[0]
+    return adj
+
+
 def _squeeze_idx(a):
     if isinstance(a, torch.Tensor):
         a = a.cpu().numpy()
@@ -303,12 +313,14 @@ class IDDGCN_Model:
     def _adjacency(self, adj_mats):
         if isinstance(adj_mats, DeviceAdjacency):       # get_adj_mats(..., device=cuda)
             return adj_mats
-        key = id(adj_mats)
+        # key on the caller's objects (the list itself, or the tuple of its relation matrices when the
+        # list was spliced into x): rebuilt only when the caller hands over a different graph
+        key = tuple(id(a) for a in adj_mats)
         hit = self._graph_cache.get(key)
-        if hit is not None and hit[0] is adj_mats:
+        if hit is not None and all(a is b for a, b in zip(hit[0], adj_mats)):
             return hit[1]
-        dadj = DeviceAdjacency(adj_mats, self.num_entities, self._dev)
-        self._graph_cache = {key: (adj_mats, dadj)}
+        dadj = DeviceAdjacency(list(adj_mats), self.num_entities, self._dev)
+        self._graph_cache = {key: (list(adj_mats), dadj)}
         return dadj
 
     def save_weights(self, filepath):
@@ -329,9 +341,13 @@ class IDDGCN_Model:
 
     # -- calls ---------------------------------------------------------------
     def _unpack(self, x):
+        """x = [ALL_INDICES, h, r, t, ADJ_MATS] (IDDGCN.py:399-407).  ADJ_MATS may be the reference's
+        list of per-relation sparse matrices, spliced in or nested, or one DeviceAdjacency
+        (get_adj_mats(..., device=cuda)).  The adjacency object is returned as the caller passed it, so
+        the graph cache (keyed on it) hits across fit/predict calls."""
         all_idx, h, r, t, *adj = x
-        adj = adj[0] if len(adj) == 1 and isinstance(adj[0], (list, tuple)) else adj
-        return _squeeze_idx(h), _squeeze_idx(r), _squeeze_idx(t), list(adj)
+        adj = _unwrap_adj(adj)
+        return _squeeze_idx(h), _squeeze_idx(r), _squeeze_idx(t), adj
 
     def predict(self, x, batch_size=None, verbose=0, **kwargs):
         """model.predict (IDDGCN_eval.py:61-69,97-105): returns (1, B) probabilities."""
@@ -341,6 +357,16 @@ class IDDGCN_Model:
         ed = eng.edges(np.stack([h, r, t], 1))
         p = eng.predict(self._params, dadj, ed)
         return p.detach().cpu().numpy().reshape(1, -1)
+
+    def predict_logits(self, x):
+        """The pre-sigmoid DistMult scores of model.predict's edges, (1, B): the argument of the sigmoid
+        at IDDGCN.py:108 (what the reference's y_pred is the sigmoid of)."""
+        eng = self._device_state()
+        h, r, t, adj = self._unpack(x)
+        dadj = self._adjacency(adj)
+        ed = eng.edges(np.stack([h, r, t], 1))
+        _, s = eng.predict(self._params, dadj, ed, logits=True)
+        return s.detach().cpu().numpy().reshape(1, -1)
 
     def __call__(self, x, training=False):
         return torch.as_tensor(self.predict(x))
@@ -373,7 +399,7 @@ class IDDGCN_Model:
         if self._opt_state is None:
             o = self.optimizer
             self._opt_state = KerasAdam(self._params, o.learning_rate, o.beta_1, o.beta_2, o.epsilon)
-        allreduce = GradAllReduce(self._grads.flat) if ws > 1 else None
+        comm = BucketedAllReduce() if ws > 1 else None
         history = History()
         cbs = [history] + list(callbacks or [])
         for cb in cbs:
@@ -392,7 +418,7 @@ class IDDGCN_Model:
                 loss_sum = graphed.replay()
             else:
                 loss_sum = eng.train_step(self._params, self._grads, self._opt_state, dadj, ed, t_global=T,
-                                          allreduce=allreduce)
+                                          comm=comm)
             if lazy:
                 pending.append(loss_sum if graphed is not None else loss_sum.clone())
                 continue

@@ -3,8 +3,13 @@
 torch is used only as the device-memory / stream provider: every wrapper takes
 CUDA(HIP) tensors, validates shapes/dtypes on the host (so a bad shape never
 reaches a kernel), and passes raw pointers plus torch's current stream.
+Index VALUES (entity / relation ids) are validated where they enter the
+product path — graph.get_adj_mats / DeviceAdjacency / ScoredEdges (host or
+device build, error flag) and the layer-level calls in model.py; direct callers
+of these wrappers can turn on per-call range checks with IDDGCN_CHECK_INDICES=1.
 """
 import ctypes
+import os
 
 import torch
 
@@ -35,10 +40,22 @@ def _req(t, dtype, shape=None, name="tensor"):
         raise L.IddgcnError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
 
 
+# Index RANGES are checked here only when IDDGCN_CHECK_INDICES=1 (one device reduction + host sync per
+# index array, a debug mode): the product path's indices come from graph.ScoredEdges / DeviceAdjacency,
+# whose builders validate every entity / relation id on the host or in the device build (error flag).
+CHECK_INDEX_RANGES = os.environ.get("IDDGCN_CHECK_INDICES", "0") == "1"
+
+
 def _idx_ok(idx, n_rows, bound, name):
+    """dtype / shape / contiguity of an int32 index array; with CHECK_INDEX_RANGES (or always for a
+    CPU-resident check-free size-0 array) also 0 <= idx < bound."""
     if idx is None:
         return
     _req(idx, _I32, (n_rows,), name)
+    if CHECK_INDEX_RANGES and bound is not None and idx.numel():
+        lo, hi = int(idx.min()), int(idx.max())
+        if lo < 0 or hi >= int(bound):
+            raise L.IddgcnError(f"{name}: index out of range [0, {int(bound)}): min {lo}, max {hi}")
 
 
 def spmm_csr(row_ptr, col, vals, X, Y, n_seg, n_rows, accumulate=False):
@@ -99,7 +116,9 @@ def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=
         _req(coef, _F32, None, "coef")
         _req(V, _F32, None, "V")
         _idx_ok(coef_idx, M, coef.shape[0], "coef_idx")
-        _idx_ok(v_idx, M, None, "v_idx")
+        vrows = (int(v_rel_stride) // int(D if v_row_stride is None else v_row_stride)
+                 if (v_row_stride is None or v_row_stride) and v_rel_stride else None)
+        _idx_ok(v_idx, M, vrows, "v_idx")
     if act == L.ACT_DSIGMOID:
         _req(aux, _F32, (M, D), "aux")
     if act == L.ACT_DSIGMOID_COMBINE:
@@ -196,9 +215,10 @@ def combine(Y, coef, V, out, *, y_idx=None, coef_idx=None, v_idx=None, v_rel_str
     _req(coef, _F32, None, "coef")
     _req(V, _F32, None, "V")
     _req(out, _F32, (M, D), "out")
-    for n, ix in (("y_idx", y_idx), ("coef_idx", coef_idx), ("v_idx", v_idx)):
-        _idx_ok(ix, M, None, n)
     vrs = V.shape[1] * D if v_rel_stride is None else v_rel_stride
+    for n, ix, bound in (("y_idx", y_idx, Y.shape[0]), ("coef_idx", coef_idx, coef.shape[0]),
+                         ("v_idx", v_idx, int(vrs) // D)):
+        _idx_ok(ix, M, bound, n)
     L.check(L.lib().iddgcn_combine_f32(_stream(), M, D, R, _ptr(Y), _ptr(y_idx), _ptr(coef), _ptr(coef_idx),
                                        _ptr(V), _ptr(v_idx), int(vrs), _ptr(out)), "combine")
 
@@ -207,8 +227,10 @@ def distmult_blocks(T):
     return int(L.lib().iddgcn_distmult_blocks(int(T)))
 
 
-def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_out=None, ds_out=None,
+def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_out=None, s_out=None, ds_out=None,
                  do_out=None, drel_slab=None, loss_slab=None):
+    """DistMult score (IDDGCN.py:103-109): p_out = sigmoid(s), s_out = s (the pre-sigmoid logit); with y the
+    Keras BCE and both backward seeds."""
     T = h_idx.shape[0]
     R, D = rel.shape
     _req(h_idx, _I32, (T,), "h_idx")
@@ -218,6 +240,12 @@ def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_
     _req(rel, _F32, (R, D), "rel")
     _req(y, _F32, (T,), "y")
     _req(p_out, _F32, (T,), "p_out")
+    _req(s_out, _F32, (T,), "s_out")
+    _idx_ok(h_idx, T, Xh.shape[0], "h_idx")
+    _idx_ok(t_idx, T, Xt.shape[0], "t_idx")
+    _idx_ok(r_idx, T, R, "r_idx")
+    if t_idx is None and Xt.shape[0] < T:
+        raise L.IddgcnError("distmult: Xt has fewer rows than scored edges")
     nb = distmult_blocks(T)
     if y is not None:
         _req(ds_out, _F32, (T,), "ds_out")
@@ -226,13 +254,14 @@ def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_
             raise L.IddgcnError("distmult slabs too small")
     L.check(L.lib().iddgcn_distmult_bce_f32(_stream(), T, D, R, _ptr(Xh), _ptr(h_idx), _ptr(Xt), _ptr(t_idx),
                                             _ptr(r_idx), _ptr(rel), _ptr(y), float(scale), _ptr(p_out),
-                                            _ptr(ds_out), _ptr(do_out), _ptr(drel_slab), _ptr(loss_slab), nb),
+                                            _ptr(s_out), _ptr(ds_out), _ptr(do_out), _ptr(drel_slab), _ptr(loss_slab),
+                                            nb),
             "distmult_bce")
     return nb
 
 
 def distmult_bce_heads(seg_ptr, perm, Xh, Xt, r_idx, rel, y, do_out, dXh, drel_slab, loss_slab, *, scale=1.0,
-                      p_out=None, ds_out=None):
+                      p_out=None, s_out=None, ds_out=None):
     """Training DistMult + BCE + tail seed (do_out) + head seed (dXh) in one pass over head segments.
     y=None selects the prediction seed (gradient of scale * sum_e p_e; loss slabs sum p_e)."""
     T = r_idx.shape[0]
@@ -248,13 +277,14 @@ def distmult_bce_heads(seg_ptr, perm, Xh, Xt, r_idx, rel, y, do_out, dXh, drel_s
     _req(do_out, _F32, (T, D), "do_out")
     _req(dXh, _F32, (n_nodes, D), "dXh")
     _req(p_out, _F32, (T,), "p_out")
+    _req(s_out, _F32, (T,), "s_out")
     _req(ds_out, _F32, (T,), "ds_out")
     nb = distmult_blocks(T)
     if drel_slab.numel() < nb * R * D or loss_slab.numel() < nb:
         raise L.IddgcnError("distmult slabs too small")
     L.check(L.lib().iddgcn_distmult_bce_heads_f32(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(perm), _ptr(Xh),
                                                   _ptr(Xt), _ptr(r_idx), _ptr(rel), _ptr(y), float(scale),
-                                                  _ptr(p_out), _ptr(ds_out), _ptr(do_out), _ptr(dXh),
+                                                  _ptr(p_out), _ptr(s_out), _ptr(ds_out), _ptr(do_out), _ptr(dXh),
                                                   _ptr(drel_slab), _ptr(loss_slab), nb), "distmult_bce_heads")
     return nb
 

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 2
+#define IDDGCN_ABI_VERSION 3
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -68,7 +68,8 @@ int iddgcn_sddmm_csr_f32(void* stream, int n_seg, int n_rows, int d,
  *   v += accumulate ? C[e][c] : 0
  *   v += sum_{r<R} coef[(coef_idx ? coef_idx[e] : e)*R + r]
  *                  * V[r*v_rel_stride + (v_idx ? v_idx[e] : e)*v_row_stride + c]
- *   C[e][c] = act(v)   (NONE | SIGMOID | DSIGMOID with aux[e][c])
+ *   C[e][c] = act(v)   (NONE | SIGMOID | DSIGMOID with aux[e][c]; C may alias aux: the backward
+ *                       writes do^{l-1} over its sigma' operand x^{l-1})
  * Replaces IDDGCN.py:62-63 + 71-79 (x·S, + sigmoid(alpha_r)·(AE_r[idx]·K_r), sigmoid)
  * with P_r = AE_r·K_r precomputed at node level, and the matching backward GEMMs. */
 typedef struct {
@@ -147,7 +148,8 @@ int iddgcn_combine_f32(void* stream, int M, int d, int R,
 /* DistMult decoder (IDDGCN.py:103-109) fused with Keras BCE (IDDGCN.py:161-168)
  * and the seed of the backward.  For each scored edge e:
  *   a = Xh[h_idx[e]], b = Xt[t_idx ? t_idx[e] : e], rho = rel[r_idx[e]]
- *   p = sigmoid(sum a*rho*b)                    -> p_out[e] (if p_out)
+ *   s = sum a*rho*b                             -> s_out[e] (if s_out; the pre-sigmoid logit, IDDGCN.py:108)
+ *   p = sigmoid(s)                              -> p_out[e] (if p_out)
  * If y != NULL (training):
  *   loss_e = -(y log(clip(p)+eps) + (1-y) log(1-clip(p)+eps)), eps = 1e-7
  *   g = scale * dloss_e/dp (0 where p is clipped), ds = g p (1-p)
@@ -158,18 +160,19 @@ int iddgcn_distmult_blocks(long long T);
 int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R,
                             const float* Xh, const int* h_idx, const float* Xt, const int* t_idx,
                             const int* r_idx, const float* rel, const float* y, float scale,
-                            float* p_out, float* ds_out, float* do_out,
+                            float* p_out, float* s_out, float* ds_out, float* do_out,
                             float* drel_slab, float* loss_slab, int n_blocks);
 
 /* Training form of the above that also produces the head-side seed, in ONE pass over the
  * scored edges grouped by head (seg_ptr/perm: head segments, perm in edge order within a head):
  * for head node n and e = perm[k], k in [seg_ptr[n], seg_ptr[n+1]), with a = Xh[n], b = Xt[e]:
- * p_out / ds_out (both optional), do_out, drel_slab and loss_slab exactly as
+ * p_out / s_out / ds_out (all optional), do_out, drel_slab and loss_slab exactly as
  * iddgcn_distmult_bce_f32 (t_idx = NULL), and
  *   dXh[n][c] = a(1-a) * sum_k (b[c]*ds_e)*rel[r_idx[e]][c]     (summed in perm order)
  * which is iddgcn_seg_gather_reduce_f32(seg_ptr, perm, ds, r_idx, rel, Xt, Xh).  Rows of nodes with
  * no edge get zeros.  n_blocks from iddgcn_distmult_blocks(); the drel / loss partials are
  * per block, as for iddgcn_distmult_bce_f32.
+ * do_out may alias Xt (do^3 written over x^3 in place).
  * y == NULL selects the PREDICTION seed: g = scale for every edge (the gradient of
  * scale * sum_e p_e, no clipping) and loss_slab accumulates sum_e p_e — the seed of the
  * explainers' tape.gradient(pred, ...) (explanation/explaiNE.py:85-94).
@@ -178,8 +181,8 @@ int iddgcn_distmult_bce_f32(void* stream, long long T, int d, int R,
 int iddgcn_distmult_bce_heads_f32(void* stream, int n_nodes, int d, int R, const int* seg_ptr,
                                   const int* perm, const float* Xh, const float* Xt, const int* r_idx,
                                   const float* rel, const float* y, float scale, float* p_out,
-                                  float* ds_out, float* do_out, float* dXh, float* drel_slab,
-                                  float* loss_slab, int n_blocks);
+                                  float* s_out, float* ds_out, float* do_out, float* dXh,
+                                  float* drel_slab, float* loss_slab, int n_blocks);
 
 /* Deterministic segmented gather-reduce (replaces the UnsortedSegmentSum of
  * embedding_lookup's gradient): for node n,

@@ -56,13 +56,20 @@ def adj_to_torch(adj_coo, num_entities, dtype=torch.float64):
     return mats
 
 
-def layer_call(E, head_idx, head_e, tail_idx, tail_e, adj, K, S, Wa, ba):
-    """IDDGCN.py:60-79, op for op."""
+def layer_call(E, head_idx, head_e, tail_idx, tail_e, adj, K, S, Wa, ba, ae_cache=None):
+    """IDDGCN.py:60-79, op for op.  ``ae_cache`` (a dict) keeps A_r·E across the calls of one forward:
+    the reference recomputes it in every layer from the same E (:243,256,269), so the cached value is
+    the identical tensor (a plain common-subexpression reuse for large-graph tests)."""
     head_output = head_e @ S                                     # :62
     tail_output = tail_e @ S                                     # :63
     alpha = torch.softmax(head_e @ Wa + ba, dim=-1)              # :66
     for i in range(K.shape[0]):                                  # :68
-        sum_embeddings = torch.sparse.mm(adj[i], E)              # :69-70
+        if ae_cache is not None and i in ae_cache:
+            sum_embeddings = ae_cache[i]
+        else:
+            sum_embeddings = torch.sparse.mm(adj[i], E)          # :69-70
+            if ae_cache is not None:
+                ae_cache[i] = sum_embeddings
         head_update = sum_embeddings[head_idx]                   # :71
         tail_update = sum_embeddings[tail_idx]                   # :72
         relation_weight = torch.sigmoid(alpha[:, i])             # :75
@@ -71,8 +78,9 @@ def layer_call(E, head_idx, head_e, tail_idx, tail_e, adj, K, S, Wa, ba):
     return torch.sigmoid(head_output), torch.sigmoid(tail_output)  # :79
 
 
-def model_forward(P, heads, rels, tails, adj, return_layers=False):
-    """get_IDDGCN_Model wiring (IDDGCN.py:226-275) + DistMult (:103-109)."""
+def model_forward(P, heads, rels, tails, adj, return_layers=False, return_logits=False, ae_cache=None):
+    """get_IDDGCN_Model wiring (IDDGCN.py:226-275) + DistMult (:103-109).  Returns the probabilities
+    [, the per-layer (x_h, x_t) outputs] [, the pre-sigmoid DistMult logits (:108, inside the sigmoid)]."""
     E = P["E"]
     h = torch.as_tensor(heads, dtype=torch.int64)
     r = torch.as_tensor(rels, dtype=torch.int64)
@@ -80,11 +88,13 @@ def model_forward(P, heads, rels, tails, adj, return_layers=False):
     xh, xt = E[h], E[t]                                          # :226-235
     layers = []
     for l in (1, 2, 3):                                          # :238-274 (all_e = E feeds every layer)
-        xh, xt = layer_call(E, h, xh, t, xt, adj, P[f"K{l}"], P[f"S{l}"], P[f"Wa{l}"], P[f"ba{l}"])
+        xh, xt = layer_call(E, h, xh, t, xt, adj, P[f"K{l}"], P[f"S{l}"], P[f"Wa{l}"], P[f"ba{l}"], ae_cache)
         layers.append((xh, xt))
     rel_e = P["rel"][r]                                          # :106
-    score = torch.sigmoid(torch.sum(xh * rel_e * xt, dim=-1))    # :108
-    return (score, layers) if return_layers else score
+    logit = torch.sum(xh * rel_e * xt, dim=-1)                   # :108 (argument of the sigmoid)
+    score = torch.sigmoid(logit)                                 # :108
+    out = (score,) + ((layers,) if return_layers else ()) + ((logit,) if return_logits else ())
+    return out if len(out) > 1 else score
 
 
 def keras_bce(y_true, y_pred):
@@ -169,13 +179,30 @@ class KerasAdam:
         return out
 
 
-def predict(params, triples, adj_coo, num_entities, dtype=torch.float64):
-    """model.predict (IDDGCN_eval.py:97-105): forward only, returns (B,)."""
+def predict(params, triples, adj_coo, num_entities, dtype=torch.float64, logits=False):
+    """model.predict (IDDGCN_eval.py:97-105): forward only, returns the (B,) probabilities, or with
+    ``logits=True`` (probabilities, pre-sigmoid DistMult scores)."""
     P = to_torch_params(params, dtype, requires_grad=False)
     adj = adj_to_torch(adj_coo, num_entities, dtype)
     tr = np.asarray(triples).astype(np.int64)
     with torch.no_grad():
+        if logits:
+            p, s = model_forward(P, tr[:, 0], tr[:, 1], tr[:, 2], adj, return_logits=True)
+            return p.numpy(), s.numpy()
         return model_forward(P, tr[:, 0], tr[:, 1], tr[:, 2], adj).numpy()
+
+
+def forward_detail(params, triples, adj_coo, num_entities, dtype=torch.float64):
+    """The forward of IDDGCN.py:226-275 on `triples` with everything a parity test compares: the
+    probabilities, the pre-sigmoid DistMult logits and the per-layer outputs [(x_h^l, x_t^l)], l=1..3,
+    as numpy arrays.  Cost O(len(triples)) plus one SpMM per relation per layer."""
+    P = to_torch_params(params, dtype, requires_grad=False)
+    adj = adj_to_torch(adj_coo, num_entities, dtype)
+    tr = np.asarray(triples).astype(np.int64)
+    with torch.no_grad():
+        p, layers, s = model_forward(P, tr[:, 0], tr[:, 1], tr[:, 2], adj, return_layers=True, return_logits=True,
+                                     ae_cache={})
+    return p.numpy(), s.numpy(), [(a.numpy(), b.numpy()) for a, b in layers]
 
 
 def eval_metrics(y_true, y_prob, threshold=0.5):

@@ -8,12 +8,16 @@ Fixtures (all data, no code):
   fold{k}_data.npz   bundled fold files of the reference, as int arrays:
                      X_train (mode0_fold{k}_X_train.csv), X_test, neg_X_test,
                      X_train_neg (mode0_fold{k}_X_train_neg.npy, squeezed)
-  fold{k}_eval.npz   oracle float64 eval probabilities on the bundled weights
-                     (IDDGCN_eval.py:49-122 with fold=k), labels, AUC/AUPR
+  fold{k}_eval.npz   oracle float64 eval probabilities and pre-sigmoid DistMult
+                     logits on the bundled weights (IDDGCN_eval.py:49-122 with
+                     fold=k; the same in float32 as probs32 / logits32, the
+                     fp32 drift the parity bars are stated against), labels,
+                     AUC/AUPR
   fold0_step.npz     one full train step on fold 0 from the bundled weights:
-                     loss, scores, all parameter gradients (float64 autograd
-                     of the reference op graph), params after one Keras Adam
-                     step, layer outputs for the first 256 scored edges
+                     loss, scores, logits (float64 and float32), all parameter
+                     gradients (float64 autograd of the reference op graph),
+                     params after one Keras Adam step, layer outputs for the
+                     first 256 scored edges (float64; float32 as layer*_32)
   synth_small.npz    a small synthetic graph (N=512, D=32, R=2) with the same
                      quantities at a non-saturating init
 """
@@ -27,8 +31,8 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
 
-from oracle.ref_model import (KerasAdam, adj_to_torch, eval_metrics, model_forward,  # noqa: E402
-                              predict, to_torch_params, train_step_grads)
+from oracle.ref_model import (KerasAdam, eval_metrics, forward_detail, predict,  # noqa: E402
+                              train_step_grads)
 from oracle.ref_utils import get_adj_coo, get_y_true, make_fold_files  # noqa: E402
 
 DATA = "/root/reference/datasets/prediction_datasets"
@@ -58,11 +62,13 @@ def main():
         adj = get_adj_coo(np.concatenate([f["X_train"], f["X_test"]]), N_ENT, N_REL)
         Xt = np.concatenate([f["X_test"], f["neg_X_test"]]).astype(np.int64)
         y = get_y_true(f["X_test"], Xt)
-        p64 = predict(w, Xt, adj, N_ENT, dtype=torch.float64)
-        p32 = predict(w, Xt, adj, N_ENT, dtype=torch.float32)
+        p64, s64 = predict(w, Xt, adj, N_ENT, dtype=torch.float64, logits=True)
+        p32, s32 = predict(w, Xt, adj, N_ENT, dtype=torch.float32, logits=True)
         m = eval_metrics(y, p64)
-        np.savez_compressed(os.path.join(HERE, f"fold{k}_eval.npz"), probs=p64, probs32=p32, y_true=y,
-                            roc_auc=m["roc_auc"], aupr=m["aupr"], accuracy=m["accuracy"], f1=m["f1"])
+        np.savez_compressed(os.path.join(HERE, f"fold{k}_eval.npz"), probs=p64, probs32=p32, logits=s64,
+                            logits32=s32, y_true=y, roc_auc=m["roc_auc"], aupr=m["aupr"],
+                            accuracy=m["accuracy"], f1=m["f1"])
+        print(f"fold {k}: max|logit| {np.abs(s64).max():.2f}, fp32 logit drift {np.abs(s32 - s64).max():.2e}")
         print(f"fold {k}: auc {m['roc_auc']:.6f} aupr {m['aupr']:.6f}")
 
     # one training step on fold 0 from the bundled weights
@@ -72,16 +78,19 @@ def main():
     loss, scores, grads = train_step_grads(w, f["X_train"], f["X_train_neg"], adj, N_ENT)
     opt = KerasAdam()
     new = opt.step({k: v.astype(np.float64) for k, v in w.items()}, grads)
-    P = to_torch_params(w, torch.float64, requires_grad=False)
-    tr = f["X_train"][:256].astype(np.int64)
-    with torch.no_grad():
-        _, layers = model_forward(P, tr[:, 0], tr[:, 1], tr[:, 2], adj_to_torch(adj, N_ENT), return_layers=True)
-    out = {"loss": loss, "scores": scores}
+    scored = np.concatenate([f["X_train"], f["X_train_neg"]])
+    _, s64, layers = forward_detail(w, scored, adj, N_ENT, dtype=torch.float64)
+    _, s32, _ = forward_detail(w, scored, adj, N_ENT, dtype=torch.float32)
+    _, _, layers32 = forward_detail(w, f["X_train"][:256], adj, N_ENT, dtype=torch.float32)
+    out = {"loss": loss, "scores": scores, "logits": s64, "logits32": s32}
     out.update({f"grad_{k}": v for k, v in grads.items()})
     out.update({f"adam1_{k}": v for k, v in new.items()})
-    for i, (xh, xt) in enumerate(layers, 1):
-        out[f"layer{i}_head"] = xh.numpy()
-        out[f"layer{i}_tail"] = xt.numpy()
+    for i, ((xh, xt), (xh32, xt32)) in enumerate(zip(layers, layers32), 1):
+        out[f"layer{i}_head"] = xh[:256]
+        out[f"layer{i}_tail"] = xt[:256]
+        out[f"layer{i}_head32"] = xh32
+        out[f"layer{i}_tail32"] = xt32
+    print(f"fold0 step: max|logit| {np.abs(s64).max():.2f}, fp32 logit drift {np.abs(s32 - s64).max():.2e}")
     np.savez_compressed(os.path.join(HERE, "fold0_step.npz"), **out)
     print("fold0 step loss", loss)
 
@@ -116,7 +125,11 @@ def main():
     loss, scores, grads = train_step_grads(sp, tri, neg, adj, N)
     opt = KerasAdam()
     new = opt.step({k: v.astype(np.float64) for k, v in sp.items()}, grads)
-    out = {"triples": tri, "neg": neg, "loss": loss, "scores": scores, "N": N, "R": R, "D": D}
+    _, s64, layers = forward_detail(sp, np.concatenate([tri, neg]), adj, N, dtype=torch.float64)
+    out = {"triples": tri, "neg": neg, "loss": loss, "scores": scores, "logits": s64, "N": N, "R": R, "D": D}
+    for i, (xh, xt) in enumerate(layers, 1):
+        out[f"layer{i}_head"] = xh
+        out[f"layer{i}_tail"] = xt
     out.update({f"param_{k}": v for k, v in sp.items()})
     out.update({f"grad_{k}": v for k, v in grads.items()})
     out.update({f"adam1_{k}": v for k, v in new.items()})

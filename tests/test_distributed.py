@@ -1,9 +1,11 @@
 """Edge-partitioned data parallelism on CPU: world_size 2, gloo backend (no GPU needed).
 
-The product's DP logic is exercised for real: `shard_triples` partitions the scored edges,
-`GradAllReduce` sums the flat gradient buffer + loss in one collective.  The per-rank compute
-is the CPU oracle here (the HIP engine needs a GPU); each rank normalises by the GLOBAL edge
-count exactly as Engine.train_step(t_global=T) does.
+The product's DP logic is exercised for real: `shard_triples` partitions the scored edges and
+`BucketedAllReduce` sums the flat gradient buffer + loss slot IN PLACE, bucket by bucket, in the
+order Engine.backward hands the buckets over (all small gradients + loss, then row chunks of dE).
+The per-rank compute is the CPU oracle here (the HIP engine needs a GPU; tests/test_gpu_parallel.py
+runs the engine itself); each rank normalises by the GLOBAL edge count exactly as
+Engine.train_step(t_global=T) does.
 """
 import os
 import socket
@@ -14,7 +16,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from iddgcn_amd.parallel import GradAllReduce, shard_range, shard_triples
+from iddgcn_amd.engine import param_layout
+from iddgcn_amd.parallel import BucketedAllReduce, shard_range, shard_triples
 
 
 def _free_port():
@@ -40,12 +43,19 @@ def _worker(rank, world, port, q):
         pos, neg = my_tri[my_lab == 1], my_tri[my_lab == 0]
         adj = get_adj_coo(g["triples"], N, R)            # the graph is replicated on every rank
         loss, _, grads = train_step_grads(params, pos, neg, adj, N)
-        keys = sorted(grads)
+        D = int(g["D"])
+        keys = [name for name, _, _ in param_layout(N, R, D)]           # FlatParams order: E first
         T, Ts = len(tri), len(my_tri)
-        flat = torch.cat([torch.as_tensor(grads[k]).reshape(-1) for k in keys]) * (Ts / T)
-        loss_sum = torch.tensor([loss * Ts], dtype=torch.float64)
-        GradAllReduce(flat)(flat, loss_sum)
-        q.put((rank, flat.numpy(), float(loss_sum) / T, keys))
+        buf = torch.cat([torch.as_tensor(grads[k]).reshape(-1) for k in keys] +
+                        [torch.tensor([loss * T], dtype=torch.float64)]) * (Ts / T)    # [flat | loss slot]
+        comm = BucketedAllReduce(min_bucket_rows=64)
+        comm.ready(buf[N * D:])                         # small gradients + loss
+        chunks = comm.row_chunks(N)
+        assert len(chunks) > 1
+        for n0, n1 in chunks:                           # dE row chunks
+            comm.ready(buf[n0 * D:n1 * D])
+        comm.finish()
+        q.put((rank, buf[:-1].numpy(), float(buf[-1]) / T, keys))
     finally:
         dist.destroy_process_group()
 
@@ -78,5 +88,18 @@ def test_dp_world2_gloo_equals_full_batch(golden):
     (_, f0, l0, keys), (_, f1, l1, _) = res
     assert np.array_equal(f0, f1) and l0 == l1                  # identical on every rank after the all-reduce
     full = np.concatenate([g[f"grad_{k}"].reshape(-1) for k in keys])
+    assert f0.shape == full.shape
     np.testing.assert_allclose(f0, full, rtol=0, atol=1e-12 * np.abs(full).max() + 1e-18)
     assert abs(l0 - float(g["loss"])) < 1e-12
+
+
+def test_bucketed_row_chunks_cover_rows():
+    c = BucketedAllReduce(max_chunks=4, min_bucket_rows=100)
+    for n in (0, 1, 99, 100, 250, 1000, 100_000):
+        ch = c.row_chunks(n)
+        if n == 0:
+            assert ch == []
+            continue
+        assert ch[0][0] == 0 and ch[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(ch, ch[1:]))
+        assert len(ch) <= 4 and (len(ch) == 1 or min(b - a for a, b in ch) >= 100)

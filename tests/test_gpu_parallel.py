@@ -1,0 +1,120 @@
+"""The data-parallel product path on the GPU (IDDGCN.py:123-178,399-412 sharded).
+
+* Two scored-edge shards through Engine (t_global = T, as every rank of a DP step runs them) sum to
+  the full-batch gradients and loss: the edge partitioning itself is exact up to fp32 summation
+  order (the shard partials are added in another order than the full batch's segment sums), bar
+  1e-5 of max|g| per tensor at a non-saturating init, 5e-5 on the saturated trained fold-0 weights
+  (where the fp32 reference formulation itself is 4e-3 of max|g| away from fp64).
+* The multi-rank branch of IDDGCN_Model.fit() (shard_triples -> per-rank ScoredEdges -> train_step with
+  the in-place bucketed all-reduce) with 2 ranks sharing one GPU over gloo (host-staged buckets) gives
+  every rank the full-batch gradients, loss and — Adam being replicated — identical weights.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from iddgcn_amd.engine import Engine, FlatParams
+from iddgcn_amd.graph import get_adj_mats
+from iddgcn_amd.parallel import shard_range
+from iddgcn_amd.utils import synthetic_graph
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _mild(N, R, D, seed):
+    rng = np.random.default_rng(seed)
+    p = {"E": rng.standard_normal((N, D)) / np.sqrt(D)}
+    for l in (1, 2, 3):
+        p[f"K{l}"] = rng.standard_normal((R, D, D)) / D
+        p[f"S{l}"] = rng.standard_normal((D, D)) / np.sqrt(D)
+        p[f"Wa{l}"] = rng.standard_normal((D, R)) / np.sqrt(D)
+        p[f"ba{l}"] = rng.standard_normal(R) * 0.1
+    p["rel"] = rng.standard_normal((R, D))
+    return {k: v.astype(np.float32) for k, v in p.items()}
+
+
+@pytest.mark.parametrize("D,gemm", [(64, "split"), (256, "split"), (256, "exact")])
+def test_two_shards_sum_to_full_batch(D, gemm, cuda):
+    N, R = 3000, 2
+    pos, neg = synthetic_graph(N, R, 12000, seed=21)
+    tri = np.concatenate([pos, neg])
+    lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+    T = len(tri)
+    eng = Engine(N, R, D, cuda, gemm=gemm)
+    P = FlatParams(N, R, D, cuda)
+    P.load(_mild(N, R, D, 4))
+    adj = eng.adjacency(get_adj_mats(pos, N, R))
+    G = FlatParams(N, R, D, cuda)
+    loss, _ = eng.loss_and_grads(P, G, adj, eng.edges(tri, lab))
+    full, full_loss = G.to_numpy(), float(loss.item())
+    acc = FlatParams(N, R, D, cuda)
+    for rank in range(2):
+        lo, hi = shard_range(T, rank, 2)
+        Gs = FlatParams(N, R, D, cuda)
+        eng.loss_and_grads(P, Gs, adj, eng.edges(tri[lo:hi], lab[lo:hi]), t_global=T)
+        acc.buf += Gs.buf
+    torch.cuda.synchronize()
+    assert abs(float(acc.loss.item()) - full_loss) <= 1e-6 * full_loss
+    shards = acc.to_numpy()
+    for k, g in full.items():
+        assert np.abs(shards[k] - g).max() <= 1e-5 * np.abs(g).max() + 1e-30, k
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _fit_once(world, rank, q):
+    """fold-0 shape, bundled weights, ONE full-batch fit() epoch; returns (loss, grads, weights)."""
+    from iddgcn_amd import Adam, BinaryCrossentropy, get_IDDGCN_Model
+    d = dict(np.load(os.path.join(HERE, "golden", "fold0_data.npz")))
+    model = get_IDDGCN_Model(845, 4, 64, 64, 89, None, 0, 0)
+    model.load_weights(os.path.join(HERE, "golden", "weights_fold0.npz"))
+    model.neg_triples = d["X_train_neg"][None]
+    model.compile(loss=BinaryCrossentropy(), optimizer=Adam(learning_rate=0.001))
+    X = d["X_train"][None]
+    adj = get_adj_mats(d["X_train"], 845, 4)
+    hist = model.fit(x=[np.arange(845)[None], X[:, :, 0], X[:, :, 1], X[:, :, 2], adj],
+                     y=np.ones((1, X.shape[1])), epochs=1, verbose=0)
+    q.put((rank, hist.history["loss"][0], model._grads.to_numpy(), model.get_weights()))
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _fit_once(world, rank, q)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fit_world2_gloo_one_gpu_equals_single_process(cuda):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    _fit_once(1, -1, q)
+    _, loss1, g1, w1 = q.get(timeout=60)
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, l0, g0, w0), (_, l1, gr1, wr1) = res
+    assert l0 == l1 and all(np.array_equal(a, b) for a, b in zip(w0, wr1))   # replicated after all-reduce
+    assert all(np.array_equal(g0[k], gr1[k]) for k in g0)
+    assert abs(l0 - loss1) <= 1e-6 * loss1
+    for k, g in g1.items():
+        assert np.abs(g0[k] - g).max() <= 5e-5 * np.abs(g).max() + 1e-30, k
