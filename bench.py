@@ -10,6 +10,7 @@ random init, inputs resident in HBM before the timed region):
                         rank owns 4M scored edges of a 2M*N-edge graph on the same 100k nodes.
   --config 4            1M nodes, 2 relations, 20M edges, D=256, T = 40M scored edges; STRONG-scaled
                         (the 40M scored edges are split over the N ranks).
+  --config 5            1M nodes, 8 relations, 40M edges + 10M negatives, D=256, T = 50M; STRONG-scaled.
   --config 2            the reference's fold-0 shape (845 nodes, 4 relations, D=64), one GPU.
 Multi-GPU: `--gpus N` starts N ranks itself (torch.distributed.run, one process per GPU, RCCL)
 before anything touches the GPU, or joins the N ranks a launcher already started; the ranks meet in
@@ -50,6 +51,8 @@ CONFIGS = {
     2: dict(name="synthetic-fold0-shape", N=845, R=4, M=37_510, D=64, scaling="weak"),
     3: dict(name="synthetic-3", N=100_000, R=2, M=2_000_000, D=256, scaling="weak"),
     4: dict(name="synthetic-4", N=1_000_000, R=2, M=20_000_000, D=256, scaling="strong"),
+    # 40M positives, 10M negatives (one per 4 positives)
+    5: dict(name="synthetic-5", N=1_000_000, R=8, M=40_000_000, D=256, scaling="strong", neg_every=4),
 }
 
 
@@ -216,6 +219,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     weak = cfg["scaling"] == "weak"
     M = cfg["M"] * world if weak else cfg["M"]            # weak: per-GPU work fixed
     pos, neg = synthetic_graph(N, R, M, seed=0)           # identical on every rank (seeded)
+    neg = neg[::cfg.get("neg_every", 1)]
     T = len(pos) + len(neg)
     lo, hi = shard_range(T, rank, world)                  # this rank's contiguous shard (pos ++ neg)
     npos = len(pos)
@@ -250,7 +254,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
             dist.barrier()
         elapsed = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([elapsed], device=dev)
+            t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         probe_out, eng.probe = eng.probe, None
@@ -311,9 +315,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL over xGMI; IDDGCN_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing
+    # fewer GPUs (host-staged buckets, tests and 1-GPU boxes only)
+    backend = os.environ.get("IDDGCN_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     main_out = run_workload(args.config, args, world, rank, dev, args.gemm, not args.no_other_mode)

@@ -1,4 +1,5 @@
-"""ctypes binding of libiddgcn_hip.so (C-ABI declared in include/iddgcn.h and include/iddgcn_graph.h).
+"""ctypes binding of libiddgcn_hip.so (C-ABI declared in include/iddgcn.h, iddgcn_graph.h,
+iddgcn_similarity.h and iddgcn_sampling.h).
 
 The product path has no CPU fallback: if the shared library is missing or was
 built for another ABI version, :func:`lib` raises immediately.
@@ -49,6 +50,7 @@ SIGNATURES = {
     "iddgcn_gemm_tn_blocks": (ci, [cll, ci]),
     "iddgcn_gemm_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
     "iddgcn_rowgemm_batched_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs), ci]),
+    "iddgcn_rowgemm_kernel_id": (ci, [ctypes.POINTER(RowGemmArgs)]),
     "iddgcn_adam_table_f32": (ci, [vp, cll, vp, vp, vp, vp, vp, vp, cf, cf, cf, ci]),
     "iddgcn_step_advance": (ci, [vp, vp, vp, vp]),
     "iddgcn_gemm_tn_seg_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci, vp, vp, ci, vp, vp, cll, vp, vp, ci]),
@@ -73,6 +75,13 @@ SIGNATURES = {
     "iddgcn_build_adjacency": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cll]),
     "iddgcn_scored_edges_workspace": (cll, [cll, ci]),
     "iddgcn_build_scored_edges": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cll]),
+    # include/iddgcn_sampling.h
+    "iddgcn_randint_mask": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "iddgcn_mt19937_seed": (ci, [vp, ctypes.c_uint32, vp]),
+    "iddgcn_mt19937_generate": (ci, [vp, vp, cll, vp]),
+    "iddgcn_accept_chunks": (cll, [cll]),
+    "iddgcn_masked_accept": (ci, [vp, vp, cll, ctypes.c_uint32, cll, vp, vp, vp]),
+    "iddgcn_assemble_negatives": (ci, [vp, cll, vp, vp, vp, vp]),
     # include/iddgcn_similarity.h
     "iddgcn_similarity_workspace": (cll, [ci, ci]),
     "iddgcn_similarity_pairs": (ci, [vp, ci, ci, vp, ctypes.c_double, vp, cll, vp, cll, vp, vp, cll]),

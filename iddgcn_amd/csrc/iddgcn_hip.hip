@@ -602,14 +602,15 @@ static_assert(ROWS_PER_WAVE == 4, "the early-wave s_waitcnt vmcnt(4) counts the 
 constexpr int LDA = D + 4;                             // padded rows: conflict-free ds_read_b128
 constexpr int A_FLOATS = TR * LDA;                     // 33,280 B
 constexpr int SLAB = TR * 32;                          // 32 rows x 32 cols
-constexpr int NS_MAX = 2;
 constexpr int COEF = 64;                               // 32 rows x R (R <= 2)
+constexpr int COEF8 = 32 * MAX_R;                      // 32 rows x R (R <= 8)
 constexpr int IDX = 64;                                // next tile's v_idx (32) + coef_idx (32)
 constexpr int CMP = 32;                                // distinct V rows of the tile (run starts)
 constexpr int CINV = 32;                               // split mode: 1/scale of the wave's 32 columns
-constexpr int WAVE_FLOATS = NS_MAX * SLAB + COEF + IDX + CMP + CINV;
-constexpr int ROWINV = 2 * TR;                         // split mode: 1/scale of each A row, per buffer
-constexpr int LDS_FLOATS = 2 * A_FLOATS + NW * WAVE_FLOATS + ROWINV;   // 131 KiB
+// gathered V with more than 2 relations (NV = 4 or 8 slots, R <= NV at run time): slabs r >= 1 hold
+// only the first GATHER_CAP distinct rows of a tile, so 8 relations fit the LDS; a tile with more runs
+// of equal v_idx (tail-sorted edges have 1-3) reads the V rows past the cap from global memory (L2)
+constexpr int GATHER_CAP = 7;
 }  // namespace r3
 
 // ---- split-fp16 operands (X3 kernels) -------------------------------------------------------
@@ -669,17 +670,27 @@ __device__ __forceinline__ float wave_max(float v) {             // max over the
 // the tail activation x^1 of layer 1 never has to be re-read by the backward.  The caller
 // guarantees at most REC_CAP runs of equal v_idx per 32-row tile (tail-sorted edges: 1-4).
 constexpr int REC_CAP = 8;
+// NV: gathered V tables (0 = none; 1, 2 = exactly R; 4, 8 = capacity for R <= NV, capped slabs).
+// Up to ROWGEMM_BATCH independent GEMMs of the same variant run in one launch: blockIdx.y = entry.
 template <int NV, bool AUX, bool HAS_COEF, bool X3, bool REC = false>
-__global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
+__global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     using namespace r3;
-    static_assert(!REC || (NV >= 2 && !AUX && HAS_COEF), "REC: V_0 + coefficient-weighted V_1.., no aux");
+    const RowGemmP p = pb.p[blockIdx.y];
+    static_assert(!REC || (NV >= 2 && NV <= 3 && !AUX && HAS_COEF), "REC: V_0 + coefficient-weighted V_1.., no aux");
+    static_assert(REC || NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
+    constexpr bool WIDE = !REC && NV > 2;              // capped slabs, run-time R <= NV
     constexpr int NS = NV + (AUX ? 1 : 0);
     constexpr int NSL = NS > 1 ? NS : 1;               // slabs per wave (slab 0 also stages C)
-    // Slab 0 holds 32 rows (it also stages the C tile); REC slabs r >= 1 hold REC_CAP rows.
-    constexpr int CAPV = REC ? REC_CAP : 32;
+    // Slab 0 holds 32 rows (it also stages the C tile); REC slabs r >= 1 hold REC_CAP rows, WIDE
+    // slabs r >= 1 GATHER_CAP rows.
+    constexpr int CAPV = REC ? REC_CAP : (WIDE ? GATHER_CAP : 32);
     constexpr int SLABC = CAPV * 32;
     constexpr int SLABS = SLAB + (NSL - 1) * SLABC;    // floats of all slabs of one wave
-    constexpr int WF = SLABS + COEF + IDX + CMP + CINV;
+    // coefficient slots: 32 rows x R; up to 8 relations for WIDE and for broadcast V (NV = 0)
+    constexpr bool COEF_WIDE = WIDE || (NV == 0 && HAS_COEF);
+    constexpr int COEFN = COEF_WIDE ? COEF8 : COEF;
+    constexpr int CFN = COEF_WIDE ? MAX_R : 2;         // coefficients each lane holds
+    constexpr int WF = SLABS + COEFN + IDX + CMP + CINV;
     // A-tile pipeline depth: three buffers (A(t+2) in flight while A(t) feeds the MFMAs) when the
     // LDS budget allows, two otherwise
     constexpr int NBUF = (3 * A_FLOATS + NW * WF + 3 * TR) * 4 <= 160 * 1024 ? 3 : 2;
@@ -771,7 +782,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     auto clampe = [&](long long e) { return e > Mlast ? Mlast : e; };
 
     // ---- row indices of the next tile: DMA'd into a wave-private LDS slot -------------
-    int* idxw = reinterpret_cast<int*>(coefw + r3::COEF);      // [0,32) v_idx, [32,64) coef_idx
+    int* idxw = reinterpret_cast<int*>(coefw + COEFN);         // [0,32) v_idx, [32,64) coef_idx
     int vslot = 0;                                               // slab row of this lane's V row
     const bool need_idx = (NV > 0 && p.v_idx) || (HAS_COEF && p.coef_idx);
     auto dma_idx = [&](long long t) {
@@ -836,8 +847,12 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
                 const long long v = cmpw[row < u ? row : u - 1];
 #pragma unroll
                 for (int r = 0; r < NV; ++r) {
-                    if constexpr (REC) {
-                        if (r > 0 && kb >= CAPV) continue;   // (precondition broken: stay in bounds)
+                    if constexpr (WIDE) {
+                        if (r >= R) break;
+                    }
+                    if constexpr (REC || WIDE) {
+                        // capped slab: rows past CAPV stay unwritten (precondition broken: stay in bounds)
+                        if (r > 0 && row >= CAPV) continue;
                     }
                     const float* gp = p.V + r * p.v_rel_stride + v * D + c0 + g * 4;
                     __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + soff(r) + kb * 32), 16, 0, 0);
@@ -855,13 +870,17 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
             }
         }
         if (HAS_COEF) {
-            const float* g = p.coef;             // lanes past 32*R read a valid dummy
-            if (lane < TR * R) {
-                const int row = lane / R, r = lane % R;
-                const long long ci = p.coef_idx ? (long long)idxw[32 + row] : clampe(t * TR + row);
-                g = p.coef + ci * R + r;
+            // 32 x R coefficients, 64 per DMA instruction (R <= 2: one instruction)
+            for (int k0 = 0; k0 < TR * R; k0 += 64) {
+                const float* g = p.coef;             // lanes past 32*R read a valid dummy
+                const int q = k0 + lane;
+                if (q < TR * R) {
+                    const int row = q / R, r = q - row * R;
+                    const long long ci = p.coef_idx ? (long long)idxw[32 + row] : clampe(t * TR + row);
+                    g = p.coef + ci * R + r;
+                }
+                __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(coefw + k0), 4, 0, 0);
             }
-            __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)coefw, 4, 0, 0);
         }
     };
 
@@ -880,9 +899,15 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
     // stage phase: combine + activation into slab 0 (LDS only, plus the C loads of `accumulate`)
     auto epi_stage = [&](long long t, const f32x16& acc) {
         const __amdgpu_buffer_rsrc_t rc = out_rsrc(t);
-        float cf[NS_MAX] = {0.f, 0.f};
+        float cf[CFN];
+#pragma unroll
+        for (int r = 0; r < CFN; ++r) cf[r] = 0.f;
         if (HAS_COEF) {
-            if (REC ? R == 2 : (NV == 2 || (NV == 0 && R == 2))) {
+            if constexpr (COEF_WIDE) {
+#pragma unroll
+                for (int r = 0; r < CFN; ++r)
+                    if (r < R) cf[r] = coefw[i * R + r];
+            } else if (REC ? R == 2 : (NV == 2 || (NV == 0 && R == 2))) {
                 const float2 c2 = *reinterpret_cast<const float2*>(coefw + i * 2);
                 cf[0] = c2.x;
                 cf[1] = c2.y;
@@ -915,12 +940,24 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmP p) {
                 const int offv = vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
 #pragma unroll
                 for (int r = 0; r < NV; ++r) {
-                    const f32x4 s = ld4(slabw + r * SLAB + offv);
+                    if constexpr (WIDE) {
+                        if (r >= R) break;
+                    }
+                    f32x4 s = ld4(slabw + soff(r) + offv);
+                    if constexpr (WIDE) {
+                        if (r > 0 && vslot >= CAPV) {    // a distinct row past the capped slab: from L2
+                            const int vrow = cmpw[vslot];
+                            typedef const __attribute__((address_space(1))) f32x4* gf4p;
+                            s = *(gf4p)(p.V + r * p.v_rel_stride + (long long)vrow * D + col);
+                        }
+                    }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
                 }
             } else if (HAS_COEF) {      // broadcast V rows (v_row_stride == 0): tiny, cache-resident
-                for (int r = 0; r < R; ++r) {
+#pragma unroll
+                for (int r = 0; r < CFN; ++r) {
+                    if (r >= R) break;
                     const f32x4 s = ld4(p.V + r * p.v_rel_stride + col);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
@@ -2361,6 +2398,73 @@ __global__ void step_advance_kernel(int* __restrict__ step, float* __restrict__ 
     *step = s + 1;
 }
 
+// ---- D = 256 row-GEMM variant selection (rowgemm256_v3_kernel) ----
+struct V3Sel {
+    int nv;                 // gathered V tables (template NV)
+    bool aux, hc, rec;
+};
+// Which v3 instantiation computes this call, or false (the DMA-v2 / register-staged kernels then run).
+bool v3_select(const RowGemmP& p, V3Sel& sel) {
+    if (!(g_rowgemm_path == 0 || g_gemm_split)) return false;
+    const bool gatherV = p.R > 0 && p.v_row_stride != 0;
+    const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
+    if (p.act == IDDGCN_ACT_DSIGMOID_COMBINE) {
+        // x^1 recompute: R <= 2, dense V rows, the caller's bound on V runs per 32-row tile
+        if (!(p.R <= 2 && p.v_row_stride == 256 && p.v_runs_max >= 1 && p.v_runs_max <= REC_CAP)) return false;
+        sel = {p.R + 1, false, true, true};
+        return true;
+    }
+    if (gatherV) {
+        if (dsig || p.v_row_stride != 256) return false;
+        if (p.R <= 2) {
+            sel = {p.R, false, true, false};
+            return true;
+        }
+        // more relations: capped slabs (rows past the cap of a tile come from L2)
+        sel = {p.R <= 4 ? 4 : 8, false, true, false};
+        return true;
+    }
+    sel = {0, dsig, p.R > 0, false};
+    return true;
+}
+
+// One launch of up to ROWGEMM_BATCH v3 GEMMs of the same variant (blockIdx.y = entry).  The persistent
+// grid is ~256 workgroups in all (one per CU: 131-155 KB of LDS each), shared out over the entries.
+void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel) {
+    const long long per = n > 0 ? (256 + n - 1) / n : 256;
+    long long nbmax = 0;
+    for (int k = 0; k < n; ++k) {
+        RowGemmP& p = pb.p[k];
+        const long long nt = ((long long)p.M + r3::TR - 1) / r3::TR;
+        long long nb = nt < per ? nt : per;
+        if (nb < 1) nb = 1;
+        p.tiles_per_block = (int)((nt + nb - 1) / nb);
+        if (p.tiles_per_block < 1) p.tiles_per_block = 1;
+        nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
+        if (nb > nbmax) nbmax = nb;
+    }
+    if (nbmax == 0) return;
+    const dim3 g((unsigned)nbmax, (unsigned)n), blk(512);
+    const bool x3 = g_gemm_split != 0;
+#define V3L(NV, AUX, HC, REC)                                                                        \
+    {                                                                                                \
+        if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, REC>), g, blk, 0, st, pb); \
+        else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, false, REC>), g, blk, 0, st, pb);   \
+    }
+    if (sel.rec) {
+        if (sel.nv == 2) V3L(2, false, true, true)
+        else V3L(3, false, true, true)
+    } else if (sel.nv == 1) V3L(1, false, true, false)
+    else if (sel.nv == 2) V3L(2, false, true, false)
+    else if (sel.nv == 4) V3L(4, false, true, false)
+    else if (sel.nv == 8) V3L(8, false, true, false)
+    else if (sel.hc && sel.aux) V3L(0, true, true, false)
+    else if (sel.hc) V3L(0, false, true, false)
+    else if (sel.aux) V3L(0, true, false, false)
+    else V3L(0, false, false, false)
+#undef V3L
+}
+
 inline unsigned grid_for(long long rows, int lpr) {
     const long long threads = rows * lpr;
     return (unsigned)((threads + 255) / 256);
@@ -2455,55 +2559,20 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     }
     const bool gatherV = p.R > 0 && p.v_row_stride != 0;
     const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
+    V3Sel sel;
+    if (a->D == 256 && v3_select(p, sel)) {
+        RowGemmBatch pb;
+        pb.p[0] = p;
+        launch_v3(st, pb, 1, sel);
+        return launch_status();
+    }
     if (p.act == IDDGCN_ACT_DSIGMOID_COMBINE) {
-        // fast path: D = 256, R <= 2, dense V rows, the caller's bound on V runs per 32-row tile
-        if (a->D == 256 && p.R <= 2 && p.v_row_stride == 256 && p.v_runs_max >= 1 && p.v_runs_max <= REC_CAP &&
-            (g_rowgemm_path == 0 || g_gemm_split)) {
-            const long long nt = ((long long)p.M + r3::TR - 1) / r3::TR;
-            long long nb = nt < 256 ? nt : 256;
-            p.tiles_per_block = (int)((nt + nb - 1) / nb);
-            nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
-            const dim3 g((unsigned)nb), blk(512);
-#define V3R(NV)                                                                                           \
-            {                                                                                             \
-                if (g_gemm_split) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, false, true, true, true>), g, blk, 0, st, p); \
-                else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, false, true, false, true>), g, blk, 0, st, p);           \
-            }
-            if (p.R == 1) V3R(2)
-            else V3R(3)
-#undef V3R
-            return launch_status();
-        }
         switch (a->D) {      // any v_idx order: the register-staged kernel
             case 32: RGEMM(32, 2048); break;
             case 64: RGEMM(64, 2048); break;
             case 128: RGEMM(128, 1024); break;
             default: RGEMM(256, 256); break;
         }
-        return launch_status();
-    }
-    // v3 (staggered, wave-private slabs): D=256, R <= 2
-    const bool v3_ok = a->D == 256 && p.R <= 2 && !(gatherV && dsig) && (!gatherV || p.v_row_stride == 256) &&
-                       g_rowgemm_path == 0;
-    if (v3_ok || (a->D == 256 && g_gemm_split && p.R <= 2 && !(gatherV && dsig) &&
-                  (!gatherV || p.v_row_stride == 256))) {
-        const long long nt = ((long long)p.M + r3::TR - 1) / r3::TR;
-        long long nb = nt < 256 ? nt : 256;
-        p.tiles_per_block = (int)((nt + nb - 1) / nb);
-        nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
-        const dim3 g((unsigned)nb), blk(512);
-#define V3K(NV, AUX, HC)                                                                             \
-        {                                                                                            \
-            if (g_gemm_split) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true>), g, blk, 0, st, p); \
-            else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, false>), g, blk, 0, st, p);           \
-        }
-        if (gatherV && p.R == 1) V3K(1, false, true)
-        else if (gatherV) V3K(2, false, true)
-        else if (p.R > 0 && dsig) V3K(0, true, true)
-        else if (p.R > 0) V3K(0, false, true)
-        else if (dsig) V3K(0, true, false)
-        else V3K(0, false, false)
-#undef V3K
         return launch_status();
     }
     const int epi_rows = gatherV ? p.R : (dsig ? 1 : 0);
@@ -2527,6 +2596,25 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     return launch_status();
 }
 
+int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* a) {
+    if (!a || !dim_ok(a->D)) return -1;
+    RowGemmP p;
+    p.M = a->M; p.A = a->A; p.a_idx = a->a_idx; p.B = a->B; p.b_trans = a->b_trans;
+    p.C = a->C; p.accumulate = a->accumulate; p.R = a->R; p.coef = a->coef; p.coef_idx = a->coef_idx;
+    p.V = a->V; p.v_idx = a->v_idx; p.v_rel_stride = a->v_rel_stride; p.v_row_stride = a->v_row_stride;
+    p.act = a->act; p.aux = a->aux; p.v_runs_max = a->v_runs_max;
+    V3Sel sel;
+    if (a->D == 256 && v3_select(p, sel))
+        return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.rec ? 4 : 0);
+    const bool gatherV = p.R > 0 && p.v_row_stride != 0;
+    const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
+    const int epi_rows = gatherV ? p.R : (dsig ? 1 : 0);
+    if (p.act != IDDGCN_ACT_DSIGMOID_COMBINE && a->D == 256 && epi_rows <= r256::EPI_MAX && !(gatherV && dsig) &&
+        (!gatherV || p.v_row_stride == 256) && g_rowgemm_path != 1)
+        return 200;
+    return 100;
+}
+
 int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
     if (!a || n < 0 || n > ROWGEMM_BATCH) return IDDGCN_E_BAD_ARG;
     if (n == 0) return 0;
@@ -2542,7 +2630,27 @@ int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
             return IDDGCN_E_BAD_ARG;
         if (a[k].act < IDDGCN_ACT_NONE || a[k].act > IDDGCN_ACT_DSIGMOID_COMBINE) return IDDGCN_E_BAD_ARG;
     }
-    if (!one_launch) {          // D = 256: the pipelined kernels, one launch per entry
+    if (!one_launch) {          // D = 256: one v3 launch when every entry maps to the same variant
+        RowGemmBatch pb;
+        V3Sel sel0{}, sel{};
+        bool same = true;
+        int m = 0;
+        for (int k = 0; k < n && same; ++k) {
+            if (a[k].M == 0) continue;
+            RowGemmP& p = pb.p[m];
+            p.M = a[k].M; p.A = a[k].A; p.a_idx = a[k].a_idx; p.B = a[k].B; p.b_trans = a[k].b_trans;
+            p.C = a[k].C; p.accumulate = a[k].accumulate; p.R = a[k].R; p.coef = a[k].coef;
+            p.coef_idx = a[k].coef_idx; p.V = a[k].V; p.v_idx = a[k].v_idx; p.v_rel_stride = a[k].v_rel_stride;
+            p.v_row_stride = a[k].v_row_stride; p.act = a[k].act; p.aux = a[k].aux; p.v_runs_max = a[k].v_runs_max;
+            if (!v3_select(p, sel)) same = false;
+            else if (m == 0) sel0 = sel;
+            else same = sel.nv == sel0.nv && sel.aux == sel0.aux && sel.hc == sel0.hc && sel.rec == sel0.rec;
+            ++m;
+        }
+        if (same) {
+            if (m > 0) launch_v3((hipStream_t)stream, pb, m, sel0);
+            return launch_status();
+        }
         for (int k = 0; k < n; ++k) {
             const int rc = iddgcn_rowgemm_f32(stream, a + k);
             if (rc) return rc;
@@ -2699,7 +2807,7 @@ int iddgcn_combine_f32(void* stream, int M, int d, int R, const float* Y, const 
     if (M < 0 || !Y || !out || (R > 0 && (!coef || !V))) return IDDGCN_E_BAD_ARG;
     if (M == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if (d == 256 && y_idx && y_idx == v_idx && !coef_idx && R <= 4) {
+    if (d == 256 && y_idx && y_idx == v_idx && !coef_idx) {
         const long long nchunk = ((long long)M + RC_CH - 1) / RC_CH;
         long long nb = (nchunk + 3) / 4;
         if (nb > 2048) nb = 2048;
@@ -2709,7 +2817,11 @@ int iddgcn_combine_f32(void* stream, int M, int d, int R, const float* Y, const 
             case 1: RCK(1); break;
             case 2: RCK(2); break;
             case 3: RCK(3); break;
-            default: RCK(4); break;
+            case 4: RCK(4); break;
+            case 5: RCK(5); break;
+            case 6: RCK(6); break;
+            case 7: RCK(7); break;
+            default: RCK(8); break;
         }
 #undef RCK
         return launch_status();

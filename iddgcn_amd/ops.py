@@ -87,6 +87,13 @@ def rowgemm(A, B, C, **kw):
     L.check(L.lib().iddgcn_rowgemm_f32(_stream(), ctypes.byref(args)), "rowgemm")
 
 
+def rowgemm_kernel_id(A, B, C, **kw):
+    """Which kernel rowgemm(A, B, C, **kw) runs (iddgcn_rowgemm_kernel_id): 300 + 10*NV + ... for the D=256
+    v3 pipeline, 200 the v2 LDS-DMA kernel, 100 the register-staged one."""
+    args = _rowgemm_args(A, B, C, **kw)
+    return int(L.lib().iddgcn_rowgemm_kernel_id(ctypes.byref(args)))
+
+
 def rowgemm_batched(calls):
     """Independent row GEMMs of one width in one launch (iddgcn_rowgemm_batched_f32).  calls: list of
     (A, B, C, kwargs) as for rowgemm; at most 16."""
@@ -480,4 +487,60 @@ def similarity_triples(sorted_keys, N, relation, start):
     out = torch.empty((n, 3), dtype=_I64, device=sorted_keys.device)
     L.check(L.lib().iddgcn_similarity_triples(_stream(), n, N, int(relation), int(start), _ptr(sorted_keys),
                                               _ptr(out)), "similarity_triples")
+    return out
+
+
+# -- negative sampling (include/iddgcn_sampling.h) -----------------------------------------------
+def mt19937_words(seed, n, device):
+    """The first n words of np.random.seed(seed)'s MT19937 stream (tempered uint32, as int32 bits)."""
+    state = torch.empty(625, dtype=_I32, device=device)
+    L.check(L.lib().iddgcn_mt19937_seed(_stream(), int(seed), _ptr(state)), "mt19937_seed")
+    out = torch.empty(max(int(n), 1), dtype=_I32, device=device)
+    L.check(L.lib().iddgcn_mt19937_generate(_stream(), _ptr(state), int(n), _ptr(out)), "mt19937_generate")
+    return out[:int(n)]
+
+
+def negative_samples(triples, num_entities, seed):
+    """utils1.generate_negative_samples_np (utils1.py:646-655) on the GPU, bit-exact: triples (M, 3)
+    int64 GPU tensor -> (M, 3) int64 negatives.  Host synchronisations: one per round of entity words
+    (normally one)."""
+    _req(triples, _I64, None, "triples")
+    if triples.dim() != 2 or triples.shape[1] != 3:
+        raise L.IddgcnError(f"triples must be (M, 3), got {tuple(triples.shape)}")
+    N = int(num_entities)
+    if not 1 <= N <= 2 ** 31 - 1:
+        raise L.IddgcnError("num_entities must be in [1, 2^31)")
+    if not 0 <= int(seed) <= 2 ** 32 - 1:
+        raise L.IddgcnError("seed must be between 0 and 2**32 - 1 (np.random.seed)")
+    lib, dev, M = L.lib(), triples.device, triples.shape[0]
+    out = torch.empty(M, 3, dtype=_I64, device=dev)
+    if M == 0:
+        return out
+    state = torch.empty(625, dtype=_I32, device=dev)
+    L.check(lib.iddgcn_mt19937_seed(_stream(), int(seed), _ptr(state)), "mt19937_seed")
+    cond = torch.empty(M, dtype=_I32, device=dev)
+    L.check(lib.iddgcn_mt19937_generate(_stream(), _ptr(state), M, _ptr(cond)), "mt19937_generate")
+    ent = None
+    if N > 1:
+        rng = N - 1
+        accept = (rng + 1) / (int(lib.iddgcn_randint_mask(rng)) + 1)       # > 1/2
+        words = torch.empty(0, dtype=_I32, device=dev)
+        ent = torch.empty(M, dtype=_I32, device=dev)
+        need = M
+        while True:
+            more = int(need / accept * 1.01) + 4096
+            new = torch.empty(more, dtype=_I32, device=dev)
+            L.check(lib.iddgcn_mt19937_generate(_stream(), _ptr(state), more, _ptr(new)), "mt19937_generate")
+            words = torch.cat([words, new]) if words.numel() else new
+            nc = int(lib.iddgcn_accept_chunks(words.numel()))
+            counts = torch.empty(nc, dtype=_I32, device=dev)
+            offs = torch.empty(nc + 1, dtype=_I64, device=dev)
+            L.check(lib.iddgcn_masked_accept(_stream(), _ptr(words), words.numel(), rng, M, _ptr(counts), _ptr(offs),
+                                             _ptr(ent)), "masked_accept")
+            got = int(offs[nc].item())
+            if got >= M:
+                break
+            need = M - got
+    L.check(lib.iddgcn_assemble_negatives(_stream(), M, _ptr(triples), _ptr(cond), _ptr(ent), _ptr(out)),
+            "assemble_negatives")
     return out

@@ -82,9 +82,17 @@ typedef struct {
     const float* V; const int* v_idx;
     long long v_rel_stride, v_row_stride;
     int act; const float* aux;
-    int v_runs_max;       /* ABI 2: bound on runs of equal v_idx per 32-row block, 0 = unknown */
+    int v_runs_max;       /* bound on runs of equal v_idx per aligned 32-row block, 0 = unknown (the
+                             D = 256 x^1 recompute, IDDGCN_ACT_DSIGMOID_COMBINE, needs it) */
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
+
+/* Which kernel iddgcn_rowgemm_f32 would run for these arguments (a test / benchmark hook; nothing is
+ * launched): 300 + 10*NV + aux + 2*coef + 4*recompute for the D = 256 v3 pipeline (NV = gathered V
+ * tables: 1, 2, or capacity 4 / 8 for R <= 8, whose LDS slabs keep 7 distinct V rows per 32-row tile
+ * and read further ones from L2), 200 for the v2 LDS-DMA row GEMM, 100 for the register-staged kernel
+ * (any D, any V order), -1 for an invalid D. */
+int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* args);
 
 /* Select the D=256 GEMM pipelines (host-side switch for A/B tests and benchmarks;
  * all paths are bitwise identical): 0 (default) = staggered v3 row GEMM + LDS-DMA TN GEMM,
@@ -222,8 +230,8 @@ int iddgcn_reduce_slabs_f32(void* stream, int n_slabs, long long n, const float*
                             float* out, int accumulate, float scale);
 
 /* Up to 16 independent iddgcn_rowgemm_f32 calls of one width D (e.g. the per-relation, per-layer
- * node projections A_r·E·K_r of IDDGCN.py:71-77) in ONE launch for D < 256; at D = 256 the entries
- * run one after another on the pipelined kernels. */
+ * node projections A_r·E·K_r of IDDGCN.py:71-77) in ONE launch (blockIdx.y = entry); at D = 256 when
+ * every entry maps to the same v3 variant (iddgcn_rowgemm_kernel_id), else one launch per entry. */
 int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* args, int n);
 
 /* Keras-2.7 Adam, one tensor (IDDGCN.py:174,392).  sparse_form=0: TF ApplyAdam

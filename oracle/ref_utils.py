@@ -62,25 +62,71 @@ def get_y_true(X_test_pos, X_test_rule):
     return (merged['_merge'] == 'both').astype(int).values
 
 
+def _merge_left_only(frame, sub):
+    """pd.merge(frame, sub, how='left', indicator=True) rows marked 'left_only', as the reference
+    computes the training side of its cold-start splits (utils1.py:767-769)."""
+    m = pd.merge(frame, sub, how='left', indicator=True)
+    return m[m['_merge'] == 'left_only'].drop('_merge', axis=1).astype(int)
+
+
+def _cold_fold(frame, nodes, mode3):
+    """utils1.py:762-804 / 817-865 for one fold: rows touching ``nodes`` are the test side; mode 3 then
+    halves the other endpoints of those rows between test and train."""
+    pre_test = frame[(frame['obj'].isin(nodes)) | (frame['sbj'].isin(nodes))]
+    pre_train = _merge_left_only(frame, pre_test)
+    if not mode3:
+        return pre_train, pre_test.astype(int)
+    new_node = list(np.setdiff1d(np.unique(pre_test[['obj', 'sbj']].values), nodes))
+    nt, ntr = new_node[:len(new_node) // 2], new_node[len(new_node) // 2:]
+    test = pre_test[~pre_test['obj'].isin(nt) & ~pre_test['sbj'].isin(nt)].astype(int)
+    train = pre_train[~pre_train['obj'].isin(ntr) & ~pre_train['sbj'].isin(ntr)].astype(int)
+    return train, test
+
+
 def split_pos_triple_into_folds(dc, cc, dd, num_folds, seed, mode=0):
-    """utils1.py:741-755 (mode 0 only — the mode the bundled folds use)."""
-    if mode != 0:
-        raise NotImplementedError("only mode 0 (the bundled split) is restated")
+    """utils1.py:741-807 (all four modes)."""
     dc = dc.sample(frac=1, random_state=seed).reset_index(drop=True)
     cc = cc.sample(frac=1, random_state=seed).reset_index(drop=True)
     dd = dd.sample(frac=1, random_state=seed).reset_index(drop=True)
-    cc_dd = pd.concat([cc, dd], axis=0)
-    splits = []
-    for tr, te in KFold(n_splits=num_folds).split(dc):
-        splits.append((pd.concat([dc.iloc[tr], cc_dd], axis=0), dc.iloc[te]))
-    return splits
+    if mode == 0:
+        cc_dd = pd.concat([cc, dd], axis=0)
+        splits = []
+        for tr, te in KFold(n_splits=num_folds).split(dc):
+            splits.append((pd.concat([dc.iloc[tr], cc_dd], axis=0), dc.iloc[te]))
+        return splits
+    allt = pd.concat([dc, dd, cc], axis=0).astype(int)
+    out = []
+    for i in range(num_folds):
+        if mode == 1:
+            lf = 660 // num_folds
+            nodes = range(int(lf * i), int(lf * (i + 1)))
+        elif mode == 2:
+            lf = 157 / num_folds
+            nodes = range(int(lf * i + 660), int(lf * (i + 1) + 660))
+        else:
+            lf = 660 / num_folds
+            nodes = range(int(lf * i), int(lf * (i + 1)))
+        out.append(_cold_fold(allt, nodes, mode not in (1, 2)))
+    return out
 
 
 def split_neg_triple_into_folds(dc, num_folds, seed, mode=0):
-    """utils1.py:808-815 (mode 0)."""
-    if mode != 0:
-        raise NotImplementedError("only mode 0 (the bundled split) is restated")
-    return [(dc.iloc[tr], dc.iloc[te]) for tr, te in KFold(n_splits=num_folds).split(dc)]
+    """utils1.py:808-867 (all four modes)."""
+    if mode == 0:
+        return [(dc.iloc[tr], dc.iloc[te]) for tr, te in KFold(n_splits=num_folds).split(dc)]
+    out = []
+    for i in range(num_folds):
+        if mode == 1:
+            lf = 477 // num_folds
+            nodes = range(int(lf * i), int(lf * (i + 1)))
+        elif mode == 2:
+            lf = 157 / num_folds
+            nodes = range(int(lf * i + 477), int(lf * (i + 1) + 477))
+        else:
+            lf = 477 / num_folds
+            nodes = range(int(lf * i), int(lf * (i + 1)))
+        out.append(_cold_fold(dc, nodes, mode not in (1, 2)))
+    return out
 
 
 def make_fold_files(data_dir, fold, seed=89, num_splits=5):

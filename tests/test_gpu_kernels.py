@@ -741,3 +741,105 @@ def test_gemm_tn_dma_path_bitwise_equals_register_path(M, cuda):
             L.lib().iddgcn_set_rowgemm_path(old)
     assert torch.equal(out[0], out[1])
     close(out[0], A.double().t() @ B.double(), 2e-6 * np.sqrt(M))
+
+
+def _tail_runs(lengths, M):
+    """Sorted row indices built from consecutive runs of the given lengths (tail-sorted edges)."""
+    idx = torch.repeat_interleave(torch.arange(len(lengths)), torch.as_tensor(lengths))[:M]
+    return idx
+
+
+def _runs32(idx):
+    M = idx.numel()
+    start = torch.ones(M, dtype=torch.int64)
+    start[1:] = (idx[1:] != idx[:-1]).long()
+    start[0::32] = 1
+    pad = torch.zeros((M + 31) // 32 * 32, dtype=torch.int64)
+    pad[:M] = start
+    return int(pad.view(-1, 32).sum(1).max())
+
+
+@pytest.mark.parametrize("R", [3, 4, 5, 8])
+@pytest.mark.parametrize("gm", ["exact", "split"])
+@pytest.mark.parametrize("order", ["tail_runs", "structured", "identity", "random"])
+def test_rowgemm256_many_relations_gather(R, gm, order, cuda):
+    """The D=256 row GEMM with a gathered combine of R > 2 relations (BASELINE config 5: R = 8): capped
+    gather slabs (7 distinct V rows per relation per 32-row tile in LDS, further ones read from L2),
+    run-time R below the slot capacity (R = 3, 5).  Row orders: tail-sorted runs (the edge forward),
+    tiles with 1..32 runs, identity rows (the node-level head chain: 32 distinct rows per tile) and
+    random rows.  vs fp64: exact path 2e-5, split path <= 2x the exact path's error."""
+    g = torch.Generator().manual_seed(100 + R + len(order))
+    D, N, M = 256, 4000, 30_000 + 5
+    if order == "tail_runs":
+        t = _tail_runs(torch.randint(6, 60, (N,), generator=g), M)
+    elif order == "structured":
+        t = _run_structured_idx(M, N, g)
+    elif order == "identity":
+        N = M
+        t = None
+    else:
+        t = torch.randint(0, N, (M,), generator=g)
+    A = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
+    S = (torch.randn(D, D, generator=g, dtype=torch.float64) / 16).to(cuda)
+    W = torch.rand(M, R, generator=g, dtype=torch.float64).to(cuda)
+    P = torch.randn(R, N, D, generator=g, dtype=torch.float64).to(cuda)
+    rows = torch.arange(M, device=cuda) if t is None else t.to(cuda)
+    ref = torch.sigmoid(A @ S + sum(W[:, r:r + 1] * P[r][rows] for r in range(R)))
+    kw = dict(coef=W.float(), V=P.float(), v_idx=None if t is None else rows.int(), v_rel_stride=N * D,
+              act=L.ACT_SIGMOID)
+    errs = {}
+    for mode in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16) if gm == "split" else (L.GEMM_EXACT_F32,):
+        with _gemm_mode(mode):
+            C = torch.empty(M, D, device=cuda)
+            assert ops.rowgemm_kernel_id(A.float(), S.float(), C, **kw) == 300 + 10 * (4 if R <= 4 else 8) + 2
+            ops.rowgemm(A.float(), S.float(), C, **kw)
+        errs[mode] = _maxrel(C, ref)
+    assert errs[L.GEMM_EXACT_F32] <= 2e-5, errs
+    if gm == "split":
+        assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
+
+
+@pytest.mark.parametrize("R", [4, 8])
+@pytest.mark.parametrize("gm", ["exact", "split"])
+def test_rowgemm256_rank_update_many_relations(R, gm, cuda):
+    """D=256 node-level head backward with R > 2 (broadcast V rows, up to 8 coefficients per row):
+    C = (C + dO·S^T + dz·Wa^T) * X(1-X), on the v3 kernel."""
+    g = torch.Generator().manual_seed(7 * R)
+    D, M = 256, 9001
+    dO, S = rnd(M, D, dev=cuda, gen=g), rnd(D, D, dev=cuda, gen=g, scale=1 / 16)
+    dz, Wa = rnd(M, R, dev=cuda, gen=g), rnd(D, R, dev=cuda, gen=g)
+    X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
+    C0 = rnd(M, D, dev=cuda, gen=g)
+    ref = (C0 + dO @ S.t() + dz @ Wa.t()) * X * (1 - X)
+    kw = dict(b_trans=True, accumulate=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D,
+              v_row_stride=0, act=L.ACT_DSIGMOID, aux=X.float())
+    with _gemm_mode(L.GEMM_SPLIT_F16 if gm == "split" else L.GEMM_EXACT_F32):
+        C = C0.float().clone()
+        assert ops.rowgemm_kernel_id(dO.float(), S.float(), C, **kw) == 300 + 2 + 1
+        ops.rowgemm(dO.float(), S.float(), C, **kw)
+    assert _maxrel(C, ref) <= 2e-5
+
+
+@pytest.mark.parametrize("gm", ["exact", "split"])
+def test_rowgemm256_batched_one_launch_bitwise(gm, cuda):
+    """D=256 batches whose entries share a v3 variant run as ONE launch (blockIdx.y = entry), bitwise
+    equal to one call per entry: ragged row counts (1 row, an empty entry, 100k rows), plain
+    projections and transposed-accumulate ones."""
+    g = torch.Generator().manual_seed(5)
+    D = 256
+    for kw in (dict(), dict(b_trans=True, accumulate=True)):
+        calls = []
+        for M in [5000, 1, 0, 100_003, 777, 32, 4096]:
+            A = torch.randn(max(M, 1), D, generator=g).to(cuda)
+            B = (torch.randn(D, D, generator=g) / 16).to(cuda)
+            calls.append((A, B, torch.randn(M, D, generator=g).to(cuda)))
+        with _gemm_mode(L.GEMM_SPLIT_F16 if gm == "split" else L.GEMM_EXACT_F32):
+            single = []
+            for A, B, C0 in calls:
+                C = C0.clone()
+                ops.rowgemm(A, B, C, M=C.shape[0], **kw)
+                single.append(C)
+            outs = [C0.clone() for _, _, C0 in calls]
+            ops.rowgemm_batched([(A, B, C, dict(kw, M=C.shape[0])) for (A, B, _), C in zip(calls, outs)])
+        for a, b in zip(single, outs):
+            assert torch.equal(a, b)

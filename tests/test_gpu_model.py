@@ -198,6 +198,46 @@ def test_wide_step_parity_vs_oracle(D, R, gemm, cuda):
     np.testing.assert_allclose(out["logits"], logits, rtol=0, atol=1e-4)
 
 
+@pytest.mark.parametrize("R,gemm", [(3, "split"), (4, "exact"), (8, "split"), (8, "exact")])
+def test_many_relations_wide_step_vs_oracle(R, gemm, cuda):
+    """D=256 with R > 2 relations (BASELINE config 5 has 8): the forward edge GEMM runs the capped-slab
+    v3 kernel (asserted), the backward its broadcast-coefficient form, the node-level head chain the
+    capped kernel with most V rows from L2; one full step vs the float64 oracle at the non-saturating
+    bars, plus the logits at 1e-4."""
+    from iddgcn_amd import _lib as L
+    from iddgcn_amd import ops
+    N, D = 600, 256
+    pos, neg = synthetic_graph(N, R, 12000, seed=31)
+    neg = neg[:6000]
+    rng = np.random.default_rng(R)
+    params = {"E": rng.standard_normal((N, D)) / np.sqrt(D)}
+    for l in (1, 2, 3):
+        params[f"K{l}"] = rng.standard_normal((R, D, D)) / D
+        params[f"S{l}"] = rng.standard_normal((D, D)) / np.sqrt(D)
+        params[f"relw{l}"] = rng.uniform(-.05, .05, R)
+        params[f"Wa{l}"] = rng.standard_normal((D, R)) / np.sqrt(D)
+        params[f"ba{l}"] = rng.standard_normal(R) * 0.1
+    params["rel"] = rng.standard_normal((R, D))
+    params = {k: v.astype(np.float32) for k, v in params.items()}
+    adj = get_adj_coo(pos, N, R)
+    loss, scores, grads = train_step_grads(params, pos, neg, adj, N)
+    _, logits, _ = forward_detail(params, np.concatenate([pos, neg]), adj, N)
+    out = run_step(params, pos, neg, N, R, D, cuda, gemm=gemm)
+    assert abs(out["loss"] - loss) <= 1e-5 * loss
+    np.testing.assert_allclose(out["scores"], scores, rtol=0, atol=1e-5)
+    np.testing.assert_allclose(out["logits"], logits, rtol=0, atol=1e-4)
+    grad_check(out["grads"], grads, 2e-4)
+    # the forward edge GEMM of this step takes the capped-slab v3 kernel
+    eng = Engine(N, R, D, cuda, gemm=gemm)
+    ed = eng.edges(np.concatenate([pos, neg]))
+    x = torch.empty(ed.T, D, device=cuda)
+    w = torch.empty(ed.T, R, device=cuda)
+    Pn = torch.empty(R, N, D, device=cuda)
+    kid = ops.rowgemm_kernel_id(x, torch.empty(D, D, device=cuda), x, coef=w, V=Pn, v_idx=ed.t, v_rel_stride=N * D,
+                                act=L.ACT_SIGMOID)
+    assert kid == 300 + 10 * (4 if R <= 4 else 8) + 2, kid
+
+
 @pytest.mark.parametrize("gemm", ["split", "exact"])
 def test_x1_recompute_step_vs_oracle(gemm, cuda):
     """D=256 with dense tail runs (30 scored edges per tail, <= 8 runs per 32-edge block), so the

@@ -14,8 +14,9 @@ from tests.conftest import ROOT
 
 
 def header_symbols():
-    src = "".join(open(os.path.join(ROOT, "include", f)).read() for f in ("iddgcn.h", "iddgcn_graph.h", "iddgcn_similarity.h"))
-    return sorted(set(re.findall(r"^\s*(?:int|long long)\s+(iddgcn_\w+)\s*\(", src, flags=re.M)))
+    import glob
+    src = "".join(open(f).read() for f in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
+    return sorted(set(re.findall(r"^\s*(?:int|long long|uint32_t)\s+(iddgcn_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_library_exports_every_header_symbol():
