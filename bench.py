@@ -46,13 +46,16 @@ GEMM_NOTE = {
 }
 # the arithmetic the path computes in, per GEMM mode (the bench line's "dtype")
 DTYPE = {"split": "f32 (D=256 GEMMs on split-fp16x2 operands, fp32 accumulate)", "exact": "f32"}
+DTYPE_BF16 = ("bf16 edge tables (x^l, do^l) with bf16 MFMA for the edge GEMMs (weights as bf16 hi+lo), fp32 node "
+              "tables, accumulation and epilogues (perf-only mode, BASELINE config 5)")
 
 CONFIGS = {
     2: dict(name="synthetic-fold0-shape", N=845, R=4, M=37_510, D=64, scaling="weak"),
     3: dict(name="synthetic-3", N=100_000, R=2, M=2_000_000, D=256, scaling="weak"),
     4: dict(name="synthetic-4", N=1_000_000, R=2, M=20_000_000, D=256, scaling="strong"),
     # 40M positives, 10M negatives (one per 4 positives)
-    5: dict(name="synthetic-5", N=1_000_000, R=8, M=40_000_000, D=256, scaling="strong", neg_every=4),
+    5: dict(name="synthetic-5", N=1_000_000, R=8, M=40_000_000, D=256, scaling="strong", neg_every=4,
+            features="bf16"),
 }
 
 
@@ -80,20 +83,26 @@ def launch_ranks(args):
     return None
 
 
-def kernel_roofline(name, N, R, D, T, gemm, avg_ms):
+def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4):
     """Roofline of one edge-level GEMM launch.
 
     flops: 2*D^2*T algorithmic (x3 f16 MFMA instructions on the f16 peak in split mode);
     bytes (algorithmic, fp32): fwd reads x^{l-1}, writes x^l, reads W[h_e] (R per edge), t_e and the
     distinct P_r rows (R*N*D once); bwd reads do and the sigma' operand x, writes do' (the layer-2 bwd,
     "rec", rebuilds x^1 from the distinct ES1 / P^1 rows and W^1[h_e] instead of reading it); dS reads
-    x and do.  bound = whichever roofline time is larger."""
+    x and do (eb = bytes per edge-table element: 4, or 2 in the bf16-feature mode, whose GEMMs run 2 bf16
+    MFMAs per k-step).  bound = whichever roofline time is larger."""
     flops = 2.0 * D * D * T
-    nbytes = {"tail_fwd_gemm": 8.0 * D * T + 4.0 * R * T + 4.0 * T + 4.0 * R * N * D,
-              "tail_bwd_gemm": 12.0 * D * T,
-              "tail_bwd_rec_gemm": 8.0 * D * T + 4.0 * R * T + 4.0 * T + 4.0 * (R + 1) * N * D,
-              "tail_dS_tn": 8.0 * D * T}[name]
-    hw_flops, peak_f = (3 * flops, MFMA_F16_PEAK_TFLOPS) if gemm == "split" else (flops, MFMA_F32_PEAK_TFLOPS)
+    nbytes = {"tail_fwd_gemm": 2.0 * eb * D * T + 4.0 * R * T + 4.0 * T + 4.0 * R * N * D,
+              "tail_bwd_gemm": 3.0 * eb * D * T,
+              "tail_bwd_rec_gemm": 2.0 * eb * D * T + 4.0 * R * T + 4.0 * T + 4.0 * (R + 1) * N * D,
+              "tail_dS_tn": 2.0 * eb * D * T}[name]
+    if eb == 2:
+        hw_flops, peak_f = 2 * flops, MFMA_F16_PEAK_TFLOPS
+    elif gemm == "split":
+        hw_flops, peak_f = 3 * flops, MFMA_F16_PEAK_TFLOPS
+    else:
+        hw_flops, peak_f = flops, MFMA_F32_PEAK_TFLOPS
     t_mfma = hw_flops / (peak_f * 1e12)
     t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
     s = avg_ms * 1e-3
@@ -226,7 +235,9 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     tri = np.concatenate([pos[lo:min(hi, npos)], neg[max(lo - npos, 0):max(hi - npos, 0)]])
     lab = np.concatenate([np.ones(max(0, min(hi, npos) - lo), np.float32),
                           np.zeros(max(0, hi - max(lo, npos)), np.float32)])
-    eng = Engine(N, R, D, dev, gemm=gemm, recompute_x1=args.recompute_x1, fuse_tail_seg=args.fuse_tail_seg)
+    feat = args.features or cfg.get("features", "f32")
+    eng = Engine(N, R, D, dev, gemm=gemm, recompute_x1=args.recompute_x1, fuse_tail_seg=args.fuse_tail_seg,
+                 features=feat)
     adj = get_adj_mats(pos, N, R, device=dev)            # device graph build (bit-identical to the host's)
     ed = eng.edges(tri, lab)
     del pos, neg, tri, lab
@@ -262,12 +273,13 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
 
     elapsed, loss_val, probe = timed_run(gemm, probe_kernels)
     out = {"value": M / (elapsed / args.steps), "ms_per_step": elapsed / args.steps * 1e3,
-           "scaling": cfg["scaling"], "dtype": DTYPE[gemm], "gemm_operands": GEMM_NOTE[gemm],
+           "scaling": cfg["scaling"], "dtype": DTYPE_BF16 if feat == "bf16" else DTYPE[gemm],
+           "gemm_operands": GEMM_NOTE[gemm] + ("; edge GEMMs bf16 (features=bf16)" if feat == "bf16" else ""),
            "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
                       "scored_edges": T, "scored_edges_per_gpu": ed.T, "feat_dim": D,
-                      "parallelism": f"edge-dp{world}", "gemm": gemm},
+                      "parallelism": f"edge-dp{world}", "gemm": gemm, "features": feat},
            "scored_edges_per_s": T / (elapsed / args.steps), "loss": loss_val}
-    if other_mode:
+    if other_mode and feat == "f32":
         mode2 = "exact" if gemm == "split" else "split"
         el2, loss2, _ = timed_run(mode2, False)
         out["other_gemm_mode"] = {"gemm": mode2, "dtype": DTYPE[mode2], "value": M / (el2 / args.steps),
@@ -277,7 +289,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         # of the MFMA time (hardware MFMA work on the mode's peak) and the HBM time (algorithmic bytes)
         kt = {k: [a.elapsed_time(b) for a, b in v] for k, v in probe.items()}
         dom = max(kt, key=lambda k: sum(kt[k]))
-        rl = kernel_roofline(dom, N, R, D, ed.T, gemm, statistics.mean(kt[dom]))
+        rl = kernel_roofline(dom, N, R, D, ed.T, gemm, statistics.mean(kt[dom]), eb=2 if feat == "bf16" else 4)
         rl["traffic"], rl["traffic_source"] = pmc_traffic(dom, gemm, cfg["name"], world)
         rl["box_stream_GBs"] = stream_probe(torch, dev, ed.T, D)
         out["kernel_ms_per_step"] = {k: sum(v) / args.steps for k, v in kt.items()}
@@ -296,6 +308,8 @@ def main():
     ap.add_argument("--also", type=int, nargs="*", default=[], choices=sorted(CONFIGS),
                     help="further workloads timed in the same run, reported under 'also'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--features", default=None, choices=["f32", "bf16"],
+                    help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
     ap.add_argument("--gemm", default="split", choices=["split", "exact"],
                     help="operand precision of the D=256 MFMA GEMMs (the other mode is timed too)")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")

@@ -68,6 +68,14 @@ SIGNATURES = {
     "iddgcn_gather_rows_f32": (ci, [vp, cll, ci, vp, vp, vp]),
     "iddgcn_reduce_slabs_f32": (ci, [vp, ci, cll, vp, vp, ci, cf]),
     "iddgcn_adam_f32": (ci, [vp, cll, vp, vp, vp, vp, cf, cf, cf, cf, ci]),
+    # bf16-feature mode
+    "iddgcn_rowgemm_bf16": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
+    "iddgcn_gemm_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
+    "iddgcn_combine_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
+    "iddgcn_distmult_bce_bf16": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci]),
+    "iddgcn_distmult_bce_heads_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
+                                            vp, ci]),
+    "iddgcn_tail_seg_reduce_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, cll, vp, cll, vp, vp]),
     # include/iddgcn_graph.h
     "iddgcn_radix_sort_workspace": (cll, [cll, ci]),
     "iddgcn_radix_sort_pairs": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, cll]),

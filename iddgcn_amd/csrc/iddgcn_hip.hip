@@ -23,6 +23,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 #define MAX_R 8
 #define EPS_BCE 1e-7f
@@ -157,6 +161,26 @@ __device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+// bf16 edge tables (the bf16-feature mode): 4 values = 8 bytes, round-to-nearest-even on store
+__device__ __forceinline__ f32x4 bf4_to_f32(bf16x4 v) {
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+__device__ __forceinline__ bf16x4 f32_to_bf4(f32x4 v) {
+    return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+__device__ __forceinline__ f32x4 ld4bf(const __bf16* p) { return bf4_to_f32(*reinterpret_cast<const bf16x4*>(p)); }
+__device__ __forceinline__ void st4bf(__bf16* p, f32x4 v) { *reinterpret_cast<bf16x4*>(p) = f32_to_bf4(v); }
+// 4 consecutive elements of an edge table that is fp32 or (BF) bf16, addressed in elements
+template <bool BF>
+__device__ __forceinline__ f32x4 ld4e(const float* base, long long idx) {
+    if constexpr (BF) return ld4bf(reinterpret_cast<const __bf16*>(base) + idx);
+    else return ld4(base + idx);
+}
+template <bool BF>
+__device__ __forceinline__ void st4e(float* base, long long idx, f32x4 v) {
+    if constexpr (BF) st4bf(reinterpret_cast<__bf16*>(base) + idx, v);
+    else st4(base + idx, v);
+}
 __device__ __forceinline__ f32x4 fma4(f32x4 a, f32x4 b, f32x4 c) {
     return f32x4{fmaf(a[0], b[0], c[0]), fmaf(a[1], b[1], c[1]), fmaf(a[2], b[2], c[2]), fmaf(a[3], b[3], c[3])};
 }
@@ -672,14 +696,23 @@ __device__ __forceinline__ float wave_max(float v) {             // max over the
 constexpr int REC_CAP = 8;
 // NV: gathered V tables (0 = none; 1, 2 = exactly R; 4, 8 = capacity for R <= NV, capped slabs).
 // Up to ROWGEMM_BATCH independent GEMMs of the same variant run in one launch: blockIdx.y = entry.
-template <int NV, bool AUX, bool HAS_COEF, bool X3, bool REC = false>
+// CW: broadcast V (NV = 0) with more than 2 coefficients per row (R <= 8); R <= 2 keeps the 2-slot
+// coefficient code (the wide form is 2.4x slower on the node-level head-chain backward at R = 2).
+// BF: the bf16-feature mode (perf only): A, the sigma' operand and C are bf16 edge tables (512-B rows;
+// A lands in the hi-plane slot of an LDS row as it is), the weights a bf16 hi + lo pair, two
+// v_mfma_f32_32x32x16_bf16 per k-step, fp32 accumulation and epilogue.  X3 must be set with it.
+template <int NV, bool AUX, bool HAS_COEF, bool X3, bool REC = false, bool CW = false, bool BF = false>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     using namespace r3;
     const RowGemmP p = pb.p[blockIdx.y];
+    static_assert(!BF || (X3 && !REC), "BF: the 16-bit A-plane pipeline, no recompute");
     static_assert(!REC || (NV >= 2 && NV <= 3 && !AUX && HAS_COEF), "REC: V_0 + coefficient-weighted V_1.., no aux");
     static_assert(REC || NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
     constexpr bool WIDE = !REC && NV > 2;              // capped slabs, run-time R <= NV
-    constexpr int NS = NV + (AUX ? 1 : 0);
+    // the sigma' slab: after the V slabs; BF keeps it out of slab 0, whose fp32 staging of the output
+    // would overwrite bf16 aux rows other lanes have not read yet (different row pitches)
+    constexpr int AUXS = (BF && NV == 0) ? 1 : NV;
+    constexpr int NS = AUX ? AUXS + 1 : NV;
     constexpr int NSL = NS > 1 ? NS : 1;               // slabs per wave (slab 0 also stages C)
     // Slab 0 holds 32 rows (it also stages the C tile); REC slabs r >= 1 hold REC_CAP rows, WIDE
     // slabs r >= 1 GATHER_CAP rows.
@@ -687,7 +720,8 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     constexpr int SLABC = CAPV * 32;
     constexpr int SLABS = SLAB + (NSL - 1) * SLABC;    // floats of all slabs of one wave
     // coefficient slots: 32 rows x R; up to 8 relations for WIDE and for broadcast V (NV = 0)
-    constexpr bool COEF_WIDE = WIDE || (NV == 0 && HAS_COEF);
+    static_assert(!CW || (NV == 0 && HAS_COEF), "CW: broadcast V rows only");
+    constexpr bool COEF_WIDE = WIDE || CW;
     constexpr int COEFN = COEF_WIDE ? COEF8 : COEF;
     constexpr int CFN = COEF_WIDE ? MAX_R : 2;         // coefficients each lane holds
     constexpr int WF = SLABS + COEFN + IDX + CMP + CINV;
@@ -721,6 +755,21 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             const int kk = 8 * (s >> 2) + 4 * h + (s & 3);
             breg[s] = p.b_trans ? p.B[(c0 + i) * D + kk] : p.B[kk * D + c0 + i];
         }
+    } else if constexpr (BF) {
+        // bf16 has fp32's exponent range: no scales; W = hi + lo, hi = bf16(W), lo = bf16(W - hi)
+#pragma unroll
+        for (int q = 0; q < D / 16; ++q) {
+            bf16x8 hv, lv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = 16 * q + 8 * h + e;
+                const float w = p.b_trans ? p.B[(c0 + i) * D + k] : p.B[k * D + c0 + i];
+                hv[e] = (__bf16)w;
+                lv[e] = (__bf16)(w - (float)hv[e]);
+            }
+            bhi[q] = __builtin_bit_cast(f16x8, hv);
+            blo[q] = __builtin_bit_cast(f16x8, lv);
+        }
     } else {
         auto bval = [&](int k) { return p.b_trans ? p.B[(c0 + i) * D + k] : p.B[k * D + c0 + i]; };
         float cm = 0.f;
@@ -743,7 +792,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // X3: the wave converts its own ROWS_PER_WAVE rows of A buffer bb in place, fp32 row ->
     // [hi plane 512 B | lo plane 512 B] (k-natural order), and records 1/scale per row
     auto convert_rows = [&](int bb) {
-        if constexpr (X3) {
+        if constexpr (X3 && !BF) {
             float* base = bufA + bb * A_FLOATS;
             f32x4 x[ROWS_PER_WAVE];
             float m[ROWS_PER_WAVE];
@@ -812,8 +861,14 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             const int r = wave * ROWS_PER_WAVE + j;
             const long long e = clampe(t * TR + r);
             const long long src = p.a_idx ? (long long)sa[j] : e;
-            const float* g = p.A + src * D + lane * 4;
-            __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * LDA), 16, 0, 0);
+            if constexpr (BF) {      // a 512-B bf16 row: 32 lanes, straight into the row's hi-plane slot
+                const char* g = reinterpret_cast<const char*>(p.A) + src * D * 2 + (lane & 31) * 16;
+                if (lane < 32)
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * LDA), 16, 0, 0);
+            } else {
+                const float* g = p.A + src * D + lane * 4;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * LDA), 16, 0, 0);
+            }
         }
     };
     // Slabs are [32 rows][32 cols] with the 16-B column groups of row r XOR-swizzled by
@@ -860,13 +915,23 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             }
         }
         if (AUX) {
+            if constexpr (BF) {      // bf16 sigma' rows: [32 rows][32 bf16], 64 B per row, 16 rows per DMA
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int row = 8 * k + (lane >> 3);
-                const int g = (lane & 7) ^ ((row >> 1) & 7);
-                const long long e = clampe(t * TR + row);
-                const float* gp = p.aux + e * D + c0 + g * 4;
-                __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + soff(NV) + k * 256), 16, 0, 0);
+                for (int k = 0; k < 2; ++k) {
+                    const int row = 16 * k + (lane >> 2);
+                    const long long e = clampe(t * TR + row);
+                    const char* gp = reinterpret_cast<const char*>(p.aux) + (e * D + c0 + (lane & 3) * 8) * 2;
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + soff(AUXS) + k * 256), 16, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int row = 8 * k + (lane >> 3);
+                    const int g = (lane & 7) ^ ((row >> 1) & 7);
+                    const long long e = clampe(t * TR + row);
+                    const float* gp = p.aux + e * D + c0 + g * 4;
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + soff(AUXS) + k * 256), 16, 0, 0);
+                }
             }
         }
         if (HAS_COEF) {
@@ -890,11 +955,13 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // rewrites exactly the slots it read), then re-read row-major for 4 buffer_store_dwordx4
     // per wave through a per-tile buffer resource whose range check drops rows past M.
     const int sw = (i >> 1) & 7;
+    constexpr int EB = BF ? 2 : 4;                     // bytes per edge-table element
     auto out_rsrc = [&](long long t) {
         const long long row0 = t * TR;
         const long long left = (long long)p.M - row0;
-        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
-        return __builtin_amdgcn_make_buffer_rsrc(p.C + row0 * D, (short)0, nbytes, 0x00020000);
+        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * EB);
+        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(p.C) + row0 * D * EB, (short)0, nbytes,
+                                                 0x00020000);
     };
     // stage phase: combine + activation into slab 0 (LDS only, plus the C loads of `accumulate`)
     auto epi_stage = [&](long long t, const f32x16& acc) {
@@ -920,8 +987,10 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             const int off = i * 32 + 4 * ((2 * j + h) ^ sw);
             const int col = c0 + 8 * j + 4 * h;
             f32x4 v = {acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
-            if (p.accumulate)
-                v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (i * D + col) * 4, 0, 0));
+            if constexpr (!BF) {
+                if (p.accumulate)
+                    v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (i * D + col) * 4, 0, 0));
+            }
             if constexpr (REC) {        // v *= x(1-x), x = sigmoid(V_0 + sum_r cf_r V_{r+1})
                 const int offv = vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
                 f32x4 xs = ld4(slabw + offv);
@@ -967,7 +1036,11 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
             } else if (p.act == IDDGCN_ACT_DSIGMOID) {
-                const f32x4 x = ld4(slabw + soff(NV) + off);
+                f32x4 x;
+                if constexpr (BF)
+                    x = ld4bf(reinterpret_cast<const __bf16*>(slabw + soff(AUXS)) + i * 32 + 8 * j + 4 * h);
+                else
+                    x = ld4(slabw + soff(AUXS) + off);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = v[q] * (x[q] * (1.0f - x[q]));
             }
@@ -986,7 +1059,11 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                 asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
                 continue;
             }
-            __builtin_amdgcn_raw_buffer_store_b128(o, rc, (row * D + c0 + cg * 4) * 4, 0, 0);
+            if constexpr (BF)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, f32_to_bf4(o)), rc,
+                                                      (row * D + c0 + cg * 4) * 2, 0, 0);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128(o, rc, (row * D + c0 + cg * 4) * 4, 0, 0);
         }
     };
     auto epilogue = [&](long long t, const f32x16& acc) {
@@ -1066,6 +1143,23 @@ _Pragma("unroll") \
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 3], a_cur[3], acc, 0, 0, 0); \
                     __builtin_amdgcn_sched_barrier(0); \
                     a_cur = a_nxt; \
+                } \
+            } else if constexpr (BF) { \
+                /* bf16 A fragments straight from the row; W hi and lo, one accumulator */ \
+_Pragma("unroll") \
+                for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
+                const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
+                f16x8 ah[2]; \
+                ah[0] = __builtin_bit_cast(f16x8, ld4(arow)); \
+_Pragma("unroll") \
+                for (int q = 0; q < D / 16; ++q) { \
+                    const int cu = q & 1; \
+                    if (q + 1 < D / 16) ah[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + 8 * (q + 1))); \
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, bhi[q]), \
+                                                                  __builtin_bit_cast(bf16x8, ah[cu]), acc, 0, 0, 0); \
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, blo[q]), \
+                                                                  __builtin_bit_cast(bf16x8, ah[cu]), acc, 0, 0, 0); \
+                    __builtin_amdgcn_sched_barrier(0); \
                 } \
             } else { \
                 f32x16 acc_hi, acc_lo; \
@@ -1631,6 +1725,106 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
     }
 }
 
+// ---------------------------------------------------------------------------
+// TN reduction GEMM, D = 256, bf16 operands (the bf16-feature mode): C = A^T B over bf16 edge tables,
+// same partial-slab contract as the fp32 TN kernels.  Per 32-row tile the 512-B bf16 rows of A and B
+// are DMA'd (32 lanes per row) into 1040-B LDS rows, then wave w transposes column block w of each
+// operand IN PLACE (32 rows x 32 bf16 = 2 KB, wave-private) so that column 32w+i lies k-contiguous in
+// row i's bytes [64w, 64w+64): an MFMA fragment (8 consecutive rows of one column) is one
+// ds_read_b128.  One v_mfma_f32_32x32x16_bf16 per (k-step, column block); fp32 accumulation.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void gemm_tn256_bf16_kernel(long long M, long long rows_per_block,
+                                                              const __bf16* __restrict__ A,
+                                                              const __bf16* __restrict__ B,
+                                                              float* __restrict__ slab) {
+    using namespace tn3;
+    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * TILE];      // [buf][A|B][TK][LDR]
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int i = lane & 31, h = lane >> 5;
+    f32x16 acc[8];
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[cj][j] = 0.f;
+    const long long r_beg = (long long)blockIdx.x * rows_per_block;
+    long long r_end = r_beg + rows_per_block;
+    if (r_end > M) r_end = M;
+    const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
+
+    auto stage = [&](long long t, int b) {          // wave w stages rows 4w..4w+3 of both operands
+        float* As = lds + (b * 2 + 0) * TILE;
+        float* Bs = lds + (b * 2 + 1) * TILE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = wave * 4 + j;
+            const long long e = r_beg + t * TK + r;
+            if (e < r_end) {
+                if (lane < 32) {
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)(A + e * D + lane * 8), (lds_vptr)(As + r * LDR), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)(B + e * D + lane * 8), (lds_vptr)(Bs + r * LDR), 16, 0, 0);
+                }
+            } else if (lane < 32) {
+                st4(As + r * LDR + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                st4(Bs + r * LDR + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+            }
+        }
+    };
+    // transpose column block `wave` of one bf16 tile in place (lane (i, h): column 32w+i, rows 16h..16h+15)
+    auto transpose_block = [&](float* T) {
+        const unsigned short* src = reinterpret_cast<const unsigned short*>(T);
+        s16x4 v[4];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            v[r >> 2][r & 3] = (short)src[(16 * h + r) * (LDR * 2) + 32 * wave + i];
+        char* seg = reinterpret_cast<char*>(T + i * LDR) + 64 * wave + 32 * h;
+        *reinterpret_cast<s16x4*>(seg) = v[0];
+        *reinterpret_cast<s16x4*>(seg + 8) = v[1];
+        *reinterpret_cast<s16x4*>(seg + 16) = v[2];
+        *reinterpret_cast<s16x4*>(seg + 24) = v[3];
+    };
+    auto transpose = [&](int b) {
+        transpose_block(lds + (b * 2 + 0) * TILE);
+        transpose_block(lds + (b * 2 + 1) * TILE);
+    };
+    if (nt > 0) {
+        stage(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        transpose(0);
+        __syncthreads();
+    }
+    int b = 0;
+    for (long long t = 0; t < nt; ++t, b ^= 1) {
+        if (t + 1 < nt) stage(t + 1, b ^ 1);
+        const char* Aseg = reinterpret_cast<const char*>(lds + (b * 2 + 0) * TILE + i * LDR) + 64 * wave;
+        const char* Bseg = reinterpret_cast<const char*>(lds + (b * 2 + 1) * TILE + i * LDR);
+#pragma unroll
+        for (int s = 0; s < TK / 16; ++s) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(Aseg + 32 * s + 16 * h);
+#pragma unroll
+            for (int cj = 0; cj < 8; ++cj) {
+                const bf16x8 bf = *reinterpret_cast<const bf16x8*>(Bseg + 64 * cj + 32 * s + 16 * h);
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[cj], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t + 1 < nt) {
+            transpose(b ^ 1);
+            __syncthreads();
+        }
+    }
+    float* out = slab + (long long)blockIdx.x * D * D;
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int row = 32 * wave + (j & 3) + 8 * (j >> 2) + 4 * h;
+            out[row * D + 32 * cj + i] = acc[cj][j];
+        }
+}
+
 // out[D][R] partial of A^T dz and colsum(dz) per block; slab row layout [(D+1)][R]
 template <int D>
 __global__ __launch_bounds__(D) void gemm_tn_narrow_kernel(long long M, long long rows_per_block, int R,
@@ -1671,47 +1865,62 @@ __global__ __launch_bounds__(256) void alpha_kernel(int M, int R, const float* _
                                                     const int* __restrict__ x_idx, const float* __restrict__ Wa,
                                                     const float* __restrict__ ba, float* __restrict__ S_out,
                                                     float* __restrict__ W_out) {
+    // persistent over rows: lane sub keeps its 4 rows of W_alpha (4 x R) in registers; the R dot
+    // products of a row are reduced together (multi_reduce: one butterfly for all relations)
     constexpr int LPR = D / 4;
-    const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    constexpr int K = LPR < MAX_R ? LPR : MAX_R;         // relations reduced per butterfly
     const int sub = threadIdx.x % LPR;
-    const bool live = row < M;
-    f32x4 x = {0.f, 0.f, 0.f, 0.f};
-    if (live) {
+    float wa[4][MAX_R];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r) wa[j][r] = r < R ? Wa[(sub * 4 + j) * R + r] : 0.f;
+    float bav[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) bav[r] = r < R ? ba[r] : 0.f;
+    const long long gstride = (long long)gridDim.x * (blockDim.x / LPR);
+    // the loop condition is uniform over a row's LPR lanes (the butterflies stay inside a group)
+    for (long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / LPR; row < M; row += gstride) {
         const long long src = x_idx ? (long long)x_idx[row] : row;
-        x = ld4(X + src * D + sub * 4);
+        const f32x4 x = ld4(X + src * D + sub * 4);
+        float z[MAX_R];
+#pragma unroll
+        for (int r0 = 0; r0 < MAX_R; r0 += K) {
+            float part[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const int r = r0 + q;
+                part[q] = 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) part[q] = fmaf(x[j], wa[j][r], part[q]);
+            }
+            const float tot = multi_reduce<LPR, K>(part, sub);     // lane sub: relation r0 + sub / (LPR / K)
+#pragma unroll
+            for (int q = 0; q < K; ++q) z[r0 + q] = __shfl(tot, (threadIdx.x & ~(LPR - 1) & 63) + q * (LPR / K), 64);
+        }
+        if (sub != 0) continue;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+            if (r < R) {
+                z[r] += bav[r];
+                mx = fmaxf(mx, z[r]);
+            }
+        float sum = 0.f;
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+            if (r < R) {
+                z[r] = expf(z[r] - mx);
+                sum += z[r];
+            }
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+            if (r < R) {
+                const float sm = z[r] / sum;
+                S_out[row * R + r] = sm;
+                W_out[row * R + r] = sigmoidf_(sm);
+            }
     }
-    float z[MAX_R];
-#pragma unroll
-    for (int r = 0; r < MAX_R; ++r) {
-        float part = 0.f;
-        if (r < R) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) part += x[j] * Wa[(sub * 4 + j) * R + r];
-        }
-        z[r] = group_sum<LPR>(part);
-    }
-    if (!live || sub != 0) return;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < MAX_R; ++r)
-        if (r < R) {
-            z[r] += ba[r];
-            mx = fmaxf(mx, z[r]);
-        }
-    float sum = 0.f;
-#pragma unroll
-    for (int r = 0; r < MAX_R; ++r)
-        if (r < R) {
-            z[r] = expf(z[r] - mx);
-            sum += z[r];
-        }
-#pragma unroll
-    for (int r = 0; r < MAX_R; ++r)
-        if (r < R) {
-            const float s = z[r] / sum;
-            S_out[row * R + r] = s;
-            W_out[row * R + r] = sigmoidf_(s);
-        }
 }
 
 // ---------------------------------------------------------------------------
@@ -1807,7 +2016,7 @@ __global__ __launch_bounds__(256) void combine_kernel(int M, const float* __rest
 // of are the ones already needed.  Per-edge indices/coefficients: one per lane, broadcast
 // with readlane.
 constexpr int RC_CH = 64;
-template <int R>
+template <int R, bool BF = false>
 __global__ __launch_bounds__(256) void run_combine256_kernel(int M, const float* __restrict__ Y,
                                                              const int* __restrict__ idx,
                                                              const float* __restrict__ coef,
@@ -1865,7 +2074,7 @@ __global__ __launch_bounds__(256) void run_combine256_kernel(int M, const float*
                 for (int r = 0; r < R; ++r) v += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cf[r]), j)) * pc[r];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
-                st4(out + (e0 + j) * D + lane * 4, v);
+                st4e<BF>(out, (e0 + j) * D + lane * 4, v);
             }
             yc = yn;
 #pragma unroll
@@ -1883,7 +2092,7 @@ __global__ __launch_bounds__(256) void run_combine256_kernel(int M, const float*
 // DistMult + Keras BCE + backward seed.  256-thread blocks, grid-stride over rows;
 // per-lane-group register partials for drel and loss, block-ordered reduction.
 // ---------------------------------------------------------------------------
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const float* __restrict__ Xh,
                                                        const int* __restrict__ h_idx, const float* __restrict__ Xt,
                                                        const int* __restrict__ t_idx, const int* __restrict__ r_idx,
@@ -1925,7 +2134,7 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
 #define DM_LOAD_ROWS(A, B, RHO, YY, RI)                                        \
     _Pragma("unroll") for (int u = 0; u < U; ++u) {                             \
         A[u] = ld4(Xh + (long long)hr[u] * D + sub * 4);                        \
-        B[u] = ld4(Xt + ti[u] * D + sub * 4);                                   \
+        B[u] = ld4e<BF>(Xt, ti[u] * D + sub * 4);                               \
         RHO[u] = ld4(rel + (long long)rr[u] * D + sub * 4);                     \
         YY[u] = yv[u];                                                          \
         RI[u] = rr[u];                                                          \
@@ -1970,7 +2179,7 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
             }
             f32x4 dx = (ds * rho[u]) * a[u];
             dx = dx * (b[u] * (1.0f - b[u]));
-            st4(do_out + e * D + sub * 4, dx);
+            st4e<BF>(do_out, e * D + sub * 4, dx);
             const f32x4 dre = ds * (a[u] * b[u]);
 #pragma unroll
             for (int r = 0; r < MAX_R; ++r)
@@ -2016,7 +2225,7 @@ __global__ __launch_bounds__(256) void distmult_kernel(long long T, int R, const
 // do_out may alias Xt (the engine writes do^3 over x^3): each element is read, then written, by
 // the same lane, and every edge is visited once.
 // ---------------------------------------------------------------------------
-template <int D, int RT>
+template <int D, int RT, bool BF = false>
 __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R, const int* __restrict__ seg_ptr,
                                                              const int* __restrict__ perm,
                                                              const float* __restrict__ Xh,
@@ -2047,7 +2256,11 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
     for (long long n0 = (long long)blockIdx.x * NPB; n0 < n_nodes; n0 += nstride) {
         const long long n = n0 + threadIdx.x / 64;
         const bool live = n < n_nodes;
-        const int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
+        int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
+        if constexpr (SLOTS == 1) {     // D = 256: the whole wave is one head, its edges wave-uniform
+            beg = __builtin_amdgcn_readfirstlane(beg);
+            end = __builtin_amdgcn_readfirstlane(end);
+        }
         const int len = end - beg;
         const f32x4 a = live ? ld4(Xh + n * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -2057,7 +2270,10 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
             const int k = (it * SLOTS + slot) * U;
             long long e[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) e[u] = (k + u < len) ? (long long)perm[beg + k + u] : -1;
+            for (int u = 0; u < U; ++u) {
+                e[u] = (k + u < len) ? (long long)perm[beg + k + u] : -1;
+                if constexpr (SLOTS == 1) e[u] = __builtin_amdgcn_readfirstlane((int)e[u]);   // scalar loads below
+            }
             int rr[U];
             float yy[U];
             f32x4 b[U], rho[U];
@@ -2066,7 +2282,8 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 const bool ok = e[u] >= 0;
                 rr[u] = ok ? r_idx[e[u]] : 0;
                 yy[u] = (ok && y) ? y[e[u]] : 0.f;
-                b[u] = ok ? ld4(Xt + e[u] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (SLOTS == 1) rr[u] = __builtin_amdgcn_readfirstlane(rr[u]);
+                b[u] = ok ? ld4e<BF>(Xt, e[u] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) rho[u] = ld4(rel + (long long)rr[u] * D + sub * 4);
@@ -2101,7 +2318,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 }
                 f32x4 dx = (ds * rho[u]) * a;
                 dx = dx * (b[u] * (1.0f - b[u]));
-                st4(do_out + e[u] * D + sub * 4, dx);
+                st4e<BF>(do_out, e[u] * D + sub * 4, dx);
                 const f32x4 dre = ds * (a * b[u]);
 #pragma unroll
                 for (int r = 0; r < RT; ++r)
@@ -2186,7 +2403,7 @@ __global__ __launch_bounds__(256) void seg_gather_reduce_kernel(int n_nodes, con
 // leave most of the chip idle behind a few long serial segments); the slot partials are summed
 // in fixed order (xor-shuffles) at the end, so results stay deterministic.
 // ---------------------------------------------------------------------------
-template <int D, int R>
+template <int D, int R, bool BF = false>
 __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const int* __restrict__ seg_ptr,
                                                               const int* __restrict__ h_idx,
                                                               const float* __restrict__ W,
@@ -2204,7 +2421,11 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     const int sub = threadIdx.x % LPR;
     const int slot = (threadIdx.x % 64) / LPR;
     const bool live = n < n_nodes;
-    const int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
+    int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
+    if constexpr (SLOTS == 1) {      // D = 256: one node per wave, its edge rows (and W rows) wave-uniform
+        beg = __builtin_amdgcn_readfirstlane(beg);
+        end = __builtin_amdgcn_readfirstlane(end);
+    }
     f32x4 pr[R], acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -2225,7 +2446,8 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             const bool a = k + u < len;
             // h_idx == NULL: W is already per edge (W[e][r], gathered once per layer)
             hh[u] = a ? (h_idx ? h_idx[beg + k + u] : beg + k + u) : 0;
-            d[u] = a ? ld4(dO + (long long)(beg + k + u) * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (SLOTS == 1) hh[u] = __builtin_amdgcn_readfirstlane(hh[u]);     // scalar W loads
+            d[u] = a ? ld4e<BF>(dO, (long long)(beg + k + u) * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
         float w[U][R];
 #pragma unroll
@@ -2306,6 +2528,17 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
     }
     const int beg = (live && hseg_ptr) ? hseg_ptr[n] : 0;
     const int end = (live && hseg_ptr) ? hseg_ptr[n + 1] : 0;
+    // edge contributions, one pass over the head segment for every relation: lane sub takes
+    // k = beg+sub, beg+sub+LPR, ... and reads the edge's R contiguous dWedge values
+    float ep[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) ep[r] = 0.f;
+    for (int k = beg + sub; k < end; k += LPR) {
+        const float* dwe = dWedge + (long long)hperm[k] * R;
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+            if (r < R) ep[r] += dwe[r];
+    }
     float dw[MAX_R];
 #pragma unroll
     for (int r = 0; r < MAX_R; ++r) {
@@ -2315,12 +2548,9 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
                 const f32x4 q = d * ld4(P + r * p_rel_stride + n * D + sub * 4);
                 part = q[0] + q[1] + q[2] + q[3];
             }
-            // edge contributions: lane sub takes k = beg+sub, beg+sub+LPR, ...
-            float ep = 0.f;
-            for (int k = beg + sub; k < end; k += LPR) ep += dWedge[(long long)hperm[k] * R + r];
-            part += ep;
+            part += ep[r];
         }
-        dw[r] = group_sum<LPR>(part);
+        dw[r] = r < R ? group_sum<LPR>(part) : 0.f;
     }
     if (!live) return;
     float s[MAX_R], w[MAX_R], dsv[MAX_R];
@@ -2402,6 +2632,7 @@ __global__ void step_advance_kernel(int* __restrict__ step, float* __restrict__ 
 struct V3Sel {
     int nv;                 // gathered V tables (template NV)
     bool aux, hc, rec;
+    bool cw = false;        // broadcast V with R > 2 coefficients
 };
 // Which v3 instantiation computes this call, or false (the DMA-v2 / register-staged kernels then run).
 bool v3_select(const RowGemmP& p, V3Sel& sel) {
@@ -2411,26 +2642,26 @@ bool v3_select(const RowGemmP& p, V3Sel& sel) {
     if (p.act == IDDGCN_ACT_DSIGMOID_COMBINE) {
         // x^1 recompute: R <= 2, dense V rows, the caller's bound on V runs per 32-row tile
         if (!(p.R <= 2 && p.v_row_stride == 256 && p.v_runs_max >= 1 && p.v_runs_max <= REC_CAP)) return false;
-        sel = {p.R + 1, false, true, true};
+        sel = {p.R + 1, false, true, true, false};
         return true;
     }
     if (gatherV) {
         if (dsig || p.v_row_stride != 256) return false;
         if (p.R <= 2) {
-            sel = {p.R, false, true, false};
+            sel = {p.R, false, true, false, false};
             return true;
         }
         // more relations: capped slabs (rows past the cap of a tile come from L2)
-        sel = {p.R <= 4 ? 4 : 8, false, true, false};
+        sel = {p.R <= 4 ? 4 : 8, false, true, false, false};
         return true;
     }
-    sel = {0, dsig, p.R > 0, false};
+    sel = {0, dsig, p.R > 0, false, p.R > 2};
     return true;
 }
 
 // One launch of up to ROWGEMM_BATCH v3 GEMMs of the same variant (blockIdx.y = entry).  The persistent
 // grid is ~256 workgroups in all (one per CU: 131-155 KB of LDS each), shared out over the entries.
-void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel) {
+void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel, bool bf = false) {
     const long long per = n > 0 ? (256 + n - 1) / n : 256;
     long long nbmax = 0;
     for (int k = 0; k < n; ++k) {
@@ -2445,11 +2676,27 @@ void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel) {
     }
     if (nbmax == 0) return;
     const dim3 g((unsigned)nbmax, (unsigned)n), blk(512);
+    if (bf) {      // bf16 edge tables: gathered-combine forward, sigma' backward, plain
+#define V3B(NV, AUX, HC) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, false, false, true>), g, blk, 0, st, pb)
+        if (sel.nv == 1) V3B(1, false, true);
+        else if (sel.nv == 2) V3B(2, false, true);
+        else if (sel.nv == 4) V3B(4, false, true);
+        else if (sel.nv == 8) V3B(8, false, true);
+        else if (sel.aux) V3B(0, true, false);
+        else V3B(0, false, false);
+#undef V3B
+        return;
+    }
     const bool x3 = g_gemm_split != 0;
 #define V3L(NV, AUX, HC, REC)                                                                        \
     {                                                                                                \
         if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, REC>), g, blk, 0, st, pb); \
         else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, false, REC>), g, blk, 0, st, pb);   \
+    }
+#define V3W(AUX)                                                                                            \
+    {                                                                                                       \
+        if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, true, false, true>), g, blk, 0, st, pb); \
+        else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, false, false, true>), g, blk, 0, st, pb);   \
     }
     if (sel.rec) {
         if (sel.nv == 2) V3L(2, false, true, true)
@@ -2458,11 +2705,15 @@ void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel) {
     else if (sel.nv == 2) V3L(2, false, true, false)
     else if (sel.nv == 4) V3L(4, false, true, false)
     else if (sel.nv == 8) V3L(8, false, true, false)
-    else if (sel.hc && sel.aux) V3L(0, true, true, false)
+    else if (sel.hc && sel.cw) {
+        if (sel.aux) V3W(true)
+        else V3W(false)
+    } else if (sel.hc && sel.aux) V3L(0, true, true, false)
     else if (sel.hc) V3L(0, false, true, false)
     else if (sel.aux) V3L(0, true, false, false)
     else V3L(0, false, false, false)
 #undef V3L
+#undef V3W
 }
 
 inline unsigned grid_for(long long rows, int lpr) {
@@ -2605,7 +2856,7 @@ int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* a) {
     p.act = a->act; p.aux = a->aux; p.v_runs_max = a->v_runs_max;
     V3Sel sel;
     if (a->D == 256 && v3_select(p, sel))
-        return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.rec ? 4 : 0);
+        return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.rec ? 4 : 0) + (sel.cw ? 8 : 0);
     const bool gatherV = p.R > 0 && p.v_row_stride != 0;
     const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
     const int epi_rows = gatherV ? p.R : (dsig ? 1 : 0);
@@ -2644,7 +2895,8 @@ int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
             p.v_row_stride = a[k].v_row_stride; p.act = a[k].act; p.aux = a[k].aux; p.v_runs_max = a[k].v_runs_max;
             if (!v3_select(p, sel)) same = false;
             else if (m == 0) sel0 = sel;
-            else same = sel.nv == sel0.nv && sel.aux == sel0.aux && sel.hc == sel0.hc && sel.rec == sel0.rec;
+            else same = sel.nv == sel0.nv && sel.aux == sel0.aux && sel.hc == sel0.hc && sel.rec == sel0.rec &&
+                        sel.cw == sel0.cw;
             ++m;
         }
         if (same) {
@@ -2788,7 +3040,8 @@ int iddgcn_alpha_fwd_f32(void* stream, int M, int d, int R, const float* X, cons
     if (M < 0 || !X || !Wa || !ba || !S_out || !W_out) return IDDGCN_E_BAD_ARG;
     if (M == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const unsigned grid = grid_for(M, d / 4);
+    unsigned grid = grid_for(M, d / 4);
+    if (grid > 2048) grid = 2048;            // persistent: W_alpha loaded once per lane group
 #define AK(DD) hipLaunchKernelGGL(alpha_kernel<DD>, dim3(grid), dim3(256), 0, st, M, R, X, x_idx, Wa, ba, S_out, W_out)
     switch (d) {
         case 32: AK(32); break;
@@ -3014,6 +3267,137 @@ int iddgcn_adam_table_f32(void* stream, long long n, float* var, float* m, float
     if (n == 0) return 0;
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, var, m, v,
                        g, 0.0f, b1, b2, eps, sparse_form, alpha_table, step);
+    return launch_status();
+}
+
+int iddgcn_rowgemm_bf16(void* stream, const iddgcn_rowgemm_t* a) {
+    if (!a) return IDDGCN_E_BAD_ARG;
+    if (a->D != 256) return IDDGCN_E_BAD_DIM;
+    if (a->R < 0 || a->R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (a->M == 0) return 0;
+    if (a->M < 0 || !a->A || !a->B || !a->C || a->accumulate) return IDDGCN_E_BAD_ARG;
+    const bool gatherV = a->R > 0 && a->v_row_stride != 0;
+    const bool dsig = a->act == IDDGCN_ACT_DSIGMOID;
+    if (a->act != IDDGCN_ACT_NONE && a->act != IDDGCN_ACT_SIGMOID && !dsig) return IDDGCN_E_BAD_ARG;
+    if (dsig && (!a->aux || a->R > 0)) return IDDGCN_E_BAD_ARG;
+    if (a->R > 0 && (!gatherV || a->v_row_stride != 256 || !a->coef || !a->V)) return IDDGCN_E_BAD_ARG;
+    RowGemmP p;
+    p.M = a->M; p.A = a->A; p.a_idx = a->a_idx; p.B = a->B; p.b_trans = a->b_trans;
+    p.C = a->C; p.accumulate = 0; p.R = a->R; p.coef = a->coef; p.coef_idx = a->coef_idx;
+    p.V = a->V; p.v_idx = a->v_idx; p.v_rel_stride = a->v_rel_stride; p.v_row_stride = a->v_row_stride;
+    p.act = a->act; p.aux = a->aux; p.v_runs_max = a->v_runs_max;
+    V3Sel sel;
+    sel.nv = a->R == 0 ? 0 : a->R == 1 ? 1 : a->R == 2 ? 2 : a->R <= 4 ? 4 : 8;
+    sel.aux = dsig;
+    sel.hc = a->R > 0;
+    sel.rec = false;
+    RowGemmBatch pb;
+    pb.p[0] = p;
+    launch_v3((hipStream_t)stream, pb, 1, sel, true);
+    return launch_status();
+}
+
+int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const void* B, float* slab, int n_blocks,
+                        float* C, int accumulate) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (M < 0 || n_blocks < 1 || !A || !B || !slab || !C) return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    long long rpb = (M + n_blocks - 1) / n_blocks;
+    rpb = ((rpb + 31) / 32) * 32;
+    if (rpb < 32) rpb = 32;
+    hipLaunchKernelGGL(gemm_tn256_bf16_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb,
+                       (const __bf16*)A, (const __bf16*)B, slab);
+    int rc = launch_status();
+    if (rc) return rc;
+    const long long n = (long long)d * d;
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_blocks, n, slab, C,
+                       accumulate, 1.0f);
+    return launch_status();
+}
+
+int iddgcn_combine_bf16(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,
+                        const float* V, long long v_rel_stride, void* out) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (R < 0 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (M < 0 || !Y || !idx || !out || (R > 0 && (!coef || !V))) return IDDGCN_E_BAD_ARG;
+    if (M == 0) return 0;
+    const long long nchunk = ((long long)M + RC_CH - 1) / RC_CH;
+    long long nb = (nchunk + 3) / 4;
+    if (nb > 2048) nb = 2048;
+    hipStream_t st = (hipStream_t)stream;
+    float* o = (float*)out;
+#define RCB(RR) hipLaunchKernelGGL((run_combine256_kernel<RR, true>), dim3((unsigned)nb), dim3(256), 0, st, M, Y, idx, coef, V, v_rel_stride, o)
+    switch (R) {
+        case 0: RCB(0); break;
+        case 1: RCB(1); break;
+        case 2: RCB(2); break;
+        case 3: RCB(3); break;
+        case 4: RCB(4); break;
+        case 5: RCB(5); break;
+        case 6: RCB(6); break;
+        case 7: RCB(7); break;
+        default: RCB(8); break;
+    }
+#undef RCB
+    return launch_status();
+}
+
+int iddgcn_distmult_bce_bf16(void* stream, long long T, int d, int R, const float* Xh, const int* h_idx,
+                             const void* Xt, const int* t_idx, const int* r_idx, const float* rel, const float* y,
+                             float scale, float* p_out, float* s_out, float* ds_out, void* do_out,
+                             float* drel_slab, float* loss_slab, int n_blocks) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (T < 0 || n_blocks < 1 || !Xh || !h_idx || !Xt || !r_idx || !rel) return IDDGCN_E_BAD_ARG;
+    if (y && (!ds_out || !do_out || !drel_slab || !loss_slab)) return IDDGCN_E_BAD_ARG;
+    if (T == 0) return 0;
+    hipLaunchKernelGGL((distmult_kernel<256, true>), dim3(n_blocks), dim3(256), 0, (hipStream_t)stream, T, R, Xh, h_idx,
+                       (const float*)Xt, t_idx, r_idx, rel, y, scale, p_out, s_out, ds_out, (float*)do_out, drel_slab,
+                       loss_slab);
+    return launch_status();
+}
+
+int iddgcn_distmult_bce_heads_bf16(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* perm,
+                                   const float* Xh, const void* Xt, const int* r_idx, const float* rel,
+                                   const float* y, float scale, float* p_out, float* s_out, float* ds_out,
+                                   void* do_out, float* dXh, float* drel_slab, float* loss_slab, int n_blocks) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (n_nodes < 0 || n_blocks < 1 || !seg_ptr || !perm || !Xh || !Xt || !r_idx || !rel || !do_out || !dXh ||
+        !drel_slab || !loss_slab)
+        return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+#define HKB(RT) hipLaunchKernelGGL((distmult_heads_kernel<256, RT, true>), dim3(n_blocks), dim3(256), 0, st, n_nodes, R, seg_ptr, perm, Xh, (const float*)Xt, r_idx, rel, y, scale, p_out, s_out, ds_out, (float*)do_out, dXh, drel_slab, loss_slab)
+    if (R <= 1) HKB(1);
+    else if (R <= 2) HKB(2);
+    else if (R <= 4) HKB(4);
+    else HKB(8);
+#undef HKB
+    return launch_status();
+}
+
+int iddgcn_tail_seg_reduce_bf16(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* h_idx,
+                                const float* W, const void* dO, const float* P, long long p_rel_stride, float* dP,
+                                long long dp_rel_stride, float* dsum, float* dWedge) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (n_nodes < 0 || !seg_ptr || !W || !dO || !P || !dP || !dWedge) return IDDGCN_E_BAD_ARG;
+    if (n_nodes == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = grid_for(n_nodes, 64);
+    const float* d_o = (const float*)dO;
+#define TKB(RR) hipLaunchKernelGGL((tail_seg_reduce_kernel<256, RR, true>), dim3(grid), dim3(256), 0, st, n_nodes, seg_ptr, h_idx, W, d_o, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge)
+    switch (R) {
+        case 1: TKB(1); break;
+        case 2: TKB(2); break;
+        case 3: TKB(3); break;
+        case 4: TKB(4); break;
+        case 5: TKB(5); break;
+        case 6: TKB(6); break;
+        case 7: TKB(7); break;
+        default: TKB(8); break;
+    }
+#undef TKB
     return launch_status();
 }
 

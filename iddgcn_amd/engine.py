@@ -166,7 +166,7 @@ class Workspace:
     (each element is read before it is written, by the same lanes).  3 T x D tables instead of 5:
     123 GB instead of 205 GB at config 4 (T = 40M, D = 256)."""
 
-    def __init__(self, N, R, D, T, device, train=True):
+    def __init__(self, N, R, D, T, device, train=True, edge_dtype=torch.float32):
         f = dict(dtype=torch.float32, device=device)
         e = lambda *s: torch.empty(*s, **f)  # noqa: E731
         self.AE = e(R, N, D)
@@ -179,7 +179,8 @@ class Workspace:
         self.X = e(NUM_LAYERS, N, D)            # head chain X^1..X^3
         self.Ssm = e(NUM_LAYERS, N, R)
         self.W = e(NUM_LAYERS, N, R)
-        self.xt = e(NUM_LAYERS, T, D)           # tail chain x^1..x^3 (then, training, do^3..do^1)
+        # tail chain x^1..x^3 (then, training, do^3..do^1); bf16 in the bf16-feature mode
+        self.xt = torch.empty(NUM_LAYERS, T, D, dtype=edge_dtype, device=device)
         self.Wedge = e(NUM_LAYERS, T, R)        # W^l[h_e]: per-edge copy of the dynamic weights
         self.p = e(T)
         self.s = e(T)                           # pre-sigmoid DistMult logits (IDDGCN.py:108)
@@ -216,9 +217,17 @@ class Engine:
     """
 
     def __init__(self, num_entities, num_relations, dim, device=None, gemm="split", recompute_x1=False,
-                 fuse_tail_seg=False):
+                 fuse_tail_seg=False, features="f32"):
         if dim not in (32, 64, 128, 256):
             raise L.IddgcnError("embedding dim must be one of 32, 64, 128, 256")
+        if features not in ("f32", "bf16"):
+            raise L.IddgcnError("features must be 'f32' or 'bf16'")
+        if features == "bf16" and (dim != 256 or recompute_x1 or fuse_tail_seg):
+            raise L.IddgcnError("the bf16-feature mode is D=256 only, without recompute_x1 / fuse_tail_seg")
+        # bf16-feature mode (BASELINE config 5, perf only): the edge tables x^l / do^l stored as bf16 and
+        # the edge GEMMs on bf16 MFMA; node tables, weights, accumulation and epilogues stay fp32
+        self.features = features
+        self.edge_dtype = torch.bfloat16 if features == "bf16" else torch.float32
         if not 1 <= num_relations <= 8:
             raise L.IddgcnError("num_relations must be in [1, 8]")
         if gemm not in GEMM_MODES:
@@ -273,7 +282,7 @@ class Engine:
         key = (T, train)
         if key not in self._ws:
             self._ws = {k: v for k, v in self._ws.items() if k[1] != train}  # keep one per mode
-            self._ws[key] = Workspace(self.N, self.R, self.D, T, self.device, train)
+            self._ws[key] = Workspace(self.N, self.R, self.D, T, self.device, train, self.edge_dtype)
         return self._ws[key]
 
     # -- forward ------------------------------------------------------------
@@ -435,7 +444,7 @@ class Engine:
         ws = self.workspace(ed.T, False)
         inv = ed.inv if rows is None else ed.inv[torch.as_tensor(rows, device=ed.inv.device)]
         heads = ed.h.long()[inv]
-        return [(ws.X[l][heads], ws.xt[l][inv]) for l in range(NUM_LAYERS)]
+        return [(ws.X[l][heads], ws.xt[l][inv].float()) for l in range(NUM_LAYERS)]
 
     def loss_and_grads(self, params, grads, adj, ed, t_global=None, logits=False):
         """Forward + backward without the optimizer step: (loss sum, p) or, with ``logits=True``,

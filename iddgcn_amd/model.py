@@ -138,34 +138,30 @@ class IDDGCN_Layer(Layer):
                          rng.uniform(-0.05, 0.05, (R,)).astype(np.float32),
                          _glorot_uniform(rng, (D, R)).astype(np.float32), np.zeros((R,), np.float32)]
 
-    def __call__(self, inputs):
-        """Standalone forward, IDDGCN.py:60-79: inputs = [embeddings (N,D), head_idx (B,),
-        head_e (B,D), tail_idx (B,), tail_e (B,D), adj_mats] with GPU float32 tensors.
-        Returns (sigmoid(head_out), sigmoid(tail_out)), each (B, D)."""
+    def __call__(self, inputs, weights=None):
+        """IDDGCN.py:60-79 on GPU tensors: inputs = [embeddings (N,D), head_idx (B,), head_e (B,D),
+        tail_idx (B,), tail_e (B,D), adj_mats].  Returns (sigmoid(head_out), sigmoid(tail_out)), each (B, D),
+        differentiable (autograd.IDDGCNLayerFunction) w.r.t. embeddings, head_e, tail_e and — passed as
+        ``weights=[relation_kernels, self_kernel, W_alpha, b_alpha]`` tensors — the layer weights (the
+        layer's own weights are used as constants otherwise)."""
+        from .autograd import IDDGCNLayerFunction
         embeddings, head_idx, head_e, tail_idx, tail_e, *adj = inputs
         adj = _unwrap_adj(adj)
         dev = embeddings.device
         N, D, R = self.num_entities, self.output_dim, self.num_relations
-        K, S, _, Wa, ba = [torch.as_tensor(w, device=dev) for w in self._weights]
+        if weights is None:
+            K, S, _, Wa, ba = [torch.as_tensor(w, device=dev) for w in self._weights]
+        else:
+            K, S, Wa, ba = weights
         dadj = adj if isinstance(adj, DeviceAdjacency) else DeviceAdjacency(adj, N, dev)
         B = head_e.shape[0]
         hi = head_idx.to(device=dev, dtype=torch.int32).contiguous()
         ti = tail_idx.to(device=dev, dtype=torch.int32).contiguous()
         if B and (int(hi.min()) < 0 or int(hi.max()) >= N or int(ti.min()) < 0 or int(ti.max()) >= N):
             raise L.IddgcnError("head/tail index out of range")
-        AE = torch.empty(R, N, D, device=dev)
-        ops.spmm_csr(dadj.fwd_ptr, dadj.fwd_col, dadj.fwd_val, embeddings.contiguous(), AE, R, N)
-        P = torch.empty(R, N, D, device=dev)
-        for r in range(R):
-            ops.rowgemm(AE[r], K[r], P[r])
-        Ssm = torch.empty(B, R, device=dev)
-        W = torch.empty(B, R, device=dev)
-        ops.alpha_fwd(head_e.contiguous(), Wa, ba, Ssm, W)
-        ho = torch.empty(B, D, device=dev)
-        to = torch.empty(B, D, device=dev)
-        ops.rowgemm(head_e.contiguous(), S, ho, coef=W, V=P, v_idx=hi, v_rel_stride=N * D, act=L.ACT_SIGMOID)
-        ops.rowgemm(tail_e.contiguous(), S, to, coef=W, V=P, v_idx=ti, v_rel_stride=N * D, act=L.ACT_SIGMOID)
-        return ho, to
+        if tuple(embeddings.shape) != (N, D) or tuple(head_e.shape) != (B, D) or tuple(tail_e.shape) != (B, D):
+            raise L.IddgcnError("embeddings (N, D), head_e and tail_e (B, D) expected")
+        return IDDGCNLayerFunction.apply(embeddings, head_e, tail_e, K, S, Wa, ba, hi, ti, dadj)
 
 
 class DistMult(Layer):
@@ -182,22 +178,25 @@ class DistMult(Layer):
         rng = np.random.default_rng(self.seed)
         self._weights = [rng.standard_normal((self.num_relations, embedding_dim)).astype(np.float32)]
 
-    def __call__(self, inputs, logits=False):
-        """sigmoid(sum head_e * rel[rel_idx] * tail_e) as (1, B); ``logits=True``: the sum itself."""
+    def __call__(self, inputs, logits=False, rel_embedding=None):
+        """sigmoid(sum head_e * rel[rel_idx] * tail_e) as (1, B), differentiable (autograd.DistMultFunction)
+        w.r.t. head_e, tail_e and a ``rel_embedding`` tensor if given; ``logits=True``: the sum itself."""
+        from .autograd import DistMultFunction
         head_e, rel_idx, tail_e = inputs
         dev = head_e.device
         if not self._weights:
             self.build(head_e.shape[-1])
-        rel = torch.as_tensor(self._weights[0], device=dev)
+        rel = torch.as_tensor(self._weights[0], device=dev) if rel_embedding is None else rel_embedding
         B = head_e.shape[0]
         ri = rel_idx.to(device=dev, dtype=torch.int32).contiguous()
         if B and (int(ri.min()) < 0 or int(ri.max()) >= self.num_relations):
             raise L.IddgcnError("relation index out of range")
-        ident = torch.arange(B, device=dev, dtype=torch.int32)
-        p = torch.empty(B, device=dev)
-        s = torch.empty(B, device=dev) if logits else None
-        ops.distmult_bce(head_e.contiguous(), ident, tail_e.contiguous(), ri, rel, p_out=p, s_out=s)
-        return (s if logits else p).view(1, B)
+        if logits:
+            ident = torch.arange(B, device=dev, dtype=torch.int32)
+            p, s = torch.empty(B, device=dev), torch.empty(B, device=dev)
+            ops.distmult_bce(head_e.contiguous(), ident, tail_e.contiguous(), ri, rel.contiguous(), p_out=p, s_out=s)
+            return s.view(1, B)
+        return DistMultFunction.apply(head_e, rel, tail_e, ri).view(1, B)
 
 
 # ---------------------------------------------------------------------------

@@ -16,6 +16,7 @@ import torch
 from . import _lib as L
 
 _F32 = torch.float32
+_BF16 = torch.bfloat16
 _I32 = torch.int32
 
 
@@ -82,9 +83,13 @@ def sddmm_csr(row_ptr, col, G, X, out, n_seg, n_rows):
 
 
 def rowgemm(A, B, C, **kw):
-    """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32); see _rowgemm_args."""
+    """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32); see _rowgemm_args.  bf16 A
+    (the bf16-feature mode's edge tables) selects iddgcn_rowgemm_bf16: A, aux and C are then bf16."""
     args = _rowgemm_args(A, B, C, **kw)
-    L.check(L.lib().iddgcn_rowgemm_f32(_stream(), ctypes.byref(args)), "rowgemm")
+    if A.dtype == _BF16:
+        L.check(L.lib().iddgcn_rowgemm_bf16(_stream(), ctypes.byref(args)), "rowgemm_bf16")
+    else:
+        L.check(L.lib().iddgcn_rowgemm_f32(_stream(), ctypes.byref(args)), "rowgemm")
 
 
 def rowgemm_kernel_id(A, B, C, **kw):
@@ -111,9 +116,10 @@ def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=
     D = B.shape[0]
     M = C.shape[0] if M is None else M
     R = 0 if coef is None else coef.shape[-1]
-    _req(A, _F32, None, "A")
+    et = A.dtype if A.dtype == _BF16 else _F32         # edge-table element type (A, C, aux)
+    _req(A, et, None, "A")
     _req(B, _F32, (D, D), "B")
-    _req(C, _F32, (M, D), "C")
+    _req(C, et, (M, D), "C")
     if A.dim() != 2 or A.shape[1] != D:
         raise L.IddgcnError(f"A must be (rows, {D})")
     if a_idx is None and A.shape[0] < M:
@@ -127,7 +133,7 @@ def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=
                  if (v_row_stride is None or v_row_stride) and v_rel_stride else None)
         _idx_ok(v_idx, M, vrows, "v_idx")
     if act == L.ACT_DSIGMOID:
-        _req(aux, _F32, (M, D), "aux")
+        _req(aux, et, (M, D), "aux")
     if act == L.ACT_DSIGMOID_COMBINE:
         if not R or V is None or V.numel() < (R + 1) * int(v_rel_stride):
             raise L.IddgcnError("ACT_DSIGMOID_COMBINE needs coef (R columns) and R+1 V tables")
@@ -144,15 +150,17 @@ def tn_blocks(M, D):
 
 
 def gemm_tn(A, B, C, slab, accumulate=False):
+    """C (+)= A^T B; bf16 A and B (the bf16-feature mode) select iddgcn_gemm_tn_bf16."""
     M, D = A.shape
-    _req(A, _F32, (M, D), "A")
-    _req(B, _F32, (M, D), "B")
+    et = _BF16 if A.dtype == _BF16 else _F32
+    _req(A, et, (M, D), "A")
+    _req(B, et, (M, D), "B")
     _req(C, _F32, (D, D), "C")
     nb = tn_blocks(M, D)
     if slab.numel() < nb * D * D:
         raise L.IddgcnError("gemm_tn slab too small")
-    L.check(L.lib().iddgcn_gemm_tn_f32(_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C),
-                                       int(accumulate)), "gemm_tn")
+    fn = L.lib().iddgcn_gemm_tn_bf16 if et == _BF16 else L.lib().iddgcn_gemm_tn_f32
+    L.check(fn(_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C), int(accumulate)), "gemm_tn")
 
 
 TN_SEG_CAP = 6   # distinct tails per 32-row tile the fused kernel stages on chip (include/iddgcn.h)
@@ -218,6 +226,17 @@ def alpha_fwd(X, Wa, ba, S_out, W_out, x_idx=None, M=None):
 def combine(Y, coef, V, out, *, y_idx=None, coef_idx=None, v_idx=None, v_rel_stride=None):
     M, D = out.shape
     R = coef.shape[-1]
+    if out.dtype == _BF16:      # bf16-feature mode: the run form (y_idx == v_idx, per-row coefficients)
+        if y_idx is None or v_idx is not y_idx or coef_idx is not None:
+            raise L.IddgcnError("combine into bf16: y_idx and v_idx must be the same array, no coef_idx")
+        _req(out, _BF16, (M, D), "out")
+        _req(Y, _F32, None, "Y")
+        _req(coef, _F32, (M, R), "coef")
+        _idx_ok(y_idx, M, Y.shape[0], "y_idx")
+        vrs = V.shape[1] * D if v_rel_stride is None else v_rel_stride
+        L.check(L.lib().iddgcn_combine_bf16(_stream(), M, D, R, _ptr(Y), _ptr(y_idx), _ptr(coef), _ptr(V), int(vrs),
+                                            _ptr(out)), "combine_bf16")
+        return
     _req(Y, _F32, None, "Y")
     _req(coef, _F32, None, "coef")
     _req(V, _F32, None, "V")
@@ -242,8 +261,9 @@ def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_
     R, D = rel.shape
     _req(h_idx, _I32, (T,), "h_idx")
     _req(r_idx, _I32, (T,), "r_idx")
+    bf = Xt.dtype == _BF16
     _req(Xh, _F32, None, "Xh")
-    _req(Xt, _F32, None, "Xt")
+    _req(Xt, _BF16 if bf else _F32, None, "Xt")
     _req(rel, _F32, (R, D), "rel")
     _req(y, _F32, (T,), "y")
     _req(p_out, _F32, (T,), "p_out")
@@ -256,10 +276,11 @@ def distmult_bce(Xh, h_idx, Xt, r_idx, rel, *, t_idx=None, y=None, scale=1.0, p_
     nb = distmult_blocks(T)
     if y is not None:
         _req(ds_out, _F32, (T,), "ds_out")
-        _req(do_out, _F32, (T, D), "do_out")
+        _req(do_out, Xt.dtype, (T, D), "do_out")
         if drel_slab.numel() < nb * R * D or loss_slab.numel() < nb:
             raise L.IddgcnError("distmult slabs too small")
-    L.check(L.lib().iddgcn_distmult_bce_f32(_stream(), T, D, R, _ptr(Xh), _ptr(h_idx), _ptr(Xt), _ptr(t_idx),
+    fn = L.lib().iddgcn_distmult_bce_bf16 if bf else L.lib().iddgcn_distmult_bce_f32
+    L.check(fn(_stream(), T, D, R, _ptr(Xh), _ptr(h_idx), _ptr(Xt), _ptr(t_idx),
                                             _ptr(r_idx), _ptr(rel), _ptr(y), float(scale), _ptr(p_out),
                                             _ptr(s_out), _ptr(ds_out), _ptr(do_out), _ptr(drel_slab), _ptr(loss_slab),
                                             nb),
@@ -277,11 +298,12 @@ def distmult_bce_heads(seg_ptr, perm, Xh, Xt, r_idx, rel, y, do_out, dXh, drel_s
     _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")
     _req(perm, _I32, (T,), "perm")
     _req(r_idx, _I32, (T,), "r_idx")
+    et = _BF16 if Xt.dtype == _BF16 else _F32
     _req(Xh, _F32, (n_nodes, D), "Xh")
-    _req(Xt, _F32, (T, D), "Xt")
+    _req(Xt, et, (T, D), "Xt")
     _req(rel, _F32, (R, D), "rel")
     _req(y, _F32, (T,), "y")
-    _req(do_out, _F32, (T, D), "do_out")
+    _req(do_out, et, (T, D), "do_out")
     _req(dXh, _F32, (n_nodes, D), "dXh")
     _req(p_out, _F32, (T,), "p_out")
     _req(s_out, _F32, (T,), "s_out")
@@ -289,7 +311,8 @@ def distmult_bce_heads(seg_ptr, perm, Xh, Xt, r_idx, rel, y, do_out, dXh, drel_s
     nb = distmult_blocks(T)
     if drel_slab.numel() < nb * R * D or loss_slab.numel() < nb:
         raise L.IddgcnError("distmult slabs too small")
-    L.check(L.lib().iddgcn_distmult_bce_heads_f32(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(perm), _ptr(Xh),
+    fn = L.lib().iddgcn_distmult_bce_heads_bf16 if et == _BF16 else L.lib().iddgcn_distmult_bce_heads_f32
+    L.check(fn(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(perm), _ptr(Xh),
                                                   _ptr(Xt), _ptr(r_idx), _ptr(rel), _ptr(y), float(scale),
                                                   _ptr(p_out), _ptr(s_out), _ptr(ds_out), _ptr(do_out), _ptr(dXh),
                                                   _ptr(drel_slab), _ptr(loss_slab), nb), "distmult_bce_heads")
@@ -313,7 +336,9 @@ def tail_seg_reduce(seg_ptr, h_idx, W, dO, P, dP, dWedge, dsum=None):
     _req(dsum, _F32, (n_nodes, D), "dsum")
     if h_idx is None and W.shape[0] != dO.shape[0]:
         raise L.IddgcnError("tail_seg_reduce: per-edge W must have one row per edge")
-    L.check(L.lib().iddgcn_tail_seg_reduce_f32(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(h_idx), _ptr(W),
+    _req(dO, _BF16 if dO.dtype == _BF16 else _F32, None, "dO")
+    fn = L.lib().iddgcn_tail_seg_reduce_bf16 if dO.dtype == _BF16 else L.lib().iddgcn_tail_seg_reduce_f32
+    L.check(fn(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(h_idx), _ptr(W),
                                                _ptr(dO), _ptr(P), n_nodes * D, _ptr(dP), n_nodes * D, _ptr(dsum),
                                                _ptr(dWedge)), "tail_seg_reduce")
 

@@ -88,7 +88,8 @@ typedef struct {
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 
 /* Which kernel iddgcn_rowgemm_f32 would run for these arguments (a test / benchmark hook; nothing is
- * launched): 300 + 10*NV + aux + 2*coef + 4*recompute for the D = 256 v3 pipeline (NV = gathered V
+ * launched): 300 + 10*NV + aux + 2*coef + 4*recompute + 8*(broadcast V with R > 2 coefficients)
+ * for the D = 256 v3 pipeline (NV = gathered V
  * tables: 1, 2, or capacity 4 / 8 for R <= 8, whose LDS slabs keep 7 distinct V rows per 32-row tile
  * and read further ones from L2), 200 for the v2 LDS-DMA row GEMM, 100 for the register-staged kernel
  * (any D, any V order), -1 for an invalid D. */
@@ -249,6 +250,39 @@ int iddgcn_adam_table_f32(void* stream, long long n, float* var, float* m, float
                           const float* alpha_table, const int* step, float b1, float b2, float eps,
                           int sparse_form);
 int iddgcn_step_advance(void* stream, int* step, float* loss_history, const float* loss);
+
+/* ---- bf16-feature mode (BASELINE config 5: "bf16 features with MFMA XW"; perf only) -----------------
+ * The edge tables x^1..x^3 and the edge-level gradients do^l are stored as bf16 (512-B rows at D = 256,
+ * passed as void*); node tables, weights, coefficients, accumulation and every epilogue stay fp32.
+ * GEMMs multiply bf16 edge rows by the weights as a bf16 hi + lo pair (two v_mfma_f32_32x32x16_bf16 per
+ * k-step), so the only rounding beyond fp32 is the bf16 storage of the edge tables.  D = 256 only. */
+
+/* iddgcn_rowgemm_f32 with A, aux and C bf16: the edge forward (gathered V, R <= 8, coefficients per row),
+ * the sigma' backward (act DSIGMOID with aux) and plain forms; no accumulate, no broadcast V. */
+int iddgcn_rowgemm_bf16(void* stream, const iddgcn_rowgemm_t* args);
+
+/* iddgcn_gemm_tn_f32 with bf16 A and B (slab / blocks / C as there). */
+int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const void* B, float* slab, int n_blocks,
+                        float* C, int accumulate);
+
+/* The run form of iddgcn_combine_f32 (y_idx == v_idx = idx, coefficients per row) writing bf16 out. */
+int iddgcn_combine_bf16(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,
+                        const float* V, long long v_rel_stride, void* out);
+
+/* iddgcn_distmult_bce_f32 / _heads_f32 with Xt and do_out bf16 (do_out may alias Xt). */
+int iddgcn_distmult_bce_bf16(void* stream, long long T, int d, int R, const float* Xh, const int* h_idx,
+                             const void* Xt, const int* t_idx, const int* r_idx, const float* rel, const float* y,
+                             float scale, float* p_out, float* s_out, float* ds_out, void* do_out,
+                             float* drel_slab, float* loss_slab, int n_blocks);
+int iddgcn_distmult_bce_heads_bf16(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* perm,
+                                   const float* Xh, const void* Xt, const int* r_idx, const float* rel,
+                                   const float* y, float scale, float* p_out, float* s_out, float* ds_out,
+                                   void* do_out, float* dXh, float* drel_slab, float* loss_slab, int n_blocks);
+
+/* iddgcn_tail_seg_reduce_f32 with dO bf16. */
+int iddgcn_tail_seg_reduce_bf16(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* h_idx,
+                                const float* W, const void* dO, const float* P, long long p_rel_stride, float* dP,
+                                long long dp_rel_stride, float* dsum, float* dWedge);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,137 @@
+"""The bf16-feature mode (BASELINE config 5: "bf16 features with MFMA XW"; perf only, no parity claim
+to the fp32 reference): edge tables x^l / do^l stored as bf16, edge GEMMs on bf16 MFMA with fp32
+accumulation and fp32 epilogues.
+
+Kernel bars: each bf16 kernel against an fp64 torch reference of the same op evaluated on the SAME
+bf16-rounded inputs — the only extra error allowed is the bf16 rounding of the output (2^-8 relative)
+and the bf16 hi+lo representation of the weights (2^-16 relative): outputs within 6e-3 of max|ref|
+for bf16-stored results, 1e-5 for fp32 results (TN partials, dP, logits of exact bf16 inputs).
+Model bar: a bf16-mode training step against the fp32 engine on the same inputs at a non-saturating
+init — loss within 2e-2 relative, probabilities within 2e-2, every gradient within 5e-2 of its max|g|.
+"""
+import numpy as np
+import pytest
+import torch
+
+from iddgcn_amd import _lib as L
+from iddgcn_amd import ops
+from iddgcn_amd.engine import Engine, FlatParams
+from iddgcn_amd.graph import get_adj_mats
+from iddgcn_amd.utils import synthetic_graph
+
+pytestmark = pytest.mark.gpu
+D = 256
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def maxrel(got, ref):
+    return ((got.double() - ref).abs().max() / ref.abs().max()).item()
+
+
+def tails(M, N, g):
+    lengths = torch.randint(4, 60, (N,), generator=g)
+    return torch.repeat_interleave(torch.arange(N), lengths)[:M]
+
+
+@pytest.mark.parametrize("R", [1, 2, 8])
+def test_rowgemm_bf16_forward_combine(R, cuda):
+    g = torch.Generator().manual_seed(R)
+    N, M = 3000, 40_007
+    A = bf(torch.rand(M, D, generator=g)).to(cuda)
+    S = (torch.randn(D, D, generator=g, dtype=torch.float64) / 16).to(cuda)
+    W = torch.rand(M, R, generator=g, dtype=torch.float64).to(cuda)
+    P = torch.randn(R, N, D, generator=g, dtype=torch.float64).to(cuda)
+    t = tails(M, N, g).to(cuda)
+    ref = torch.sigmoid(A.double() @ S + sum(W[:, r:r + 1] * P[r][t] for r in range(R)))
+    C = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
+    ops.rowgemm(A, S.float(), C, coef=W.float(), V=P.float(), v_idx=t.int(), v_rel_stride=N * D, act=L.ACT_SIGMOID)
+    assert maxrel(C, ref) <= 6e-3
+
+
+def test_rowgemm_bf16_backward_dsigmoid(cuda):
+    g = torch.Generator().manual_seed(7)
+    M = 30_001
+    dO = bf(torch.randn(M, D, generator=g) * 1e-4).to(cuda)
+    S = (torch.randn(D, D, generator=g, dtype=torch.float64) / 16).to(cuda)
+    X = bf(torch.rand(M, D, generator=g)).to(cuda)
+    ref = (dO.double() @ S.t()) * X.double() * (1 - X.double())
+    C = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
+    ops.rowgemm(dO, S.float(), C, b_trans=True, act=L.ACT_DSIGMOID, aux=X)
+    assert maxrel(C, ref) <= 6e-3
+    Xi = X.clone()                     # in place over the sigma' operand, as the engine runs it
+    ops.rowgemm(dO, S.float(), Xi, b_trans=True, act=L.ACT_DSIGMOID, aux=Xi)
+    assert torch.equal(Xi, C)
+
+
+@pytest.mark.parametrize("M", [31, 5003, 300_017])
+def test_gemm_tn_bf16(M, cuda):
+    g = torch.Generator().manual_seed(M)
+    A = bf(torch.randn(M, D, generator=g)).to(cuda)
+    B = bf(torch.randn(M, D, generator=g) * 1e-3).to(cuda)
+    ref = A.double().t() @ B.double()
+    C = torch.empty(D, D, device=cuda)
+    slab = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
+    ops.gemm_tn(A, B, C, slab)
+    assert maxrel(C, ref) <= 1e-5
+
+
+@pytest.mark.parametrize("R", [2, 8])
+def test_combine_tail_seg_distmult_bf16(R, cuda):
+    g = torch.Generator().manual_seed(11 * R)
+    N, M = 2000, 50_000
+    t = tails(M, N, g).to(cuda).int()
+    Y = torch.randn(N, D, generator=g).to(cuda)
+    W = torch.rand(M, R, generator=g).to(cuda)
+    P = torch.randn(R, N, D, generator=g).to(cuda)
+    out = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
+    ops.combine(Y, W, P, out, y_idx=t, v_idx=t)
+    tl = t.long()
+    ref = torch.sigmoid(Y.double()[tl] + sum(W.double()[:, r:r + 1] * P.double()[r][tl] for r in range(R)))
+    assert maxrel(out, ref) <= 6e-3
+    # tail-side segmented reduction over bf16 rows == the fp32 kernel on the same (widened) rows
+    tptr = torch.searchsorted(t, torch.arange(N + 1, device=cuda, dtype=torch.int32)).int()
+    dP, dWe = torch.empty(R, N, D, device=cuda), torch.empty(M, R, device=cuda)
+    ops.tail_seg_reduce(tptr, None, W, out, P, dP, dWe)
+    dP32, dWe32 = torch.empty_like(dP), torch.empty_like(dWe)
+    ops.tail_seg_reduce(tptr, None, W, out.float(), P, dP32, dWe32)
+    assert torch.equal(dP, dP32) and torch.equal(dWe, dWe32)
+    # DistMult scores of bf16 tails == the fp32 kernel on the widened rows
+    h = torch.randint(0, N, (M,), generator=g).int().to(cuda)
+    r = torch.randint(0, R, (M,), generator=g).int().to(cuda)
+    rel = torch.randn(R, D, generator=g).to(cuda)
+    Xh = torch.rand(N, D, generator=g).to(cuda)
+    p, s = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
+    ops.distmult_bce(Xh, h, out, r, rel, p_out=p, s_out=s)
+    p32, s32 = torch.empty_like(p), torch.empty_like(s)
+    ops.distmult_bce(Xh, h, out.float(), r, rel, p_out=p32, s_out=s32)
+    assert torch.equal(s, s32) and torch.equal(p, p32)
+
+
+@pytest.mark.parametrize("R", [2, 8])
+def test_bf16_mode_step_tracks_fp32(R, cuda):
+    N = 1500
+    pos, neg = synthetic_graph(N, R, 16000, seed=40 + R)
+    tri = np.concatenate([pos, neg])
+    lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+    rng = np.random.default_rng(R)
+    params = {"E": rng.standard_normal((N, D)) / np.sqrt(D), "rel": rng.standard_normal((R, D))}
+    for l in (1, 2, 3):
+        params.update({f"K{l}": rng.standard_normal((R, D, D)) / D, f"S{l}": rng.standard_normal((D, D)) / np.sqrt(D),
+                       f"Wa{l}": rng.standard_normal((D, R)) / np.sqrt(D), f"ba{l}": rng.standard_normal(R) * 0.1})
+    out = {}
+    for feat in ("f32", "bf16"):
+        eng = Engine(N, R, D, cuda, features=feat)
+        P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
+        P.load(params)
+        adj = eng.adjacency(get_adj_mats(pos, N, R))
+        loss, p = eng.loss_and_grads(P, G, adj, eng.edges(tri, lab))
+        out[feat] = (float(loss.item()), p.cpu().numpy(), G.to_numpy())
+    (l32, p32, g32), (lb, pb, gb) = out["f32"], out["bf16"]
+    assert abs(lb - l32) <= 2e-2 * l32
+    assert np.abs(pb - p32).max() <= 2e-2
+    for k, v in g32.items():
+        assert np.all(np.isfinite(gb[k])), k
+        assert np.abs(gb[k] - v).max() <= 5e-2 * np.abs(v).max() + 1e-30, k

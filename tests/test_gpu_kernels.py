@@ -815,7 +815,7 @@ def test_rowgemm256_rank_update_many_relations(R, gm, cuda):
               v_row_stride=0, act=L.ACT_DSIGMOID, aux=X.float())
     with _gemm_mode(L.GEMM_SPLIT_F16 if gm == "split" else L.GEMM_EXACT_F32):
         C = C0.float().clone()
-        assert ops.rowgemm_kernel_id(dO.float(), S.float(), C, **kw) == 300 + 2 + 1
+        assert ops.rowgemm_kernel_id(dO.float(), S.float(), C, **kw) == 300 + 2 + 1 + 8
         ops.rowgemm(dO.float(), S.float(), C, **kw)
     assert _maxrel(C, ref) <= 2e-5
 

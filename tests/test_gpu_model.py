@@ -454,3 +454,45 @@ def test_standalone_layer_call_matches_oracle(golden, cuda):
     # layer outputs are sigmoids of pre-activations up to |x|~800: fp32 bar 1e-4 (north_star logits bar)
     np.testing.assert_allclose(ho.cpu().numpy(), rh.numpy(), atol=1e-4, rtol=0)
     np.testing.assert_allclose(to.cpu().numpy(), rt.numpy(), atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("D,R", [(64, 4), (256, 2), (256, 8)])
+def test_layer_and_distmult_autograd_vs_oracle(D, R, cuda):
+    """IDDGCN_Layer / DistMult as differentiable calls (autograd.IDDGCNLayerFunction, DistMultFunction):
+    gradients of a random linear functional of the layer outputs and the DistMult scores w.r.t. the
+    embeddings, the layer inputs and every layer weight vs torch autograd of the oracle's layer_call
+    (IDDGCN.py:60-79) in float64; non-saturating init, bar 1e-4 of max|g| (fp32 kernels, K <= 256)."""
+    from iddgcn_amd import DistMult, IDDGCN_Layer
+    from oracle.ref_model import adj_to_torch, layer_call
+    N, B = 700, 3000
+    pos, _ = synthetic_graph(N, R, 9000, seed=D + R)
+    rng = np.random.default_rng(D)
+    E = rng.standard_normal((N, D)) / np.sqrt(D)
+    K, S = rng.standard_normal((R, D, D)) / D, rng.standard_normal((D, D)) / np.sqrt(D)
+    Wa, ba = rng.standard_normal((D, R)) / np.sqrt(D), rng.standard_normal(R) * 0.1
+    rel = rng.standard_normal((R, D))
+    h, t, r = rng.integers(0, N, B), rng.integers(0, N, B), rng.integers(0, R, B)
+    G1, G2, G3 = rng.standard_normal((B, D)), rng.standard_normal((B, D)), rng.standard_normal(B)
+    adj = get_adj_mats(pos, N, R)
+
+    def run(dev, dtype, ours):
+        f = lambda a: torch.tensor(a, dtype=dtype, device=dev, requires_grad=True)  # noqa: E731
+        Et, Kt, St, Wat, bat, relt = f(E), f(K), f(S), f(Wa), f(ba), f(rel)
+        ht, tt, rt = (torch.as_tensor(x, device=dev) for x in (h, t, r))
+        xh, xt = Et[ht], Et[tt]
+        if ours:
+            lay = IDDGCN_Layer(N, R, D, 1)
+            ho, to = lay([Et, ht, xh, tt, xt, adj], weights=[Kt, St, Wat, bat])
+            dm = DistMult(R, 1, embedding_dim=D)
+            p = dm([ho, rt, to], rel_embedding=relt)[0]
+        else:
+            ho, to = layer_call(Et, ht, xh, tt, xt, adj_to_torch(get_adj_coo(pos, N, R), N), Kt, St, Wat, bat)
+            p = torch.sigmoid((ho * relt[rt] * to).sum(-1))
+        g = lambda a: torch.as_tensor(a, dtype=dtype, device=dev)  # noqa: E731
+        loss = (ho * g(G1)).sum() + (to * g(G2)).sum() + (p * g(G3)).sum()
+        return [x.detach().cpu().double().numpy() for x in torch.autograd.grad(loss, [Et, Kt, St, Wat, bat, relt])]
+
+    ref = run("cpu", torch.float64, False)
+    got = run(cuda, torch.float32, True)
+    for name, a, b in zip(["E", "K", "S", "Wa", "ba", "rel"], got, ref):
+        assert np.abs(a - b).max() <= 1e-4 * np.abs(b).max() + 1e-30, name
