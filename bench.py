@@ -220,7 +220,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     import torch.distributed as dist
     from iddgcn_amd.engine import Engine, FlatParams, KerasAdam
     from iddgcn_amd.graph import get_adj_mats
-    from iddgcn_amd.parallel import BucketedAllReduce, shard_range
+    from iddgcn_amd.parallel import BucketedAllReduce, RelationShard, shard_range
     from iddgcn_amd.utils import synthetic_graph
 
     cfg = CONFIGS[cid]
@@ -244,6 +244,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
     init = reference_init(np, N, R, D, 89)
     comm = BucketedAllReduce() if world > 1 else None
+    if args.shard == "relation" and world > 1:
+        eng.node_shard = RelationShard(R, N)     # SURVEY §8(e) alternative: node tables split by relation
 
     def timed_run(mode, probe):
         """W warm-up steps, then K timed steps between barriers + synchronize; max over ranks."""
@@ -277,7 +279,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
            "gemm_operands": GEMM_NOTE[gemm] + ("; edge GEMMs bf16 (features=bf16)" if feat == "bf16" else ""),
            "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
                       "scored_edges": T, "scored_edges_per_gpu": ed.T, "feat_dim": D,
-                      "parallelism": f"edge-dp{world}", "gemm": gemm, "features": feat},
+                      "parallelism": f"edge-dp{world}" + ("+relation-sharded-nodes" if eng.node_shard else ""),
+                      "gemm": gemm, "features": feat},
            "scored_edges_per_s": T / (elapsed / args.steps), "loss": loss_val}
     if other_mode and feat == "f32":
         mode2 = "exact" if gemm == "split" else "split"
@@ -308,6 +311,8 @@ def main():
     ap.add_argument("--also", type=int, nargs="*", default=[], choices=sorted(CONFIGS),
                     help="further workloads timed in the same run, reported under 'also'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", default="edge", choices=["edge", "relation"],
+                    help="multi-GPU: edge partitioning only (default) or also relation-sharded node tables")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],
                     help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
     ap.add_argument("--gemm", default="split", choices=["split", "exact"],

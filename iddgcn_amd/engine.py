@@ -286,17 +286,31 @@ class Engine:
         return self._ws[key]
 
     # -- forward ------------------------------------------------------------
+    node_shard = None      # parallel.RelationShard: per-relation node tables split over the ranks
+
     def forward(self, P, adj, ed, ws, train):
         N, R, D, T = self.N, self.R, self.D, ed.T
         E = P["E"]
-        # AE_r = A_r·E, all relations in one launch (IDDGCN.py:69-70)
-        ops.spmm_csr(adj.fwd_ptr, adj.fwd_col, adj.fwd_val, E, ws.AE, R, N)
-        # P_r^l = AE_r·K_r^l (node-level form of IDDGCN.py:71-72,76-77) and, layer 1, x·S1 at node
-        # level for both sides (inputs E[h], E[t]): independent GEMMs, batched (one launch below D=256)
-        proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], {}) for l in range(NUM_LAYERS) for r in range(R)]
+        sh = self.node_shard
+        if sh is None:
+            # AE_r = A_r·E, all relations in one launch (IDDGCN.py:69-70)
+            ops.spmm_csr(adj.fwd_ptr, adj.fwd_col, adj.fwd_val, E, ws.AE, R, N)
+            # P_r^l = AE_r·K_r^l (node-level form of IDDGCN.py:71-72,76-77) and, layer 1, x·S1 at node
+            # level for both sides (inputs E[h], E[t]): independent GEMMs, batched (one launch below D=256)
+            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], {}) for l in range(NUM_LAYERS) for r in range(R)]
+        else:
+            # relation-sharded: this rank's (relation, node-row) pieces of AE_r and P_r^l, then all-gather P
+            proj = []
+            for r, n0, n1 in sh.pieces():
+                ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + n0:r * (N + 1) + n1 + 1], adj.fwd_col, adj.fwd_val, E,
+                             ws.AE[r][n0:n1].view(1, n1 - n0, D), 1, n1 - n0)
+                proj += [(ws.AE[r][n0:n1], P[f"K{l + 1}"][r], ws.P[l, r][n0:n1], {}) for l in range(NUM_LAYERS)]
         proj.append((E, P["S1"], ws.ES1, {}))
         for i in range(0, len(proj), 16):
             ops.rowgemm_batched(proj[i:i + 16])
+        if sh is not None:
+            for l in range(NUM_LAYERS):
+                sh.all_gather(ws.P[l].view(R * N, D))
         ops.alpha_fwd(E, P["Wa1"], P["ba1"], ws.Ssm[0], ws.W[0])
         ops.gather_rows(ws.W[0], ed.h, ws.Wedge[0])
         ops.combine(ws.ES1, ws.W[0], ws.P[0], ws.X[0])
@@ -338,6 +352,8 @@ class Engine:
         produces them, so the all-reduce of the large dE overlaps the SpMM of the next chunk."""
         N, R, D = self.N, self.R, self.D
         dOn, dOn_next = ws.dOn_a, ws.dOn_b      # head seed dO^3, written by distmult_bce_heads
+        if self.node_shard is not None:
+            ws.dAE.zero_()                      # rows other ranks own stay 0 in the dE SpMM below
         for l in (2, 1, 0):                     # layer index l -> reference layer l+1
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
             do = ws.xt[l]                       # do^{l+1}, written over x^{l+1}
@@ -381,10 +397,21 @@ class Engine:
                             v_row_stride=0)
             # relation kernels: dK_r = AE_r^T dP_r ; dAE_r += dP_r K_r^T
             K, dK = P[f"K{l + 1}"], G[f"K{l + 1}"]
-            for r in range(R):
-                ops.gemm_tn(ws.AE[r], ws.dP[r], dK[r], ws.tn_slab)
-            ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2)))
-                                 for r in range(R)])
+            sh = self.node_shard
+            if sh is None:
+                for r in range(R):
+                    ops.gemm_tn(ws.AE[r], ws.dP[r], dK[r], ws.tn_slab)
+                ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2)))
+                                     for r in range(R)])
+            else:
+                # relation-sharded: the owners sum the edge partials of dP, then form their rows of dK_r (a
+                # partial over rows, all-reduced with the other small gradients) and of dAE_r
+                sh.reduce_scatter(ws.dP.view(R * N, D))
+                dK.zero_()
+                for r, n0, n1 in sh.pieces():
+                    ops.gemm_tn(ws.AE[r][n0:n1], ws.dP[r][n0:n1], dK[r], ws.tn_slab, accumulate=True)
+                ops.rowgemm_batched([(ws.dP[r][n0:n1], K[r], ws.dAE[r][n0:n1], dict(b_trans=True, accumulate=True))
+                                     for r, n0, n1 in sh.pieces()])
             dOn, dOn_next = dOn_next, dOn
         # DistMult rel grad and the loss: every gradient past E is final now
         ops.reduce_slabs(ws.drel_slab, ws.nb_dm, G["rel"])

@@ -77,3 +77,81 @@ class BucketedAllReduce:
         """Whole-buffer form (one bucket)."""
         self.ready(buf)
         self.finish()
+
+
+class RelationShard:
+    """Relation-sharded node tables (SURVEY §8(e)'s alternative to edge partitioning, BASELINE config 4's
+    "relation-sharded" wording), combined with the edge partitioning of the scored edges.
+
+    The per-relation node tables AE_r = A_r E and P_r^l = AE_r K_r^l are the step's node-level work.  Here
+    they are split over the p ranks by flat (relation, node) row r*N + n: rank k computes the rows
+    [k*c, (k+1)*c), c = ceil(R*N / p) — whole relations when p divides R (pure relation sharding: R = 8 on
+    8 GPUs is one relation per GPU), row blocks of relations otherwise — and the ranks exchange:
+      forward   all-gather of P^l (3 x R*N*D floats) so every rank's edge-level work sees every P_r;
+      backward  reduce-scatter of dP^l (the edge partial sums) to the owners, which form dK_r (a
+                partial over their rows, summed with the other small gradients) and dAE_r (their rows);
+                dE = sum_r A_r^T dAE_r then rides in the usual all-reduce of the flat gradient buffer.
+    That is ~6 R*N*D floats of collectives per step against edge partitioning's ~N*D (one dE all-reduce)
+    in exchange for 1/p of the SpMM and node GEMM work; bench.py --shard relation measures the trade.
+    gloo groups (several ranks sharing a GPU in tests) stage the tensors through host memory."""
+
+    def __init__(self, R, N, group=None):
+        self.group = group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.R, self.N = R, N
+        self.RN = R * N
+        self.chunk = -(-self.RN // self.world)
+        self.a = min(self.RN, self.rank * self.chunk)
+        self.b = min(self.RN, self.a + self.chunk)
+        self._gloo = dist.get_backend(group) == "gloo"
+
+    def pieces(self):
+        """(r, n0, n1): the owned rows, per relation."""
+        out = []
+        for r in range(self.R):
+            n0, n1 = max(self.a, r * self.N) - r * self.N, min(self.b, (r + 1) * self.N) - r * self.N
+            if n1 > n0:
+                out.append((r, n0, n1))
+        return out
+
+    def _padded(self, table):
+        import torch
+        need = self.world * self.chunk
+        if need == self.RN:
+            return table, False
+        return torch.zeros(need, table.shape[1], dtype=table.dtype, device=table.device), True
+
+    def all_gather(self, table):
+        """table: [R*N, D] with this rank's rows filled -> every row filled, on every rank."""
+        import torch
+        full, padded = self._padded(table)
+        if padded:
+            full[self.a:self.b].copy_(table[self.a:self.b])
+        mine = full[self.rank * self.chunk:(self.rank + 1) * self.chunk]
+        if self._gloo:
+            host = full.cpu()
+            parts = list(host.split(self.chunk))
+            dist.all_gather(parts, host[self.rank * self.chunk:(self.rank + 1) * self.chunk].clone(), group=self.group)
+            full.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(full, mine, group=self.group)
+        if padded:
+            table.copy_(full[:self.RN])
+
+    def reduce_scatter(self, table):
+        """table: [R*N, D] partial sums on every rank -> this rank's rows hold the sums over ranks."""
+        import torch
+        full, padded = self._padded(table)
+        if padded:
+            full[:self.RN].copy_(table)
+        mine = full[self.rank * self.chunk:(self.rank + 1) * self.chunk]
+        if self._gloo:
+            host = full.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+            mine.copy_(host[self.rank * self.chunk:(self.rank + 1) * self.chunk])
+        else:
+            out = torch.empty_like(mine)
+            dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.group)
+            mine.copy_(out)
+        if padded:
+            table[self.a:self.b].copy_(full[self.a:self.b])

@@ -103,3 +103,43 @@ def test_bucketed_row_chunks_cover_rows():
         assert ch[0][0] == 0 and ch[-1][1] == n
         assert all(a[1] == b[0] for a, b in zip(ch, ch[1:]))
         assert len(ch) <= 4 and (len(ch) == 1 or min(b - a for a, b in ch) >= 100)
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from iddgcn_amd.parallel import RelationShard
+        R, N, D = 3, 5, 4
+        sh = RelationShard(R, N)
+        t = torch.full((R * N, D), -1.0)
+        for r, n0, n1 in sh.pieces():
+            for n in range(n0, n1):
+                t[r * N + n] = r * N + n
+        sh.all_gather(t)
+        u = torch.ones(R * N, D) * (rank + 1)
+        sh.reduce_scatter(u)
+        q.put((rank, sh.pieces(), t.numpy(), u.numpy(), sh.a, sh.b))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_relation_shard_collectives_world2_gloo():
+    """RelationShard (parallel.py): owned (relation, row) pieces partition R*N rows; all_gather fills
+    every row on every rank; reduce_scatter leaves the cross-rank sum in the owned rows (R*N = 15 is not
+    divisible by 2: the padded path)."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rows = sorted(r * 5 + n for _, pieces, *_ in res for r, n0, n1 in pieces for n in range(n0, n1))
+    assert rows == list(range(15))
+    for rank, _, t, u, a, b in res:
+        assert np.array_equal(t[:, 0], np.arange(15))
+        assert np.all(u[a:b] == 3.0)

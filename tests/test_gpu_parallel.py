@@ -118,3 +118,73 @@ def test_fit_world2_gloo_one_gpu_equals_single_process(cuda):
     assert abs(l0 - loss1) <= 1e-6 * loss1
     for k, g in g1.items():
         assert np.abs(g0[k] - g).max() <= 2e-4 * np.abs(g).max() + 1e-30, k
+
+
+def _step_worker(rank, world, port, q, mode, N, R, D):
+    """One data-parallel step (forward + backward + bucketed all-reduce, no Adam) on this rank's shard of
+    the scored edges, edge-partitioned or with relation-sharded node tables."""
+    import torch.distributed as dist
+    from iddgcn_amd.parallel import BucketedAllReduce, RelationShard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        pos, neg = synthetic_graph(N, R, 9000, seed=77)
+        tri = np.concatenate([pos, neg])
+        lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+        lo, hi = shard_range(len(tri), rank, world)
+        eng = Engine(N, R, D, dev)
+        if mode == "relation":
+            eng.node_shard = RelationShard(R, N)
+        P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
+        P.load(_mild(N, R, D, 9))
+        adj = eng.adjacency(get_adj_mats(pos, N, R))
+        ed = eng.edges(tri[lo:hi], lab[lo:hi])
+        comm = BucketedAllReduce(min_bucket_rows=64)
+        ws = eng.workspace(ed.T, True)
+        eng._t_global = len(tri)
+        with eng._precision():
+            eng.forward(P, adj, ed, ws, True)
+            eng.backward(P, G, adj, ed, ws, comm)
+        comm.finish()
+        torch.cuda.synchronize()
+        q.put((rank, float(G.loss.item()), G.to_numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("N,R,D", [(600, 2, 64), (601, 3, 256)])
+def test_relation_sharded_step_equals_full_batch(N, R, D, cuda):
+    """SURVEY §8(e)'s relation-sharded alternative (RelationShard: per-relation node tables split over the
+    ranks by (relation, row), all-gather of P^l, reduce-scatter of dP^l), 2 ranks on one GPU over gloo:
+    the step's loss and every gradient equal the single-process full batch and the edge-partitioned
+    2-rank step (1e-5 of max|g|).  (601, 3): R*N not divisible by the world size (padded collectives)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pos, neg = synthetic_graph(N, R, 9000, seed=77)
+    tri = np.concatenate([pos, neg])
+    lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+    eng = Engine(N, R, D, cuda)
+    P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
+    P.load(_mild(N, R, D, 9))
+    loss, _ = eng.loss_and_grads(P, G, eng.adjacency(get_adj_mats(pos, N, R)), eng.edges(tri, lab))
+    full, full_loss = G.to_numpy(), float(loss.item())
+    del eng, P, G
+    res = {}
+    for mode in ("edge", "relation"):
+        port = _free_port()
+        procs = [ctx.Process(target=_step_worker, args=(r, 2, port, q, mode, N, R, D)) for r in range(2)]
+        for p in procs:
+            p.start()
+        out = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        assert out[0][1] == out[1][1]
+        assert all(np.array_equal(out[0][2][k], out[1][2][k]) for k in full)
+        res[mode] = out[0]
+    for mode, (_, l, g) in res.items():
+        assert abs(l - full_loss) <= 1e-6 * full_loss, mode
+        for k, v in full.items():
+            assert np.abs(g[k] - v).max() <= 1e-5 * np.abs(v).max() + 1e-30, (mode, k)
