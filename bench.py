@@ -213,7 +213,8 @@ def cpu_baseline(cfg, budget_s=25.0):
                        f"{t:.2f} s/step")}
 
 
-def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=True):
+def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=True, shard=None, steps=None,
+                 warmup=None):
     """Build one workload on the GPU, time W + K training steps, return the bench-line fields."""
     import numpy as np
     import torch
@@ -225,6 +226,9 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
 
     cfg = CONFIGS[cid]
     N, R, D = cfg["N"], cfg["R"], cfg["D"]
+    shard = args.shard if shard is None else shard
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
     weak = cfg["scaling"] == "weak"
     M = cfg["M"] * world if weak else cfg["M"]            # weak: per-GPU work fixed
     pos, neg = synthetic_graph(N, R, M, seed=0)           # identical on every rank (seeded)
@@ -244,7 +248,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
     init = reference_init(np, N, R, D, 89)
     comm = BucketedAllReduce() if world > 1 else None
-    if args.shard == "relation" and world > 1:
+    if shard == "relation" and world > 1:
         eng.node_shard = RelationShard(R, N)     # SURVEY §8(e) alternative: node tables split by relation
 
     def timed_run(mode, probe):
@@ -252,7 +256,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         eng.gemm = mode
         P.load(init)                       # every mode starts from the same parameters
         opt = KerasAdam(P)
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             eng.train_step(P, G, opt, adj, ed, t_global=T, comm=comm)
         torch.cuda.synchronize()
         eng.probe = {} if probe else None
@@ -260,7 +264,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             loss = eng.train_step(P, G, opt, adj, ed, t_global=T, comm=comm)
         torch.cuda.synchronize()
         if world > 1:
@@ -274,19 +278,19 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         return elapsed, float(loss.item()) / T, probe_out
 
     elapsed, loss_val, probe = timed_run(gemm, probe_kernels)
-    out = {"value": M / (elapsed / args.steps), "ms_per_step": elapsed / args.steps * 1e3,
+    out = {"value": M / (elapsed / steps), "ms_per_step": elapsed / steps * 1e3,
            "scaling": cfg["scaling"], "dtype": DTYPE_BF16 if feat == "bf16" else DTYPE[gemm],
            "gemm_operands": GEMM_NOTE[gemm] + ("; edge GEMMs bf16 (features=bf16)" if feat == "bf16" else ""),
            "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
                       "scored_edges": T, "scored_edges_per_gpu": ed.T, "feat_dim": D,
                       "parallelism": f"edge-dp{world}" + ("+relation-sharded-nodes" if eng.node_shard else ""),
                       "gemm": gemm, "features": feat},
-           "scored_edges_per_s": T / (elapsed / args.steps), "loss": loss_val}
+           "scored_edges_per_s": T / (elapsed / steps), "loss": loss_val, "steps": steps, "warmup": warmup}
     if other_mode and feat == "f32":
         mode2 = "exact" if gemm == "split" else "split"
         el2, loss2, _ = timed_run(mode2, False)
-        out["other_gemm_mode"] = {"gemm": mode2, "dtype": DTYPE[mode2], "value": M / (el2 / args.steps),
-                                  "ms_per_step": el2 / args.steps * 1e3, "loss": loss2}
+        out["other_gemm_mode"] = {"gemm": mode2, "dtype": DTYPE[mode2], "value": M / (el2 / steps),
+                                  "ms_per_step": el2 / steps * 1e3, "loss": loss2}
     if probe:
         # dominant kernel: largest total event time inside the timed steps; its roofline is the larger
         # of the MFMA time (hardware MFMA work on the mode's peak) and the HBM time (algorithmic bytes)
@@ -295,7 +299,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         rl = kernel_roofline(dom, N, R, D, ed.T, gemm, statistics.mean(kt[dom]), eb=2 if feat == "bf16" else 4)
         rl["traffic"], rl["traffic_source"] = pmc_traffic(dom, gemm, cfg["name"], world)
         rl["box_stream_GBs"] = stream_probe(torch, dev, ed.T, D)
-        out["kernel_ms_per_step"] = {k: sum(v) / args.steps for k, v in kt.items()}
+        out["kernel_ms_per_step"] = {k: sum(v) / steps for k, v in kt.items()}
         out["roofline"] = rl
     del eng, adj, ed, P, G
     torch.cuda.empty_cache()
@@ -308,8 +312,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
-    ap.add_argument("--also", type=int, nargs="*", default=[], choices=sorted(CONFIGS),
-                    help="further workloads timed in the same run, reported under 'also'")
+    ap.add_argument("--also", nargs="*", default=None,
+                    help="further workloads timed in the same run (min(steps, 5) steps, 1 warm-up), reported "
+                         "under 'also': config ids, 'Nr' = config N with relation-sharded node tables; default "
+                         "4 5 (BASELINE configs 4 and 5), plus 4r with more than one GPU; none to skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", default="edge", choices=["edge", "relation"],
                     help="multi-GPU: edge partitioning only (default) or also relation-sharded node tables")
@@ -348,6 +354,7 @@ def main():
     dev = torch.device("cuda", local)
 
     main_out = run_workload(args.config, args, world, rank, dev, args.gemm, not args.no_other_mode)
+    main_out.pop("steps"), main_out.pop("warmup")
     result = {
         "metric": "adjacency edges/s per IDDGCN training step (pos fwd + neg fwd + bwd + Adam)",
         "value": main_out.pop("value"),
@@ -363,9 +370,15 @@ def main():
     }
     result.update(main_out)
     also = []
-    for cid in args.also:
+    todo = (["4", "5"] + (["4r"] if world > 1 else [])) if args.also is None else \
+        [a for a in args.also if a != "none"]
+    for item in todo:
+        cid, shard = int(item.rstrip("r")), ("relation" if item.endswith("r") else "edge")
+        if cid == args.config and shard == args.shard:
+            continue
         try:
-            o = run_workload(cid, args, world, rank, dev, args.gemm, False)
+            o = run_workload(cid, args, world, rank, dev, args.gemm, False, shard=shard,
+                             steps=min(args.steps, 5), warmup=1)
         except torch.OutOfMemoryError as e:      # a secondary workload never costs the headline line
             torch.cuda.empty_cache()
             o = {"config": {"workload": CONFIGS[cid]["name"]}, "error": f"out of memory: {e}"[:300]}

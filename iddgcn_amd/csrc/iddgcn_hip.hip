@@ -2257,7 +2257,10 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
         const long long n = n0 + threadIdx.x / 64;
         const bool live = n < n_nodes;
         int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
-        if constexpr (SLOTS == 1) {     // D = 256: the whole wave is one head, its edges wave-uniform
+        // D = 256 with many relations: the whole wave is one head, so its edges' indices are wave-uniform
+        // and go through scalar loads (R = 8: -13%; at R <= 2 the vector loads are faster, +25% otherwise)
+        constexpr bool SCALAR = SLOTS == 1 && RT >= 4;
+        if constexpr (SCALAR) {
             beg = __builtin_amdgcn_readfirstlane(beg);
             end = __builtin_amdgcn_readfirstlane(end);
         }
@@ -2272,7 +2275,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 e[u] = (k + u < len) ? (long long)perm[beg + k + u] : -1;
-                if constexpr (SLOTS == 1) e[u] = __builtin_amdgcn_readfirstlane((int)e[u]);   // scalar loads below
+                if constexpr (SCALAR) e[u] = __builtin_amdgcn_readfirstlane((int)e[u]);   // scalar loads below
             }
             int rr[U];
             float yy[U];
@@ -2282,7 +2285,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 const bool ok = e[u] >= 0;
                 rr[u] = ok ? r_idx[e[u]] : 0;
                 yy[u] = (ok && y) ? y[e[u]] : 0.f;
-                if constexpr (SLOTS == 1) rr[u] = __builtin_amdgcn_readfirstlane(rr[u]);
+                if constexpr (SCALAR) rr[u] = __builtin_amdgcn_readfirstlane(rr[u]);
                 b[u] = ok ? ld4e<BF>(Xt, e[u] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
 #pragma unroll
@@ -2422,7 +2425,10 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     const int slot = (threadIdx.x % 64) / LPR;
     const bool live = n < n_nodes;
     int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
-    if constexpr (SLOTS == 1) {      // D = 256: one node per wave, its edge rows (and W rows) wave-uniform
+    // D = 256 with many relations: one node per wave, its edge rows (and W rows) wave-uniform, the R
+    // coefficients of an edge through scalar loads (R = 8: -39%; at R <= 2 the vector loads are faster)
+    constexpr bool SCALAR = SLOTS == 1 && R >= 4;
+    if constexpr (SCALAR) {
         beg = __builtin_amdgcn_readfirstlane(beg);
         end = __builtin_amdgcn_readfirstlane(end);
     }
@@ -2446,7 +2452,7 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             const bool a = k + u < len;
             // h_idx == NULL: W is already per edge (W[e][r], gathered once per layer)
             hh[u] = a ? (h_idx ? h_idx[beg + k + u] : beg + k + u) : 0;
-            if constexpr (SLOTS == 1) hh[u] = __builtin_amdgcn_readfirstlane(hh[u]);     // scalar W loads
+            if constexpr (SCALAR) hh[u] = __builtin_amdgcn_readfirstlane(hh[u]);     // scalar W loads
             d[u] = a ? ld4e<BF>(dO, (long long)(beg + k + u) * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
         float w[U][R];

@@ -8,9 +8,10 @@ TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="bench.py --no-cpu-baseline --no-other-mode --steps 5 --warmup 2"
+BENCH="bench.py --no-cpu-baseline --no-other-mode --also none --steps 5 --warmup 2"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${2:-} > "$OUT/gpu_tests.log" 2>&1 &&
 timeout -k 10 300 python -u bench.py > "$OUT/bench.json.log" 2>&1 &&
+timeout -k 10 120 python -u $BENCH > "$OUT/bench_profiled_cmd.json.log" 2>&1 &&
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $BENCH > "$OUT/bench_traced.log" 2>&1 &&
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 $BENCH > "$OUT/pmc_fetch.log" 2>&1 &&
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 $BENCH > "$OUT/pmc_write.log" 2>&1

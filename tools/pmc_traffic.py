@@ -20,13 +20,13 @@ import sys
 import pandas as pd
 
 SYMBOLS = {
-    "split": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, true, false>",
-              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false>",
-              "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, true, true>",
-              "tail_dS_tn": "gemm_tn256_x3_kernel"},
-    "exact": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, false, false>",
-              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, false, false>",
-              "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, false, true>",
+    "split": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, true, false, false, false>",
+              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, false, false>",
+              "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, true, true, false, false>",
+              "tail_dS_tn": "gemm_tn256_x3_kernel<false>"},
+    "exact": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, false, false, false, false>",
+              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, false, false, false, false>",
+              "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, false, true, false, false>",
               "tail_dS_tn": "gemm_tn256_dma_kernel"},
 }
 
