@@ -619,6 +619,9 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
 #ifndef V3_ABL
 #define V3_ABL 0
 #endif
+#ifndef V3_CAP2
+#define V3_CAP2 0
+#endif
 namespace r3 {
 constexpr int D = 256, NW = 8, TR = 32;
 constexpr int ROWS_PER_WAVE = TR / NW;                 // A rows each wave stages
@@ -709,6 +712,8 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     static_assert(!REC || (NV >= 2 && NV <= 3 && !AUX && HAS_COEF), "REC: V_0 + coefficient-weighted V_1.., no aux");
     static_assert(REC || NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
     constexpr bool WIDE = !REC && NV > 2;              // capped slabs, run-time R <= NV
+    // capped V slabs r >= 1 (rows past the cap read from L2): WIDE, and NV = 2 when V3_CAP2 > 0
+    constexpr bool CAPPED = WIDE || (V3_CAP2 > 0 && NV == 2 && !REC);
     // the sigma' slab: after the V slabs; BF keeps it out of slab 0, whose fp32 staging of the output
     // would overwrite bf16 aux rows other lanes have not read yet (different row pitches)
     constexpr int AUXS = (BF && NV == 0) ? 1 : NV;
@@ -716,7 +721,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     constexpr int NSL = NS > 1 ? NS : 1;               // slabs per wave (slab 0 also stages C)
     // Slab 0 holds 32 rows (it also stages the C tile); REC slabs r >= 1 hold REC_CAP rows, WIDE
     // slabs r >= 1 GATHER_CAP rows.
-    constexpr int CAPV = REC ? REC_CAP : (WIDE ? GATHER_CAP : 32);
+    constexpr int CAPV = REC ? REC_CAP : (WIDE ? GATHER_CAP : (CAPPED ? V3_CAP2 : 32));
     constexpr int SLABC = CAPV * 32;
     constexpr int SLABS = SLAB + (NSL - 1) * SLABC;    // floats of all slabs of one wave
     // coefficient slots: 32 rows x R; up to 8 relations for WIDE and for broadcast V (NV = 0)
@@ -793,6 +798,10 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // [hi plane 512 B | lo plane 512 B] (k-natural order), and records 1/scale per row
     auto convert_rows = [&](int bb) {
         if constexpr (X3 && !BF) {
+            if (V3_ABL & 16) {
+                if (lane < ROWS_PER_WAVE) rowinv[bb * TR + wave * ROWS_PER_WAVE + lane] = 1.0f;
+                return;
+            }
             float* base = bufA + bb * A_FLOATS;
             f32x4 x[ROWS_PER_WAVE];
             float m[ROWS_PER_WAVE];
@@ -844,18 +853,18 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
         }
         __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)idxw, 4, 0, 0);
     };
-    // A-row gather indices: lanes 0..3 hold this wave's 4 rows; SGPR copies sa[]
-    auto load_aidx = [&](long long t) -> int {
-        if (!p.a_idx || lane >= ROWS_PER_WAVE || t >= t_end) return 0;
-        return p.a_idx[clampe(t * TR + wave * ROWS_PER_WAVE + lane)];
-    };
-    int sa[ROWS_PER_WAVE];
-    auto to_sgpr = [&](int v) {
-#pragma unroll
-        for (int j = 0; j < ROWS_PER_WAVE; ++j) sa[j] = __builtin_amdgcn_readlane(v, j);
-    };
-
+    // A rows of tile t into buffer b.  Gathered rows (a_idx, an API-only form: the training step never
+    // gathers A) load their 4 indices synchronously inside this uniform branch, so no register-destination
+    // load is ever left in flight across the pipelined LDS-DMA code (the compiler would otherwise guard
+    // its result with a vmcnt(0) that also drains every DMA in flight).
     auto dma_A = [&](long long t, int b) {
+        if (V3_ABL & 64) return;
+        int sa[ROWS_PER_WAVE];
+        if (p.a_idx) {
+            const int v = lane < ROWS_PER_WAVE ? p.a_idx[clampe(t * TR + wave * ROWS_PER_WAVE + lane)] : 0;
+#pragma unroll
+            for (int j = 0; j < ROWS_PER_WAVE; ++j) sa[j] = __builtin_amdgcn_readlane(v, j);
+        }
 #pragma unroll
         for (int j = 0; j < ROWS_PER_WAVE; ++j) {
             const int r = wave * ROWS_PER_WAVE + j;
@@ -905,7 +914,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                     if constexpr (WIDE) {
                         if (r >= R) break;
                     }
-                    if constexpr (REC || WIDE) {
+                    if constexpr (REC || CAPPED) {
                         // capped slab: rows past CAPV stay unwritten (precondition broken: stay in bounds)
                         if (r > 0 && row >= CAPV) continue;
                     }
@@ -975,9 +984,10 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                 for (int r = 0; r < CFN; ++r)
                     if (r < R) cf[r] = coefw[i * R + r];
             } else if (REC ? R == 2 : (NV == 2 || (NV == 0 && R == 2))) {
-                const float2 c2 = *reinterpret_cast<const float2*>(coefw + i * 2);
-                cf[0] = c2.x;
-                cf[1] = c2.y;
+                // two scalar reads (merged into one ds_read_b64): a float2-typed LDS read here made the
+                // compiler guard it with a vmcnt(0) that drained the A-tile DMA in flight
+                cf[0] = coefw[i * 2];
+                cf[1] = coefw[i * 2 + 1];
             } else {
                 cf[0] = coefw[i];
             }
@@ -1013,7 +1023,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                         if (r >= R) break;
                     }
                     f32x4 s = ld4(slabw + soff(r) + offv);
-                    if constexpr (WIDE) {
+                    if constexpr (CAPPED) {
                         if (r > 0 && vslot >= CAPV) {    // a distinct row past the capped slab: from L2
                             const int vrow = cmpw[vslot];
                             typedef const __attribute__((address_space(1))) f32x4* gf4p;
@@ -1073,24 +1083,15 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
 
     // ---- prologue: A(t_beg), indices and epilogue slabs of t_beg, indices of t_beg+1 ------
     {
-        const int a0 = load_aidx(t_beg);
         dma_idx(t_beg);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        to_sgpr(a0);
         dma_A(t_beg, 0);
-        if constexpr (PD == 2) {
-            const int a1 = load_aidx(t_beg + 1);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            to_sgpr(a1);
-            dma_A(t_beg + 1, 1);
-        }
-        const int an0 = load_aidx(t_beg + PD);
+        if constexpr (PD == 2) dma_A(t_beg + 1, 1);
         dma_slabs(t_beg);
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         convert_rows(0);
         dma_idx(t_beg + 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        to_sgpr(an0);
         __syncthreads();
     }
     // s_waitcnt vmcnt(n): everything but the n youngest vector-memory ops of this wave has landed
@@ -1117,9 +1118,8 @@ _Pragma("unroll") \
             /* A(t+PD) into the buffer of tile t-1 (its MFMAs ended before the last barrier) */ \
             const bool more = t + PD < t_end; \
             if (more) dma_A(t + PD, PD == 2 ? b2 : b1); \
-            const int an = load_aidx(t + PD + 1); \
-            /* ops issued so far this iteration (the youngest): A(t+PD) rows, the a_idx load */ \
-            const int n_new = (more ? ROWS_PER_WAVE : 0) + ((p.a_idx && t + PD + 1 < t_end) ? 1 : 0); \
+            /* ops issued so far this iteration (the youngest): the A(t+PD) rows */ \
+            const int n_new = more ? ROWS_PER_WAVE : 0; \
             if (LATE && t > t_beg) { \
                 wait_newest(n_new);          /* slabs(t-1), idx(t) and every older op */ \
                 epilogue(t - 1, acc); \
@@ -1171,7 +1171,7 @@ _Pragma("unroll") \
                 ah[0] = __builtin_bit_cast(f16x8, ld4(arow)); \
                 al[0] = __builtin_bit_cast(f16x8, ld4(arow + 128)); \
 _Pragma("unroll") \
-                for (int q = 0; q < D / 16; ++q) { \
+                for (int q = 0; q < ((V3_ABL & 32) ? 0 : D / 16); ++q) { \
                     const int cu = q & 1; \
                     if (q + 1 < D / 16) { \
                         ah[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + 8 * (q + 1))); \
@@ -1209,7 +1209,6 @@ _Pragma("unroll") \
                     dma_idx(t + 2); \
                 } \
             } \
-            to_sgpr(an); \
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
             __builtin_amdgcn_s_barrier(); \
             asm volatile("" ::: "memory"); \

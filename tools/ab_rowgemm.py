@@ -3,7 +3,8 @@
 Every library is driven through its own iddgcn_rowgemm_f32 entry point (the iddgcn_rowgemm_t layout
 is unchanged since ABI 2, so older builds load too), on the same inputs, in split-fp16 mode, at the
 config-3 shapes: T = 4M edge rows, N = 100k node rows.
-usage: python tools/ab_rowgemm.py lib_a.so [lib_b.so ...]
+usage: python tools/ab_rowgemm.py [--cases fwd,bwd,...] [--rounds K] lib_a.so [lib_b.so ...]
+(the libraries are timed round-robin, K rounds, 10 launches each; the per-case median over rounds is printed)
 """
 import ctypes
 import sys
@@ -23,7 +24,7 @@ def load(path):
     return lib
 
 
-def main(paths, reps=5):
+def main(paths, reps=10, rounds=3, only=None):
     dev = torch.device("cuda", 0)
     T, N, D, R = 4_000_000, 100_000, 256, 2
     g = torch.Generator(device=dev).manual_seed(0)
@@ -41,31 +42,47 @@ def main(paths, reps=5):
     WaT = torch.randn(R, D, device=dev, generator=g)
     xin = x.clone()
     cases = {
-        "fwd_combine (T)": (x, S, C, dict(coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)),
-        "bwd_dsig separate C (T)": (do, S, C, dict(b_trans=True, act=L.ACT_DSIGMOID, aux=x)),
-        "bwd_dsig C = aux (T)": (do, S, xin, dict(b_trans=True, act=L.ACT_DSIGMOID, aux=xin)),
-        "node bcast+dsig (N)": (dOn, S, Cn, dict(b_trans=True, coef=dz, V=WaT, v_rel_stride=D, v_row_stride=0,
-                                                act=L.ACT_DSIGMOID, aux=Xn)),
-        "node bcast (N)": (dOn, S, Cn, dict(b_trans=True, coef=dz, V=WaT, v_rel_stride=D, v_row_stride=0)),
-        "node plain (N)": (Xn, S, Cn, dict()),
+        "fwd": ("fwd_combine (T)", x, S, C, dict(coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)),
+        "bwd": ("bwd_dsig separate C (T)", do, S, C, dict(b_trans=True, act=L.ACT_DSIGMOID, aux=x)),
+        "bwdip": ("bwd_dsig C = aux (T)", do, S, xin, dict(b_trans=True, act=L.ACT_DSIGMOID, aux=xin)),
+        "nbd": ("node bcast+dsig (N)", dOn, S, Cn, dict(b_trans=True, coef=dz, V=WaT, v_rel_stride=D, v_row_stride=0,
+                                                        act=L.ACT_DSIGMOID, aux=Xn)),
+        "nb": ("node bcast (N)", dOn, S, Cn, dict(b_trans=True, coef=dz, V=WaT, v_rel_stride=D, v_row_stride=0)),
+        "np": ("node plain (N)", Xn, S, Cn, dict()),
     }
+    if only:
+        cases = {k: v for k, v in cases.items() if k in only}
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    libs = [load(p) for p in paths]
+    res = {(p, k): [] for p in paths for k in cases}
+    for _ in range(rounds):
+        for path, lib in zip(paths, libs):
+            lib.iddgcn_set_gemm_precision(L.GEMM_SPLIT_F16)
+            for k, (name, A, B, Cc, kw) in cases.items():
+                args = ops._rowgemm_args(A, B, Cc, **kw)
+                for _ in range(2):
+                    assert lib.iddgcn_rowgemm_f32(st, ctypes.byref(args)) == 0
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    lib.iddgcn_rowgemm_f32(st, ctypes.byref(args))
+                e1.record()
+                torch.cuda.synchronize()
+                res[(path, k)].append(e0.elapsed_time(e1) / reps * 1e3)
     for path in paths:
-        lib = load(path)
-        lib.iddgcn_set_gemm_precision(L.GEMM_SPLIT_F16)
         print(f"--- {path}", flush=True)
-        for name, (A, B, Cc, kw) in cases.items():
-            args = ops._rowgemm_args(A, B, Cc, **kw)
-            for _ in range(2):
-                assert lib.iddgcn_rowgemm_f32(st, ctypes.byref(args)) == 0
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(reps):
-                lib.iddgcn_rowgemm_f32(st, ctypes.byref(args))
-            e1.record()
-            torch.cuda.synchronize()
-            print(f"{name:28s} {e0.elapsed_time(e1) / reps * 1e3:9.1f} us", flush=True)
+        for k, (name, *_r) in cases.items():
+            v = sorted(res[(path, k)])
+            print(f"{name:28s} {v[len(v) // 2]:9.1f} us   (min {v[0]:.1f}, max {v[-1]:.1f})", flush=True)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    argv = sys.argv[1:]
+    only, rounds = None, 3
+    while argv and argv[0].startswith("--"):
+        if argv[0] == "--cases":
+            only = argv[1].split(",")
+        elif argv[0] == "--rounds":
+            rounds = int(argv[1])
+        argv = argv[2:]
+    main(argv, rounds=rounds, only=only)
