@@ -241,7 +241,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
                           np.zeros(max(0, hi - max(lo, npos)), np.float32)])
     feat = args.features or cfg.get("features", "f32")
     eng = Engine(N, R, D, dev, gemm=gemm, recompute_x1=args.recompute_x1, fuse_tail_seg=args.fuse_tail_seg,
-                 features=feat)
+                 features=feat, planes=not args.no_planes)
     adj = get_adj_mats(pos, N, R, device=dev)            # device graph build (bit-identical to the host's)
     ed = eng.edges(tri, lab)
     del pos, neg, tri, lab
@@ -317,6 +317,8 @@ def main():
                          "under 'also': config ids, 'Nr' = config N with relation-sharded node tables; default "
                          "4 5 (BASELINE configs 4 and 5), plus 4r with more than one GPU; none to skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-planes", action="store_true",
+                    help="fp32 tail tables x^1, x^2 instead of the pre-split planes form (A/B)")
     ap.add_argument("--shard", default="edge", choices=["edge", "relation"],
                     help="multi-GPU: edge partitioning only (default) or also relation-sharded node tables")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],

@@ -12,10 +12,11 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID, ACT_DSIGMOID_COMBINE = 0, 1, 2, 3
 GEMM_EXACT_F32, GEMM_SPLIT_F16 = 0, 1
+PLANES_A, PLANES_C, PLANES_AUX = 1, 2, 4          # iddgcn_rowgemm_t.planes (pre-split edge tables, ABI 4)
 
 vp = ctypes.c_void_p
 ci = ctypes.c_int
@@ -36,6 +37,7 @@ class RowGemmArgs(ctypes.Structure):
         ("v_rel_stride", cll), ("v_row_stride", cll),
         ("act", ci), ("aux", vp),
         ("v_runs_max", ci),
+        ("planes", ci),
     ]
 
 
@@ -72,6 +74,8 @@ SIGNATURES = {
     "iddgcn_rowgemm_bf16": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
     "iddgcn_gemm_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
     "iddgcn_combine_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
+    "iddgcn_combine_planes_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
+    "iddgcn_gemm_tn_planes_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
     "iddgcn_distmult_bce_bf16": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci]),
     "iddgcn_distmult_bce_heads_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
                                             vp, ci]),

@@ -306,6 +306,7 @@ struct RowGemmP {
     long long v_rel_stride, v_row_stride;
     int act; const float* aux;
     int v_runs_max;
+    int planes;           // IDDGCN_PLANES_A | _C | _AUX (D = 256 split mode, v3 kernel only)
     int tiles_per_block;
 };
 
@@ -645,9 +646,11 @@ constexpr int GATHER_CAP = 7;
 // [2^14, 2^15), then split  x*s = hi + lo*2^-11  with hi = fp16_rne(x*s) and
 // lo = fp16_rne((x*s - hi) * 2^11)  (x*s - hi is exact in fp32).  hi + lo*2^-11 carries 22
 // significant bits: the representation error is <= 2^-22 |x*s| (<= 2^-25 absolute below 2^-3 of
-// scaled range), under the sqrt(K)*2^-24 error of the K = 256 fp32 dot product itself.  A row GEMM
-// then takes three f16 MFMAs per k-step (hi*hi into one accumulator, hi*lo + lo*hi into a second,
-// combined as acc_hi + 2^-11 acc_lo) in place of eight f32 ones: 96 instead of 512 MFMA cycles.
+// scaled range), under the sqrt(K)*2^-24 error of the K = 256 fp32 dot product itself.  That is the
+// weight (column) split; the edge-row (A) side keeps lo in the units of hi (split16_same below, same
+// 22 bits while lo is a normal fp16), the form the pre-split planes tables store.  A row GEMM then
+// takes three f16 MFMAs per k-step (W_hi*A_hi + W_hi*A_lo into one accumulator, W_lo*A_hi into a
+// second, combined as acc_hi + 2^-11 acc_lo) in place of eight f32 ones: 96 instead of 512 MFMA cycles.
 __device__ __forceinline__ float pow2_scale(float amax) {     // s with amax*s in [2^14, 2^15)
     const int eb = (__float_as_int(amax) >> 23) & 0xFF;
     int se = 268 - eb;                                         // 2^(15 - (eb - 126))
@@ -660,6 +663,47 @@ __device__ __forceinline__ float pow2_inv(float s) {           // exact 1/s for 
 __device__ __forceinline__ void split16(float xs, _Float16& hi, _Float16& lo) {
     hi = (_Float16)xs;
     lo = (_Float16)((xs - (float)hi) * 2048.0f);
+}
+// the A-side (edge row) split: lo in the units of hi, lo = fp16(xs - hi) (|lo| <= ulp(hi) / 2: 11 more
+// significant bits; for xs below 2^-3 of the row's range lo goes subnormal and only bits below 2^-38 of
+// the row max are lost)
+__device__ __forceinline__ void split16_same(float xs, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)xs;
+    lo = (_Float16)(xs - (float)hi);
+}
+// ---- pre-split edge tables ("planes", IDDGCN_PLANES_*) --------------------------------------
+// A D = 256 row of values in [0, 1] (the sigmoid outputs x^1, x^2 of the tail chain) stored in 8
+// column blocks of 128 B, block b = [hi f16 of columns 32b..32b+31 | lo f16 of the same columns] (1 KiB,
+// the bytes of the fp32 row; block b occupies exactly the bytes of fp32 columns 32b..32b+31, so a kernel
+// whose wave w owns columns 32w.. can overwrite a planes row with fp32 results in place, wave-locally),
+// with the fixed scale 2^15: x*2^15 = hi + lo (split16_same).  The producer's epilogue splits once; the GEMMs that read the row
+// (the next layer's forward as A, the dS TN as A, the backward's sigma' operand) skip the per-tile
+// conversion.  This is the representation the per-row split gives rows whose max is in [0.5, 1)
+// (22 significant bits; absolute error <= 2^-24).
+constexpr float PLANE_S = 0x1p15f, PLANE_INV = 0x1p-15f;
+__device__ __forceinline__ void to_planes4(const f32x4& v, f16x4& hv, f16x4& lv) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        _Float16 hi, lo;
+        split16_same(v[q] * PLANE_S, hi, lo);
+        hv[q] = hi;
+        lv[q] = lo;
+    }
+}
+__device__ __forceinline__ f32x4 from_planes4(const f16x4& hv, const f16x4& lv) {
+    f32x4 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = ((float)hv[q] + (float)lv[q]) * PLANE_INV;
+    return x;
+}
+// byte offset of the hi f16 of column c in a planes row (its lo: + 64)
+__device__ __forceinline__ constexpr int plane_off(int c) { return 128 * (c >> 5) + 2 * (c & 31); }
+// store 4 values of columns c..c+3 (c % 4 == 0) of a planes row (row_base = the row's first byte)
+__device__ __forceinline__ void st_planes4(char* row_base, int c, const f32x4& v) {
+    f16x4 hv, lv;
+    to_planes4(v, hv, lv);
+    *reinterpret_cast<f16x4*>(row_base + plane_off(c)) = hv;
+    *reinterpret_cast<f16x4*>(row_base + plane_off(c) + 64) = lv;
 }
 // maxima over the 64 lanes of four values at once (halving butterfly: 2 + 1 swaps, 4 DPP steps);
 // on return m[j] is wave-uniform
@@ -704,10 +748,15 @@ constexpr int REC_CAP = 8;
 // BF: the bf16-feature mode (perf only): A, the sigma' operand and C are bf16 edge tables (512-B rows;
 // A lands in the hi-plane slot of an LDS row as it is), the weights a bf16 hi + lo pair, two
 // v_mfma_f32_32x32x16_bf16 per k-step, fp32 accumulation and epilogue.  X3 must be set with it.
-template <int NV, bool AUX, bool HAS_COEF, bool X3, bool REC = false, bool CW = false, bool BF = false>
+// PL (split mode): the planes form (IDDGCN_PLANES_*) of the variant: AUX kernels read the sigma' operand
+// as planes rows, gathered-combine kernels (NV = 1, 2) write C as planes rows.
+// (A planes rows are a run-time flag of every X3 kernel: convert_rows just skips.)
+template <int NV, bool AUX, bool HAS_COEF, bool X3, bool REC = false, bool CW = false, bool BF = false, bool PL = false>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     using namespace r3;
     const RowGemmP p = pb.p[blockIdx.y];
+    static_assert(!PL || (X3 && !BF && !REC && !CW && ((AUX && NV == 0) || (!AUX && (NV == 1 || NV == 2)))),
+                  "PL: split-mode sigma' backward or R <= 2 gathered forward");
     static_assert(!BF || (X3 && !REC), "BF: the 16-bit A-plane pipeline, no recompute");
     static_assert(!REC || (NV >= 2 && NV <= 3 && !AUX && HAS_COEF), "REC: V_0 + coefficient-weighted V_1.., no aux");
     static_assert(REC || NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
@@ -732,9 +781,12 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     constexpr int WF = SLABS + COEFN + IDX + CMP + CINV;
     // A-tile pipeline depth: three buffers (A(t+2) in flight while A(t) feeds the MFMAs) when the
     // LDS budget allows, two otherwise
-    constexpr int NBUF = (3 * A_FLOATS + NW * WF + 3 * TR) * 4 <= 160 * 1024 ? 3 : 2;
+    // broadcast V rows (NV = 0 with coefficients: one R x D table for every row) staged in LDS once, so the
+    // epilogue never issues a register-destination global load (its vmcnt wait would drain the DMAs)
+    constexpr int BV = (NV == 0 && HAS_COEF) ? CFN * D : 0;
+    constexpr int NBUF = (3 * A_FLOATS + NW * WF + 3 * TR + BV) * 4 <= 160 * 1024 ? 3 : 2;
     constexpr int PD = NBUF - 1;                       // prefetch distance in tiles
-    constexpr int LDSF = NBUF * A_FLOATS + NW * WF + NBUF * TR;
+    constexpr int LDSF = NBUF * A_FLOATS + NW * WF + NBUF * TR + BV;
     static_assert(LDSF * 4 <= 160 * 1024, "LDS budget");
     auto soff = [](int r) { return r == 0 ? 0 : SLAB + (r - 1) * SLABC; };   // slab r of a wave
     __shared__ __attribute__((aligned(16))) float lds[LDSF];
@@ -748,6 +800,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     float* coefw = slabw + SLABS;                              // [32][R]
     float* cinvw = slabw + WF - CINV;                          // [32] (X3)
     float* rowinv = lds + NBUF * A_FLOATS + NW * WF;           // [NBUF][TR] (X3)
+    float* bvl = rowinv + NBUF * TR;                           // [CFN][D] broadcast V rows (BV)
     const int R = p.R;
 
     // weights: exact f32 (breg, B[kk][c0+i] for 4 k-steps of 32x32x2 per ds_read) or, X3, the
@@ -776,7 +829,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             blo[q] = __builtin_bit_cast(f16x8, lv);
         }
     } else {
-        auto bval = [&](int k) { return p.b_trans ? p.B[(c0 + i) * D + k] : p.B[k * D + c0 + i]; };
+        auto bval = [&](int k) __attribute__((always_inline)) { return p.b_trans ? p.B[(c0 + i) * D + k] : p.B[k * D + c0 + i]; };
         float cm = 0.f;
         for (int q = 0; q < D / 16; ++q)
 #pragma unroll
@@ -796,10 +849,10 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     }
     // X3: the wave converts its own ROWS_PER_WAVE rows of A buffer bb in place, fp32 row ->
     // [hi plane 512 B | lo plane 512 B] (k-natural order), and records 1/scale per row
-    auto convert_rows = [&](int bb) {
+    auto convert_rows = [&](int bb) __attribute__((always_inline)) {
         if constexpr (X3 && !BF) {
-            if (V3_ABL & 16) {
-                if (lane < ROWS_PER_WAVE) rowinv[bb * TR + wave * ROWS_PER_WAVE + lane] = 1.0f;
+            if ((V3_ABL & 16) || (p.planes & IDDGCN_PLANES_A)) {   // rows arrive split (fixed scale)
+                if (lane < ROWS_PER_WAVE) rowinv[bb * TR + wave * ROWS_PER_WAVE + lane] = PLANE_INV;
                 return;
             }
             float* base = bufA + bb * A_FLOATS;
@@ -819,13 +872,13 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     _Float16 hi, lo;
-                    split16(x[j][e] * s, hi, lo);
+                    split16_same(x[j][e] * s, hi, lo);
                     hv[e] = hi;
                     lv[e] = lo;
                 }
                 char* rowp = reinterpret_cast<char*>(base + r * LDA);
-                *reinterpret_cast<f16x4*>(rowp + lane * 8) = hv;
-                *reinterpret_cast<f16x4*>(rowp + 512 + lane * 8) = lv;
+                *reinterpret_cast<f16x4*>(rowp + plane_off(lane * 4)) = hv;        // the planes layout
+                *reinterpret_cast<f16x4*>(rowp + plane_off(lane * 4) + 64) = lv;
                 if (lane == 0) rowinv[bb * TR + r] = pow2_inv(s);
             }
         }
@@ -837,13 +890,13 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     if (t_end > ntiles) t_end = ntiles;
     if (t_beg >= t_end) return;
     const long long Mlast = (long long)p.M - 1;
-    auto clampe = [&](long long e) { return e > Mlast ? Mlast : e; };
+    auto clampe = [&](long long e) __attribute__((always_inline)) { return e > Mlast ? Mlast : e; };
 
     // ---- row indices of the next tile: DMA'd into a wave-private LDS slot -------------
     int* idxw = reinterpret_cast<int*>(coefw + COEFN);         // [0,32) v_idx, [32,64) coef_idx
     int vslot = 0;                                               // slab row of this lane's V row
     const bool need_idx = (NV > 0 && p.v_idx) || (HAS_COEF && p.coef_idx);
-    auto dma_idx = [&](long long t) {
+    auto dma_idx = [&](long long t) __attribute__((always_inline)) {
         if (!need_idx || t >= t_end) return;
         const int* g = p.v_idx ? p.v_idx : p.coef_idx;          // valid dummy for unused lanes
         if (lane < 32) {
@@ -857,7 +910,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // gathers A) load their 4 indices synchronously inside this uniform branch, so no register-destination
     // load is ever left in flight across the pipelined LDS-DMA code (the compiler would otherwise guard
     // its result with a vmcnt(0) that also drains every DMA in flight).
-    auto dma_A = [&](long long t, int b) {
+    auto dma_A = [&](long long t, int b) __attribute__((always_inline)) {
         if (V3_ABL & 64) return;
         int sa[ROWS_PER_WAVE];
         if (p.a_idx) {
@@ -889,7 +942,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // ceil(u / 8) DMA instructions per relation fetch the u distinct rows.  Each lane keeps the
     // slot of its row for the epilogue (vslot).
     int* cmpw = idxw + r3::IDX;
-    auto dma_slabs = [&](long long t) {
+    auto dma_slabs = [&](long long t) __attribute__((always_inline)) {
         if (V3_ABL & 1) return;
         if (NV > 0) {
             int vi = 0;
@@ -933,6 +986,9 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                     __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + soff(AUXS) + k * 256), 16, 0, 0);
                 }
             } else {
+                // the wave's 128 B of each row: fp32 columns c0..c0+31 (logical 16-B group g = columns
+                // c0 + 4g..4g+3) or, planes rows (IDDGCN_PLANES_AUX), column block c0/32 (g < 4: hi of columns
+                // c0 + 8g..8g+7, g >= 4: lo of columns c0 + 8(g-4)..)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int row = 8 * k + (lane >> 3);
@@ -965,7 +1021,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // per wave through a per-tile buffer resource whose range check drops rows past M.
     const int sw = (i >> 1) & 7;
     constexpr int EB = BF ? 2 : 4;                     // bytes per edge-table element
-    auto out_rsrc = [&](long long t) {
+    auto out_rsrc = [&](long long t) __attribute__((always_inline)) {
         const long long row0 = t * TR;
         const long long left = (long long)p.M - row0;
         const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * EB);
@@ -973,7 +1029,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                                                  0x00020000);
     };
     // stage phase: combine + activation into slab 0 (LDS only, plus the C loads of `accumulate`)
-    auto epi_stage = [&](long long t, const f32x16& acc) {
+    auto epi_stage = [&](long long t, const f32x16& acc) __attribute__((always_inline)) {
         const __amdgpu_buffer_rsrc_t rc = out_rsrc(t);
         float cf[CFN];
 #pragma unroll
@@ -990,6 +1046,17 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                 cf[1] = coefw[i * 2 + 1];
             } else {
                 cf[0] = coefw[i];
+            }
+        }
+        // PL backward: the planes sigma' rows share slab 0 with the fp32 staging of the output, in another
+        // layout (a lane's hi / lo bytes are not the 16 B it writes back): read all four column groups first
+        f16x4 aux_h[PL && AUX ? 4 : 1], aux_l[PL && AUX ? 4 : 1];
+        if constexpr (PL && AUX) {
+            const char* rowp = reinterpret_cast<const char*>(slabw + soff(AUXS) + i * 32);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                aux_h[j] = *reinterpret_cast<const f16x4*>(rowp + 16 * (j ^ sw) + 8 * h);
+                aux_l[j] = *reinterpret_cast<const f16x4*>(rowp + 16 * ((4 + j) ^ sw) + 8 * h);
             }
         }
 #pragma unroll
@@ -1033,11 +1100,11 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
                 }
-            } else if (HAS_COEF) {      // broadcast V rows (v_row_stride == 0): tiny, cache-resident
+            } else if (HAS_COEF) {      // broadcast V rows (v_row_stride == 0), staged in LDS (bvl)
 #pragma unroll
                 for (int r = 0; r < CFN; ++r) {
                     if (r >= R) break;
-                    const f32x4 s = ld4(p.V + r * p.v_rel_stride + col);
+                    const f32x4 s = ld4(bvl + r * D + col);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
                 }
@@ -1045,12 +1112,15 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             if (p.act == IDDGCN_ACT_SIGMOID && !(V3_ABL & 8)) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
-            } else if (p.act == IDDGCN_ACT_DSIGMOID) {
+            } else if (AUX && p.act == IDDGCN_ACT_DSIGMOID) {
                 f32x4 x;
-                if constexpr (BF)
+                if constexpr (BF) {
                     x = ld4bf(reinterpret_cast<const __bf16*>(slabw + soff(AUXS)) + i * 32 + 8 * j + 4 * h);
-                else
+                } else if constexpr (PL) {
+                    x = from_planes4(aux_h[j], aux_l[j]);
+                } else {
                     x = ld4(slabw + soff(AUXS) + off);
+                }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = v[q] * (x[q] * (1.0f - x[q]));
             }
@@ -1058,7 +1128,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
         }
     };
     // store phase: row-major re-read of slab 0, 4 buffer_store_dwordx4 per wave
-    auto epi_store = [&](long long t) {
+    auto epi_store = [&](long long t) __attribute__((always_inline)) {
         const __amdgpu_buffer_rsrc_t rc = out_rsrc(t);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -1069,20 +1139,33 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                 asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
                 continue;
             }
-            if constexpr (BF)
+            if constexpr (BF) {
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, f32_to_bf4(o)), rc,
                                                       (row * D + c0 + cg * 4) * 2, 0, 0);
-            else
+            } else if constexpr (PL && !AUX) {           // IDDGCN_PLANES_C: sigmoid values in [0, 1], planes row
+                f16x4 hv, lv;
+                to_planes4(o, hv, lv);
+                const int vo = row * 1024 + plane_off(c0 + cg * 4);      // lo: soffset 64
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hv), rc, vo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lv), rc, vo, 64, 0);
+            } else {
                 __builtin_amdgcn_raw_buffer_store_b128(o, rc, (row * D + c0 + cg * 4) * 4, 0, 0);
+            }
         }
     };
-    auto epilogue = [&](long long t, const f32x16& acc) {
+    auto epilogue = [&](long long t, const f32x16& acc) __attribute__((always_inline)) {
         epi_stage(t, acc);
         epi_store(t);
     };
 
     // ---- prologue: A(t_beg), indices and epilogue slabs of t_beg, indices of t_beg+1 ------
     {
+        if constexpr (BV > 0) {
+            for (int q = threadIdx.x; q < BV; q += 512) {
+                const int r = q / D;
+                bvl[q] = r < R ? p.V[r * p.v_rel_stride + (q - r * D)] : 0.f;
+            }
+        }
         dma_idx(t_beg);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         dma_A(t_beg, 0);
@@ -1096,7 +1179,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     }
     // s_waitcnt vmcnt(n): everything but the n youngest vector-memory ops of this wave has landed
     // (LDS-DMA, loads and stores count together, in issue order)
-    auto wait_newest = [&](int n) {
+    auto wait_newest = [&](int n) __attribute__((always_inline)) {
         if (n >= 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
         else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
@@ -1168,18 +1251,21 @@ _Pragma("unroll") \
                 const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
                 /* fragments of k-steps q and q+1 in alternating registers (no copies) */ \
                 f16x8 ah[2], al[2]; \
+                /* planes layout: k-step q's hi at float 32(q>>1) + 8(q&1) of the row, lo 16 floats on */ \
                 ah[0] = __builtin_bit_cast(f16x8, ld4(arow)); \
-                al[0] = __builtin_bit_cast(f16x8, ld4(arow + 128)); \
+                al[0] = __builtin_bit_cast(f16x8, ld4(arow + 16)); \
 _Pragma("unroll") \
                 for (int q = 0; q < ((V3_ABL & 32) ? 0 : D / 16); ++q) { \
                     const int cu = q & 1; \
                     if (q + 1 < D / 16) { \
-                        ah[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + 8 * (q + 1))); \
-                        al[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + 128 + 8 * (q + 1))); \
+                        const int qo = 32 * ((q + 1) >> 1) + 8 * ((q + 1) & 1); \
+                        ah[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + qo)); \
+                        al[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + qo + 16)); \
                     } \
+                    /* A lo in the units of A hi (split16_same), W lo in 2^-11 units */ \
                     acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], ah[cu], acc_hi, 0, 0, 0); \
-                    acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], al[cu], acc_lo, 0, 0, 0); \
                     acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(blo[q], ah[cu], acc_lo, 0, 0, 0); \
+                    acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(bhi[q], al[cu], acc_hi, 0, 0, 0); \
                     __builtin_amdgcn_sched_barrier(0); \
                 } \
                 /* unscale: row i (1/s_row of this buffer), columns c0+8j+4h+q (1/s_col) */ \
@@ -1437,11 +1523,6 @@ constexpr int D = 256, TK = 32, LDR = D + 4, TILE = TK * LDR;
 constexpr float S_INIT = 0x1p126f;                       // pow2_scale(0): "no data yet"
 }
 
-__device__ __forceinline__ void split16_same(float xs, _Float16& hi, _Float16& lo) {
-    hi = (_Float16)xs;
-    lo = (_Float16)(xs - (float)hi);
-}
-
 // SEG: the tail-side segmented reduction of the same layer (tail_seg_reduce_kernel) fused into the
 // dS = x^T do pass, so do is read from HBM once instead of twice:
 //   dP_r[t] = sum_{e: t_e = t} W[e][r] do_e      (row order, fmaf chain: = tail_seg_reduce)
@@ -1464,20 +1545,35 @@ struct TnSegP {
 };
 constexpr int TNSEG_CAP = 6;
 
-template <bool SEG>
+// PA: A arrives as planes rows (IDDGCN_PLANES_A, fixed scale 2^15): no A conversion; the A fragments
+// (8 consecutive rows of one column) are read straight from the row-major hi / lo planes with two
+// ds_read_b64_tr_b16 each.  A rows then use a 272-float pitch (row stride = 16 banks mod 64: the four rows
+// of a transposed read land on disjoint banks).
+typedef short v4s16 __attribute__((vector_size(8)));
+__device__ __forceinline__ f16x8 tr_frag16(const char* p0, const char* p1) {
+    typedef __attribute__((address_space(3))) v4s16* l4p;
+    const v4s16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)p0);
+    const v4s16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)p1);
+    return __builtin_shufflevector(__builtin_bit_cast(f16x4, a), __builtin_bit_cast(f16x4, b), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+template <bool SEG, bool PA = false>
 __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long long rows_per_block,
                                                             const float* __restrict__ A,
                                                             const float* __restrict__ B,
                                                             float* __restrict__ slab, TnSegP sp) {
     using namespace tn3;
+    static_assert(!(SEG && PA), "planes A: unfused TN only");
+    constexpr int LDRA = PA ? 272 : LDR;                 // A row pitch (floats)
+    constexpr int TILE_A = TK * LDRA;
+    constexpr int BUF = TILE_A + TILE;                   // one [A | B] buffer
     // SEG region per buffer: tails[32] | run-start mask (+pad)[32] | W[32][2] | P rows [CAP][2][D];
     // then part[8][32][2]
     constexpr int SEG_BUF = 32 + 32 + 64 + TNSEG_CAP * 2 * D;
     constexpr int SEG_F = SEG ? 2 * SEG_BUF + 8 * 32 * 2 : 0;
-    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * TILE + 2 * 8 + SEG_F];   // [buf][A|B][TK][LDR], sB[buf][8]
-    static_assert((2 * 2 * TILE + 2 * 8 + SEG_F) * 4 <= 160 * 1024, "LDS budget");
-    float* sBpub = lds + 2 * 2 * TILE;
-    float* segL = lds + 2 * 2 * TILE + 2 * 8;
+    __shared__ __attribute__((aligned(16))) float lds[2 * BUF + 2 * 8 + SEG_F];   // [buf][A|B][TK][pitch], sB[buf][8]
+    static_assert((2 * BUF + 2 * 8 + SEG_F) * 4 <= 160 * 1024, "LDS budget");
+    float* sBpub = lds + 2 * BUF;
+    float* segL = lds + 2 * BUF + 2 * 8;
     float* partL = segL + 2 * SEG_BUF;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1549,7 +1645,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
         const int* tl = reinterpret_cast<const int*>(base);
         const float* Wl = base + 64;
         const float* Pl = base + 128;
-        const float* Bf = lds + (b * 2 + 1) * TILE;
+        const float* Bf = lds + b * BUF + TILE_A;
         const long long row0 = r_beg + t * TK;
         const int nrows = (int)(r_end - row0 < TK ? r_end - row0 : TK);
         const unsigned mstart = (unsigned)__builtin_amdgcn_readfirstlane(tl[32]);
@@ -1601,17 +1697,17 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
     };
 
     auto stage = [&](long long t, int b) {
-        float* As = lds + (b * 2 + 0) * TILE;
-        float* Bs = lds + (b * 2 + 1) * TILE;
+        float* As = lds + b * BUF;
+        float* Bs = As + TILE_A;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int r = wave * 4 + j;
             const long long e = r_beg + t * TK + r;
             if (e < r_end) {
-                dma_row_1k(A + e * D, As + r * LDR, lane);
+                dma_row_1k(A + e * D, As + r * LDRA, lane);
                 dma_row_1k(B + e * D, Bs + r * LDR, lane);
-            } else {
-                st4(As + r * LDR + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+            } else {                                     // zero rows (zero planes for PA)
+                st4(As + r * LDRA + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
                 st4(Bs + r * LDR + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
             }
         }
@@ -1650,10 +1746,11 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
         *reinterpret_cast<f16x8*>(seg + 64 + 32 * h + 16) = lv[1];
     };
     auto convert = [&](int b) {
-        convert_block(lds + (b * 2 + 0) * TILE, sA, true);
-        convert_block(lds + (b * 2 + 1) * TILE, sBrun, false);
+        if constexpr (!PA) convert_block(lds + b * BUF, sA, true);
+        convert_block(lds + b * BUF + TILE_A, sBrun, false);
         if (lane == 0) sBpub[b * 8 + wave] = sBrun;
     };
+    if constexpr (PA) sA = PLANE_S;
 
     int tnext = -1;
     if (nt > 0) {
@@ -1687,12 +1784,23 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
                 curB[cj] = s;
             }
         }
-        const char* Aseg = reinterpret_cast<const char*>(lds + (b * 2 + 0) * TILE + i * LDR + 32 * wave);
-        const char* Bseg = reinterpret_cast<const char*>(lds + (b * 2 + 1) * TILE + i * LDR);
+        const char* Aseg = reinterpret_cast<const char*>(lds + b * BUF + i * LDRA + 32 * wave);
+        const char* Bseg = reinterpret_cast<const char*>(lds + b * BUF + TILE_A + i * LDR);
+        // PA: lane 4q+p of its 16-lane group addresses row 8h + q, columns 32w + 16((lane>>4)&1) + 4p (planes
+        // column block w: hi at 128w + 2(column - 32w), lo 64 B on)
+        const char* Atr = reinterpret_cast<const char*>(lds + b * BUF) + ((8 * h + ((lane >> 2) & 3)) * LDRA) * 4 +
+                          128 * wave + 32 * ((lane >> 4) & 1) + 8 * (lane & 3);
 #pragma unroll
         for (int s = 0; s < TK / 16; ++s) {
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(Aseg + 32 * s + 16 * h);
-            const f16x8 al = *reinterpret_cast<const f16x8*>(Aseg + 64 + 32 * s + 16 * h);
+            f16x8 ah, al;
+            if constexpr (PA) {
+                const char* r0 = Atr + (16 * s) * LDRA * 4;
+                ah = tr_frag16(r0, r0 + 4 * LDRA * 4);
+                al = tr_frag16(r0 + 64, r0 + 4 * LDRA * 4 + 64);
+            } else {
+                ah = *reinterpret_cast<const f16x8*>(Aseg + 32 * s + 16 * h);
+                al = *reinterpret_cast<const f16x8*>(Aseg + 64 + 32 * s + 16 * h);
+            }
 #pragma unroll
             for (int cj = 0; cj < 8; ++cj) {
                 const f16x8 bh = *reinterpret_cast<const f16x8*>(Bseg + 128 * cj + 32 * s + 16 * h);
@@ -2015,7 +2123,7 @@ __global__ __launch_bounds__(256) void combine_kernel(int M, const float* __rest
 // of are the ones already needed.  Per-edge indices/coefficients: one per lane, broadcast
 // with readlane.
 constexpr int RC_CH = 64;
-template <int R, bool BF = false>
+template <int R, bool BF = false, bool PL = false>
 __global__ __launch_bounds__(256) void run_combine256_kernel(int M, const float* __restrict__ Y,
                                                              const int* __restrict__ idx,
                                                              const float* __restrict__ coef,
@@ -2073,7 +2181,10 @@ __global__ __launch_bounds__(256) void run_combine256_kernel(int M, const float*
                 for (int r = 0; r < R; ++r) v += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cf[r]), j)) * pc[r];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
-                st4e<BF>(out, (e0 + j) * D + lane * 4, v);
+                if constexpr (PL)
+                    st_planes4(reinterpret_cast<char*>(out) + (e0 + j) * 1024, lane * 4, v);
+                else
+                    st4e<BF>(out, (e0 + j) * D + lane * 4, v);
             }
             yc = yn;
 #pragma unroll
@@ -2638,9 +2749,20 @@ struct V3Sel {
     int nv;                 // gathered V tables (template NV)
     bool aux, hc, rec;
     bool cw = false;        // broadcast V with R > 2 coefficients
+    bool pl = false;        // planes C (gathered forward) / planes sigma' operand (backward)
 };
 // Which v3 instantiation computes this call, or false (the DMA-v2 / register-staged kernels then run).
+bool v3_select_(const RowGemmP& p, V3Sel& sel);
 bool v3_select(const RowGemmP& p, V3Sel& sel) {
+    if (!v3_select_(p, sel)) return false;
+    sel.pl = (p.planes & (IDDGCN_PLANES_C | IDDGCN_PLANES_AUX)) != 0;
+    if (!sel.pl) return true;
+    // the planes forms: C planes on the R <= 2 gathered forward, sigma' planes on the plain backward
+    if ((p.planes & IDDGCN_PLANES_C) && !(sel.nv >= 1 && sel.nv <= 2 && !sel.rec && !sel.aux)) return false;
+    if ((p.planes & IDDGCN_PLANES_AUX) && !(sel.aux && sel.nv == 0 && !sel.hc)) return false;
+    return true;
+}
+bool v3_select_(const RowGemmP& p, V3Sel& sel) {
     if (!(g_rowgemm_path == 0 || g_gemm_split)) return false;
     const bool gatherV = p.R > 0 && p.v_row_stride != 0;
     const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
@@ -2662,6 +2784,39 @@ bool v3_select(const RowGemmP& p, V3Sel& sel) {
     }
     sel = {0, dsig, p.R > 0, false, p.R > 2};
     return true;
+}
+
+// The device-side copy of one iddgcn_rowgemm_t (tiles_per_block is set at launch).
+RowGemmP to_p(const iddgcn_rowgemm_t& a) {
+    RowGemmP p;
+    p.M = a.M; p.A = a.A; p.a_idx = a.a_idx; p.B = a.B; p.b_trans = a.b_trans;
+    p.C = a.C; p.accumulate = a.accumulate; p.R = a.R; p.coef = a.coef; p.coef_idx = a.coef_idx;
+    p.V = a.V; p.v_idx = a.v_idx; p.v_rel_stride = a.v_rel_stride; p.v_row_stride = a.v_row_stride;
+    p.act = a.act; p.aux = a.aux; p.v_runs_max = a.v_runs_max; p.planes = a.planes;
+    p.tiles_per_block = 1;
+    return p;
+}
+// Argument check shared by the f32 row-GEMM entries (0 = fine).  Planes operands (IDDGCN_PLANES_*) need
+// D = 256, the split-fp16 mode and the v3 kernel; a planes C holds sigmoid outputs only.
+int check_rowgemm(const iddgcn_rowgemm_t& a) {
+    if (!dim_ok(a.D)) return IDDGCN_E_BAD_DIM;
+    if (a.R < 0 || a.R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (a.M == 0) return 0;
+    if (a.M < 0 || !a.A || !a.B || !a.C) return IDDGCN_E_BAD_ARG;
+    if (a.R > 0 && (!a.coef || !a.V)) return IDDGCN_E_BAD_ARG;
+    if (a.act == IDDGCN_ACT_DSIGMOID && !a.aux) return IDDGCN_E_BAD_ARG;
+    if (a.act == IDDGCN_ACT_DSIGMOID_COMBINE && (a.R < 1 || a.R + 1 > MAX_R || a.v_row_stride == 0))
+        return IDDGCN_E_BAD_ARG;
+    if (a.act < IDDGCN_ACT_NONE || a.act > IDDGCN_ACT_DSIGMOID_COMBINE) return IDDGCN_E_BAD_ARG;
+    if (a.planes) {
+        if (a.planes & ~(IDDGCN_PLANES_A | IDDGCN_PLANES_C | IDDGCN_PLANES_AUX)) return IDDGCN_E_BAD_ARG;
+        if (a.D != 256 || !g_gemm_split || a.a_idx) return IDDGCN_E_BAD_ARG;
+        if ((a.planes & IDDGCN_PLANES_C) && (a.act != IDDGCN_ACT_SIGMOID || a.accumulate)) return IDDGCN_E_BAD_ARG;
+        if ((a.planes & IDDGCN_PLANES_AUX) && a.act != IDDGCN_ACT_DSIGMOID) return IDDGCN_E_BAD_ARG;
+        V3Sel sel;
+        if (!v3_select(to_p(a), sel)) return IDDGCN_E_BAD_ARG;
+    }
+    return 0;
 }
 
 // One launch of up to ROWGEMM_BATCH v3 GEMMs of the same variant (blockIdx.y = entry).  The persistent
@@ -2703,7 +2858,11 @@ void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel, bool b
         if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, true, false, true>), g, blk, 0, st, pb); \
         else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, false, false, true>), g, blk, 0, st, pb);   \
     }
-    if (sel.rec) {
+    if (sel.pl) {           // check_rowgemm: split mode
+        if (sel.nv == 1) hipLaunchKernelGGL((rowgemm256_v3_kernel<1, false, true, true, false, false, false, true>), g, blk, 0, st, pb);
+        else if (sel.nv == 2) hipLaunchKernelGGL((rowgemm256_v3_kernel<2, false, true, true, false, false, false, true>), g, blk, 0, st, pb);
+        else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, true, false, true, false, false, false, true>), g, blk, 0, st, pb);
+    } else if (sel.rec) {
         if (sel.nv == 2) V3L(2, false, true, true)
         else V3L(3, false, true, true)
     } else if (sel.nv == 1) V3L(1, false, true, false)
@@ -2719,6 +2878,35 @@ void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel, bool b
     else V3L(0, false, false, false)
 #undef V3L
 #undef V3W
+}
+
+// the run combine (D = 256) writing bf16 rows (BF) or planes rows (PL)
+template <bool BF, bool PL>
+int run_combine_out(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,
+                    const float* V, long long v_rel_stride, void* out) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (R < 0 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (M < 0 || !Y || !idx || !out || (R > 0 && (!coef || !V))) return IDDGCN_E_BAD_ARG;
+    if (M == 0) return 0;
+    const long long nchunk = ((long long)M + RC_CH - 1) / RC_CH;
+    long long nb = (nchunk + 3) / 4;
+    if (nb > 2048) nb = 2048;
+    hipStream_t st = (hipStream_t)stream;
+    float* o = (float*)out;
+#define RCB(RR) hipLaunchKernelGGL((run_combine256_kernel<RR, BF, PL>), dim3((unsigned)nb), dim3(256), 0, st, M, Y, idx, coef, V, v_rel_stride, o)
+    switch (R) {
+        case 0: RCB(0); break;
+        case 1: RCB(1); break;
+        case 2: RCB(2); break;
+        case 3: RCB(3); break;
+        case 4: RCB(4); break;
+        case 5: RCB(5); break;
+        case 6: RCB(6); break;
+        case 7: RCB(7); break;
+        default: RCB(8); break;
+    }
+#undef RCB
+    return launch_status();
 }
 
 inline unsigned grid_for(long long rows, int lpr) {
@@ -2787,21 +2975,9 @@ int iddgcn_sddmm_csr_f32(void* stream, int n_seg, int n_rows, int d, const int* 
 
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     if (!a) return IDDGCN_E_BAD_ARG;
-    if (!dim_ok(a->D)) return IDDGCN_E_BAD_DIM;
-    if (a->R < 0 || a->R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (const int rc = check_rowgemm(*a)) return rc;
     if (a->M == 0) return 0;                 // nothing to do (an empty C may have a null pointer)
-    if (a->M < 0 || !a->A || !a->B || !a->C) return IDDGCN_E_BAD_ARG;
-    if (a->R > 0 && (!a->coef || !a->V)) return IDDGCN_E_BAD_ARG;
-    if (a->act == IDDGCN_ACT_DSIGMOID && !a->aux) return IDDGCN_E_BAD_ARG;
-    if (a->act == IDDGCN_ACT_DSIGMOID_COMBINE && (a->R < 1 || a->R + 1 > MAX_R || a->v_row_stride == 0))
-        return IDDGCN_E_BAD_ARG;
-    if (a->act < IDDGCN_ACT_NONE || a->act > IDDGCN_ACT_DSIGMOID_COMBINE) return IDDGCN_E_BAD_ARG;
-    if (a->M == 0) return 0;
-    RowGemmP p;
-    p.M = a->M; p.A = a->A; p.a_idx = a->a_idx; p.B = a->B; p.b_trans = a->b_trans;
-    p.C = a->C; p.accumulate = a->accumulate; p.R = a->R; p.coef = a->coef; p.coef_idx = a->coef_idx;
-    p.V = a->V; p.v_idx = a->v_idx; p.v_rel_stride = a->v_rel_stride; p.v_row_stride = a->v_row_stride;
-    p.act = a->act; p.aux = a->aux; p.v_runs_max = a->v_runs_max;
+    RowGemmP p = to_p(*a);
     hipStream_t st = (hipStream_t)stream;
 #define RGEMM(DD, MAXB)                                                                         \
     {                                                                                           \
@@ -2854,14 +3030,11 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
 
 int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* a) {
     if (!a || !dim_ok(a->D)) return -1;
-    RowGemmP p;
-    p.M = a->M; p.A = a->A; p.a_idx = a->a_idx; p.B = a->B; p.b_trans = a->b_trans;
-    p.C = a->C; p.accumulate = a->accumulate; p.R = a->R; p.coef = a->coef; p.coef_idx = a->coef_idx;
-    p.V = a->V; p.v_idx = a->v_idx; p.v_rel_stride = a->v_rel_stride; p.v_row_stride = a->v_row_stride;
-    p.act = a->act; p.aux = a->aux; p.v_runs_max = a->v_runs_max;
+    const RowGemmP p = to_p(*a);
     V3Sel sel;
     if (a->D == 256 && v3_select(p, sel))
-        return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.rec ? 4 : 0) + (sel.cw ? 8 : 0);
+        return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.rec ? 4 : 0) + (sel.cw ? 8 : 0) +
+               (sel.pl ? 1000 : 0);
     const bool gatherV = p.R > 0 && p.v_row_stride != 0;
     const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
     const int epi_rows = gatherV ? p.R : (dsig ? 1 : 0);
@@ -2877,14 +3050,7 @@ int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
     bool one_launch = a[0].D != 256;
     for (int k = 0; k < n; ++k) {
         if (!dim_ok(a[k].D) || a[k].D != a[0].D) return IDDGCN_E_BAD_DIM;
-        if (a[k].R < 0 || a[k].R > MAX_R) return IDDGCN_E_BAD_REL;
-        if (a[k].M == 0) continue;
-        if (a[k].M < 0 || !a[k].A || !a[k].B || !a[k].C) return IDDGCN_E_BAD_ARG;
-        if (a[k].R > 0 && (!a[k].coef || !a[k].V)) return IDDGCN_E_BAD_ARG;
-        if (a[k].act == IDDGCN_ACT_DSIGMOID && !a[k].aux) return IDDGCN_E_BAD_ARG;
-        if (a[k].act == IDDGCN_ACT_DSIGMOID_COMBINE && (a[k].R < 1 || a[k].R + 1 > MAX_R || a[k].v_row_stride == 0))
-            return IDDGCN_E_BAD_ARG;
-        if (a[k].act < IDDGCN_ACT_NONE || a[k].act > IDDGCN_ACT_DSIGMOID_COMBINE) return IDDGCN_E_BAD_ARG;
+        if (const int rc = check_rowgemm(a[k])) return rc;
     }
     if (!one_launch) {          // D = 256: one v3 launch when every entry maps to the same variant
         RowGemmBatch pb;
@@ -2894,14 +3060,11 @@ int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
         for (int k = 0; k < n && same; ++k) {
             if (a[k].M == 0) continue;
             RowGemmP& p = pb.p[m];
-            p.M = a[k].M; p.A = a[k].A; p.a_idx = a[k].a_idx; p.B = a[k].B; p.b_trans = a[k].b_trans;
-            p.C = a[k].C; p.accumulate = a[k].accumulate; p.R = a[k].R; p.coef = a[k].coef;
-            p.coef_idx = a[k].coef_idx; p.V = a[k].V; p.v_idx = a[k].v_idx; p.v_rel_stride = a[k].v_rel_stride;
-            p.v_row_stride = a[k].v_row_stride; p.act = a[k].act; p.aux = a[k].aux; p.v_runs_max = a[k].v_runs_max;
+            p = to_p(a[k]);
             if (!v3_select(p, sel)) same = false;
             else if (m == 0) sel0 = sel;
             else same = sel.nv == sel0.nv && sel.aux == sel0.aux && sel.hc == sel0.hc && sel.rec == sel0.rec &&
-                        sel.cw == sel0.cw;
+                        sel.cw == sel0.cw && sel.pl == sel0.pl;
             ++m;
         }
         if (same) {
@@ -2921,10 +3084,7 @@ int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
     const long long maxb = d == 128 ? 1024 : 2048;
     for (int k = 0; k < n; ++k) {
         RowGemmP& p = pb.p[k];
-        p.M = a[k].M; p.A = a[k].A; p.a_idx = a[k].a_idx; p.B = a[k].B; p.b_trans = a[k].b_trans;
-        p.C = a[k].C; p.accumulate = a[k].accumulate; p.R = a[k].R; p.coef = a[k].coef; p.coef_idx = a[k].coef_idx;
-        p.V = a[k].V; p.v_idx = a[k].v_idx; p.v_rel_stride = a[k].v_rel_stride; p.v_row_stride = a[k].v_row_stride;
-        p.act = a[k].act; p.aux = a[k].aux; p.v_runs_max = a[k].v_runs_max;
+        p = to_p(a[k]);
         const long long nt = ((long long)p.M + tr - 1) / tr;
         long long nb = nt < maxb ? nt : maxb;
         p.tiles_per_block = nb > 0 ? (int)((nt + nb - 1) / nb) : 1;
@@ -2970,6 +3130,24 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
         default: TNK(256); break;
     }
 #undef TNK
+    int rc = launch_status();
+    if (rc) return rc;
+    const long long n = (long long)d * d;
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_blocks, n, slab, C,
+                       accumulate, 1.0f);
+    return launch_status();
+}
+
+int iddgcn_gemm_tn_planes_f32(void* stream, long long M, int d, const void* A, const float* B, float* slab,
+                              int n_blocks, float* C, int accumulate) {
+    if (d != 256 || !g_gemm_split) return IDDGCN_E_BAD_DIM;
+    if (M < 0 || n_blocks < 1 || !A || !B || !slab || !C) return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    long long rpb = (M + n_blocks - 1) / n_blocks;
+    rpb = ((rpb + 31) / 32) * 32;
+    if (rpb < 32) rpb = 32;
+    hipLaunchKernelGGL((gemm_tn256_x3_kernel<false, true>), dim3(n_blocks), dim3(512), 0, st, M, rpb,
+                       (const float*)A, B, slab, TnSegP{});
     int rc = launch_status();
     if (rc) return rc;
     const long long n = (long long)d * d;
@@ -3286,11 +3464,9 @@ int iddgcn_rowgemm_bf16(void* stream, const iddgcn_rowgemm_t* a) {
     if (a->act != IDDGCN_ACT_NONE && a->act != IDDGCN_ACT_SIGMOID && !dsig) return IDDGCN_E_BAD_ARG;
     if (dsig && (!a->aux || a->R > 0)) return IDDGCN_E_BAD_ARG;
     if (a->R > 0 && (!gatherV || a->v_row_stride != 256 || !a->coef || !a->V)) return IDDGCN_E_BAD_ARG;
-    RowGemmP p;
-    p.M = a->M; p.A = a->A; p.a_idx = a->a_idx; p.B = a->B; p.b_trans = a->b_trans;
-    p.C = a->C; p.accumulate = 0; p.R = a->R; p.coef = a->coef; p.coef_idx = a->coef_idx;
-    p.V = a->V; p.v_idx = a->v_idx; p.v_rel_stride = a->v_rel_stride; p.v_row_stride = a->v_row_stride;
-    p.act = a->act; p.aux = a->aux; p.v_runs_max = a->v_runs_max;
+    if (a->planes) return IDDGCN_E_BAD_ARG;
+    RowGemmP p = to_p(*a);
+    p.accumulate = 0;
     V3Sel sel;
     sel.nv = a->R == 0 ? 0 : a->R == 1 ? 1 : a->R == 2 ? 2 : a->R <= 4 ? 4 : 8;
     sel.aux = dsig;
@@ -3322,29 +3498,12 @@ int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const v
 
 int iddgcn_combine_bf16(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,
                         const float* V, long long v_rel_stride, void* out) {
-    if (d != 256) return IDDGCN_E_BAD_DIM;
-    if (R < 0 || R > MAX_R) return IDDGCN_E_BAD_REL;
-    if (M < 0 || !Y || !idx || !out || (R > 0 && (!coef || !V))) return IDDGCN_E_BAD_ARG;
-    if (M == 0) return 0;
-    const long long nchunk = ((long long)M + RC_CH - 1) / RC_CH;
-    long long nb = (nchunk + 3) / 4;
-    if (nb > 2048) nb = 2048;
-    hipStream_t st = (hipStream_t)stream;
-    float* o = (float*)out;
-#define RCB(RR) hipLaunchKernelGGL((run_combine256_kernel<RR, true>), dim3((unsigned)nb), dim3(256), 0, st, M, Y, idx, coef, V, v_rel_stride, o)
-    switch (R) {
-        case 0: RCB(0); break;
-        case 1: RCB(1); break;
-        case 2: RCB(2); break;
-        case 3: RCB(3); break;
-        case 4: RCB(4); break;
-        case 5: RCB(5); break;
-        case 6: RCB(6); break;
-        case 7: RCB(7); break;
-        default: RCB(8); break;
-    }
-#undef RCB
-    return launch_status();
+    return run_combine_out<true, false>(stream, M, d, R, Y, idx, coef, V, v_rel_stride, out);
+}
+
+int iddgcn_combine_planes_f32(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,
+                              const float* V, long long v_rel_stride, void* out) {
+    return run_combine_out<false, true>(stream, M, d, R, Y, idx, coef, V, v_rel_stride, out);
 }
 
 int iddgcn_distmult_bce_bf16(void* stream, long long T, int d, int R, const float* Xh, const int* h_idx,

@@ -217,7 +217,7 @@ class Engine:
     """
 
     def __init__(self, num_entities, num_relations, dim, device=None, gemm="split", recompute_x1=False,
-                 fuse_tail_seg=False, features="f32"):
+                 fuse_tail_seg=False, features="f32", planes=True):
         if dim not in (32, 64, 128, 256):
             raise L.IddgcnError("embedding dim must be one of 32, 64, 128, 256")
         if features not in ("f32", "bf16"):
@@ -241,12 +241,23 @@ class Engine:
         # less HBM traffic per step at config 3, but the per-tile scan is serial with the TN pipeline:
         # 3.9 ms vs 2.0 + 0.9 ms unfused, so off by default)
         self.fuse_tail_seg = fuse_tail_seg
+        # pre-split tail tables x^1, x^2 (include/iddgcn.h IDDGCN_PLANES_*): their producers (layer-1
+        # combine, layer-2 forward GEMM) write [hi | lo] fp16 rows once, so the forward GEMMs of layers 2-3,
+        # the dS TN GEMMs and the sigma' backward skip their per-tile conversion (see use_planes)
+        self.planes = planes
         self.device = torch.device("cuda") if device is None else torch.device(device)
         if self.device.type != "cuda":
             raise L.IddgcnError("IDDGCN engine runs on the GPU only (no CPU fallback)")
         L.lib()  # fail loudly now if the HIP library is missing
         self._ws = {}
         self.probe = None      # {name: [(start_event, end_event), ...]} when timing kernels
+
+    @property
+    def use_planes(self):
+        """x^1, x^2 are stored pre-split: split GEMM mode at D = 256 with fp32 features, R <= 2 (the
+        gathered forward's planes form), not with the fused tail segmented reduction."""
+        return (self.planes and self.gemm == "split" and self.D == 256 and self.features == "f32" and self.R <= 2
+                and not self.fuse_tail_seg)
 
     @contextlib.contextmanager
     def _precision(self):
@@ -314,7 +325,8 @@ class Engine:
         ops.alpha_fwd(E, P["Wa1"], P["ba1"], ws.Ssm[0], ws.W[0])
         ops.gather_rows(ws.W[0], ed.h, ws.Wedge[0])
         ops.combine(ws.ES1, ws.W[0], ws.P[0], ws.X[0])
-        ops.combine(ws.ES1, ws.Wedge[0], ws.P[0], ws.xt[0], y_idx=ed.t, v_idx=ed.t)
+        pl = self.use_planes
+        ops.combine(ws.ES1, ws.Wedge[0], ws.P[0], ws.xt[0], y_idx=ed.t, v_idx=ed.t, planes_out=pl)
         # layers 2, 3
         for l in (1, 2):
             S = P[f"S{l + 1}"]
@@ -324,7 +336,8 @@ class Engine:
                         act=L.ACT_SIGMOID)
             with self._mark("tail_fwd_gemm"):
                 ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
-                            v_rel_stride=N * D, act=L.ACT_SIGMOID)
+                            v_rel_stride=N * D, act=L.ACT_SIGMOID,
+                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0)
         # DistMult (+ BCE and backward seed when training)
         if train:
             # one pass over head segments: p / loss / drel partials, the tail seed do^3 (per edge)
@@ -354,6 +367,7 @@ class Engine:
         dOn, dOn_next = ws.dOn_a, ws.dOn_b      # head seed dO^3, written by distmult_bce_heads
         if self.node_shard is not None:
             ws.dAE.zero_()                      # rows other ranks own stay 0 in the dE SpMM below
+        pl = self.use_planes                    # x^1, x^2 are planes tables (forward)
         for l in (2, 1, 0):                     # layer index l -> reference layer l+1
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
             do = ws.xt[l]                       # do^{l+1}, written over x^{l+1}
@@ -370,7 +384,7 @@ class Engine:
                         ops.gemm_tn_seg(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, seg[0], ed.t, ws.Wedge[l], Pl,
                                         ws.dP, ws.dWedge, seg[1])
                     else:
-                        ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab)
+                        ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl)
                 rec = l == 1 and self._recompute_ok(ed)
                 with self._mark("tail_bwd_rec_gemm" if rec else "tail_bwd_gemm"):
                     if rec:
@@ -379,7 +393,8 @@ class Engine:
                                     coef=ws.Wedge[0], V=ws.EP1, v_idx=ed.t, v_rel_stride=N * D,
                                     v_runs_max=ed.tail_runs32)
                     else:
-                        ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1])
+                        ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
+                                    planes=L.PLANES_AUX if pl else 0)
             # head side (node level)
             ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
                               dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)
@@ -471,7 +486,9 @@ class Engine:
         ws = self.workspace(ed.T, False)
         inv = ed.inv if rows is None else ed.inv[torch.as_tensor(rows, device=ed.inv.device)]
         heads = ed.h.long()[inv]
-        return [(ws.X[l][heads], ws.xt[l][inv].float()) for l in range(NUM_LAYERS)]
+        pl = self.use_planes
+        return [(ws.X[l][heads], ops.planes_to_f32(ws.xt[l][inv]) if pl and l < 2 else ws.xt[l][inv].float())
+                for l in range(NUM_LAYERS)]
 
     def loss_and_grads(self, params, grads, adj, ed, t_global=None, logits=False):
         """Forward + backward without the optimizer step: (loss sum, p) or, with ``logits=True``,

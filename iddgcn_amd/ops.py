@@ -109,10 +109,13 @@ def rowgemm_batched(calls):
 
 
 def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, coef_idx=None, V=None,
-                  v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None, v_runs_max=0):
+                  v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None, v_runs_max=0,
+                  planes=0):
     """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32).  act=ACT_DSIGMOID_COMBINE
     multiplies by x(1-x) with x = sigmoid(V_0[v_idx] + sum_r coef_r V_{r+1}[v_idx]) (V: R+1 tables);
-    v_runs_max bounds the runs of equal v_idx per aligned 32-row block (0 = unknown)."""
+    v_runs_max bounds the runs of equal v_idx per aligned 32-row block (0 = unknown).  planes: L.PLANES_*
+    flags, which of A / C / aux are pre-split planes tables (fp32-shaped tensors holding [hi | lo] fp16
+    rows; D = 256, split GEMM mode)."""
     D = B.shape[0]
     M = C.shape[0] if M is None else M
     R = 0 if coef is None else coef.shape[-1]
@@ -142,15 +145,16 @@ def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=
         accumulate=int(accumulate), R=R, coef=_ptr(coef), coef_idx=_ptr(coef_idx), V=_ptr(V),
         v_idx=_ptr(v_idx), v_rel_stride=int(v_rel_stride),
         v_row_stride=int(D if v_row_stride is None else v_row_stride), act=int(act), aux=_ptr(aux),
-        v_runs_max=int(v_runs_max))
+        v_runs_max=int(v_runs_max), planes=int(planes))
 
 
 def tn_blocks(M, D):
     return int(L.lib().iddgcn_gemm_tn_blocks(int(M), int(D)))
 
 
-def gemm_tn(A, B, C, slab, accumulate=False):
-    """C (+)= A^T B; bf16 A and B (the bf16-feature mode) select iddgcn_gemm_tn_bf16."""
+def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False):
+    """C (+)= A^T B; bf16 A and B (the bf16-feature mode) select iddgcn_gemm_tn_bf16; a_planes: A is a
+    pre-split planes table (iddgcn_gemm_tn_planes_f32, D = 256, split GEMM mode)."""
     M, D = A.shape
     et = _BF16 if A.dtype == _BF16 else _F32
     _req(A, et, (M, D), "A")
@@ -159,7 +163,12 @@ def gemm_tn(A, B, C, slab, accumulate=False):
     nb = tn_blocks(M, D)
     if slab.numel() < nb * D * D:
         raise L.IddgcnError("gemm_tn slab too small")
-    fn = L.lib().iddgcn_gemm_tn_bf16 if et == _BF16 else L.lib().iddgcn_gemm_tn_f32
+    if a_planes:
+        if et != _F32:
+            raise L.IddgcnError("gemm_tn: planes A takes an fp32-shaped table")
+        fn = L.lib().iddgcn_gemm_tn_planes_f32
+    else:
+        fn = L.lib().iddgcn_gemm_tn_bf16 if et == _BF16 else L.lib().iddgcn_gemm_tn_f32
     L.check(fn(_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C), int(accumulate)), "gemm_tn")
 
 
@@ -223,19 +232,22 @@ def alpha_fwd(X, Wa, ba, S_out, W_out, x_idx=None, M=None):
                                          _ptr(S_out), _ptr(W_out)), "alpha_fwd")
 
 
-def combine(Y, coef, V, out, *, y_idx=None, coef_idx=None, v_idx=None, v_rel_stride=None):
+def combine(Y, coef, V, out, *, y_idx=None, coef_idx=None, v_idx=None, v_rel_stride=None, planes_out=False):
+    """out = sigmoid(Y[y_idx] + sum_r coef[coef_idx, r] V_r[v_idx]) (iddgcn_combine_f32).  A bf16 out (the
+    bf16-feature mode) or planes_out (out a pre-split planes table, D = 256) take the run form:
+    y_idx and v_idx the same array, per-row coefficients."""
     M, D = out.shape
     R = coef.shape[-1]
-    if out.dtype == _BF16:      # bf16-feature mode: the run form (y_idx == v_idx, per-row coefficients)
+    if out.dtype == _BF16 or planes_out:
         if y_idx is None or v_idx is not y_idx or coef_idx is not None:
-            raise L.IddgcnError("combine into bf16: y_idx and v_idx must be the same array, no coef_idx")
-        _req(out, _BF16, (M, D), "out")
+            raise L.IddgcnError("combine into bf16 / planes: y_idx and v_idx must be the same array, no coef_idx")
+        _req(out, _BF16 if out.dtype == _BF16 else _F32, (M, D), "out")
         _req(Y, _F32, None, "Y")
         _req(coef, _F32, (M, R), "coef")
         _idx_ok(y_idx, M, Y.shape[0], "y_idx")
         vrs = V.shape[1] * D if v_rel_stride is None else v_rel_stride
-        L.check(L.lib().iddgcn_combine_bf16(_stream(), M, D, R, _ptr(Y), _ptr(y_idx), _ptr(coef), _ptr(V), int(vrs),
-                                            _ptr(out)), "combine_bf16")
+        fn = L.lib().iddgcn_combine_bf16 if out.dtype == _BF16 else L.lib().iddgcn_combine_planes_f32
+        L.check(fn(_stream(), M, D, R, _ptr(Y), _ptr(y_idx), _ptr(coef), _ptr(V), int(vrs), _ptr(out)), "combine_run")
         return
     _req(Y, _F32, None, "Y")
     _req(coef, _F32, None, "coef")
@@ -569,3 +581,22 @@ def negative_samples(triples, num_entities, seed):
     L.check(lib.iddgcn_assemble_negatives(_stream(), M, _ptr(triples), _ptr(cond), _ptr(ent), _ptr(out)),
             "assemble_negatives")
     return out
+
+
+PLANE_INV = 2.0 ** -15
+
+
+def planes_to_f32(t):
+    """Decode a pre-split planes table (include/iddgcn.h, IDDGCN_PLANES_*): rows of D = 256 in an
+    fp32-shaped (rows, 256) tensor, 8 column blocks of [hi f16[32] | lo f16[32]], x = (hi + lo) * 2^-15."""
+    h = t.contiguous().view(torch.float16).view(t.shape[0], t.shape[1] // 32, 2, 32)
+    return ((h[:, :, 0].float() + h[:, :, 1].float()) * PLANE_INV).reshape(t.shape[0], t.shape[1])
+
+
+def f32_to_planes(x):
+    """The planes encoding of values in [0, 1] (round-to-nearest-even fp16 casts), as the producers write it."""
+    xs = x.float() * 2.0 ** 15
+    hi = xs.half()
+    lo = (xs - hi.float()).half()
+    rows = x.shape[0]
+    return torch.stack([hi.view(rows, -1, 32), lo.view(rows, -1, 32)], 2).reshape(rows, -1).contiguous().view(torch.float32)

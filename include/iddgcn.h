@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 3
+#define IDDGCN_ABI_VERSION 4
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -41,6 +41,17 @@ extern "C" {
  * aligned 32-row block of v_idx holds more runs of equal values than that; the D = 256 kernel
  * needs <= 8 (tail-sorted edges), any other input takes the generic kernel. */
 #define IDDGCN_ACT_DSIGMOID_COMBINE 3
+
+/* Pre-split edge tables ("planes", ABI 4; D = 256, split-fp16 GEMM mode only).  A row of values in
+ * [0, 1] (sigmoid outputs) stored as 8 column blocks of 128 B, block b = [hi f16 of columns 32b..32b+31 |
+ * lo f16 of the same columns] (1 KiB, the bytes of an fp32 row; block b lies where fp32 columns
+ * 32b..32b+31 lie, so the backward may write fp32 results over its planes sigma' operand), with
+ * x * 2^15 = hi + lo, hi = fp16(x * 2^15), lo = fp16(x * 2^15 - hi): 22 significant bits, absolute error
+ * <= 2^-24.  The producer splits once; GEMMs reading the table skip their per-tile conversion.
+ * Flags of iddgcn_rowgemm_t.planes: */
+#define IDDGCN_PLANES_A    1      /* A rows are planes rows */
+#define IDDGCN_PLANES_C    2      /* C is written as planes rows (act SIGMOID, no accumulate) */
+#define IDDGCN_PLANES_AUX  4      /* the sigma' operand aux is planes rows (act DSIGMOID) */
 
 int iddgcn_abi_version(void);
 
@@ -84,12 +95,14 @@ typedef struct {
     int act; const float* aux;
     int v_runs_max;       /* bound on runs of equal v_idx per aligned 32-row block, 0 = unknown (the
                              D = 256 x^1 recompute, IDDGCN_ACT_DSIGMOID_COMBINE, needs it) */
+    int planes;           /* IDDGCN_PLANES_* flags (ABI 4; 0 = every table fp32).  Nonzero needs D = 256,
+                             the split-fp16 mode and no a_idx; invalid combinations return IDDGCN_E_BAD_ARG */
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 
 /* Which kernel iddgcn_rowgemm_f32 would run for these arguments (a test / benchmark hook; nothing is
  * launched): 300 + 10*NV + aux + 2*coef + 4*recompute + 8*(broadcast V with R > 2 coefficients)
- * for the D = 256 v3 pipeline (NV = gathered V
+ * + 1000 for the planes form (C or aux planes) for the D = 256 v3 pipeline (NV = gathered V
  * tables: 1, 2, or capacity 4 / 8 for R <= 8, whose LDS slabs keep 7 distinct V rows per 32-row tile
  * and read further ones from L2), 200 for the v2 LDS-DMA row GEMM, 100 for the register-staged kernel
  * (any D, any V order), -1 for an invalid D. */
@@ -120,6 +133,10 @@ int iddgcn_set_gemm_precision(int mode);
 int iddgcn_gemm_tn_blocks(long long M, int d);
 int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const float* B,
                        float* slab, int n_blocks, float* C, int accumulate);
+/* iddgcn_gemm_tn_f32 with A a planes table (IDDGCN_PLANES_A; D = 256, split-fp16 mode): dS = x^T do
+ * with x^{l} pre-split by its producer (IDDGCN.py:62-63 autodiff). */
+int iddgcn_gemm_tn_planes_f32(void* stream, long long M, int d, const void* A, const float* B, float* slab,
+                              int n_blocks, float* C, int accumulate);
 
 /* dS = A^T B (as iddgcn_gemm_tn_f32, split-fp16 mode, D = 256) fused with the tail-side segmented
  * reduction of the same layer (iddgcn_tail_seg_reduce_f32 without dsum), reading B (= do) once:
@@ -153,6 +170,10 @@ int iddgcn_combine_f32(void* stream, int M, int d, int R,
                        const float* Y, const int* y_idx,
                        const float* coef, const int* coef_idx,
                        const float* V, const int* v_idx, long long v_rel_stride, float* out);
+/* The run form (y_idx == v_idx = idx, coefficients per row, D = 256) writing a planes table (the layer-1
+ * tail output x^1, IDDGCN.py:62-79, pre-split for the layer-2 GEMMs). */
+int iddgcn_combine_planes_f32(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,
+                              const float* V, long long v_rel_stride, void* out);
 
 /* DistMult decoder (IDDGCN.py:103-109) fused with Keras BCE (IDDGCN.py:161-168)
  * and the seed of the backward.  For each scored edge e:
