@@ -20,10 +20,10 @@ import sys
 import pandas as pd
 
 SYMBOLS = {
-    "split": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, true, false, false, false>",
-              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, false, false>",
-              "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, true, true, false, false>",
-              "tail_dS_tn": "gemm_tn256_x3_kernel<false>"},
+    "split": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, true, false, false, false",
+              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, false, false",
+              "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, true, true, false, false",
+              "tail_dS_tn": "gemm_tn256_x3_kernel<false"},
     "exact": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, false, false, false, false>",
               "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, false, false, false, false>",
               "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, false, true, false, false>",
