@@ -1518,6 +1518,9 @@ __global__ __launch_bounds__(512) void gemm_tn256_dma_kernel(long long M, long l
 // hi*hi + hi*lo + lo*hi with lo = fp16(x*s - hi) (same units; a lo below the fp16 normal range
 // only loses bits below 2^-38 of the block max).
 // ---------------------------------------------------------------------------
+#ifndef TN_ABL
+#define TN_ABL 0            // experiment builds only: 1 skip the B conversion, 2 skip the MFMAs, 4 skip the tile DMA
+#endif
 namespace tn3 {
 constexpr int D = 256, TK = 32, LDR = D + 4, TILE = TK * LDR;
 constexpr float S_INIT = 0x1p126f;                       // pow2_scale(0): "no data yet"
@@ -1697,6 +1700,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
     };
 
     auto stage = [&](long long t, int b) {
+        if (TN_ABL & 4) return;
         float* As = lds + b * BUF;
         float* Bs = As + TILE_A;
 #pragma unroll
@@ -1746,6 +1750,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
         *reinterpret_cast<f16x8*>(seg + 64 + 32 * h + 16) = lv[1];
     };
     auto convert = [&](int b) {
+        if (TN_ABL & 1) return;
         if constexpr (!PA) convert_block(lds + b * BUF, sA, true);
         convert_block(lds + b * BUF + TILE_A, sBrun, false);
         if (lane == 0) sBpub[b * 8 + wave] = sBrun;
@@ -1791,7 +1796,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long lo
         const char* Atr = reinterpret_cast<const char*>(lds + b * BUF) + ((8 * h + ((lane >> 2) & 3)) * LDRA) * 4 +
                           128 * wave + 32 * ((lane >> 4) & 1) + 8 * (lane & 3);
 #pragma unroll
-        for (int s = 0; s < TK / 16; ++s) {
+        for (int s = 0; s < ((TN_ABL & 2) ? 0 : TK / 16); ++s) {
             f16x8 ah, al;
             if constexpr (PA) {
                 const char* r0 = Atr + (16 * s) * LDRA * 4;

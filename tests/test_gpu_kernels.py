@@ -843,3 +843,46 @@ def test_rowgemm256_batched_one_launch_bitwise(gm, cuda):
             ops.rowgemm_batched([(A, B, C, dict(kw, M=C.shape[0])) for (A, B, _), C in zip(calls, outs)])
         for a, b in zip(single, outs):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("R", [1, 2])
+@pytest.mark.parametrize("case", ["uniform", "hub", "sparse", "empty", "tiny"])
+@pytest.mark.parametrize("dsum", [False, True])
+def test_tail_seg_per_edge_w(R, case, dsum, cuda):
+    """tail_seg_reduce at D = 256 with per-edge W (h_idx = NULL, the training step's form) against float64
+    index_add references, and against the same call with h_idx = arange (W[h_idx[e]] = W[e]): dP and dsum
+    bitwise equal, dWedge within 1e-6.  Cases: runs of tails with and without edges, a hub tail with a
+    third of the edges, almost every tail without edges (3 edges on 300 tails), tiny graphs."""
+    g = torch.Generator().manual_seed(11 * R + len(case) + dsum)
+    D = 256
+    N = {"tiny": 5, "empty": 300}.get(case, 1000 + 7)
+    T = {"tiny": 37, "empty": 3, "sparse": 60}.get(case, 30_000)
+    t = torch.randint(0, N, (T,), generator=g)
+    if case == "hub":
+        t[: T // 3] = 517
+    if case == "uniform":
+        t[(t >= 100) & (t < 140)] = 99            # 40 consecutive tails without edges
+    t = torch.sort(t).values
+    tptr = torch.searchsorted(t, torch.arange(N + 1), right=False).to(torch.int32).to(cuda)
+    W = torch.rand(T, R, generator=g, dtype=torch.float64).to(cuda)
+    P = rnd(R, N, D, dev=cuda, gen=g)
+    dO = rnd(T, D, dev=cuda, gen=g)
+    tc = t.to(cuda)
+    dP, dWe = torch.full((R, N, D), 7.0, device=cuda), torch.empty(T, R, device=cuda)
+    ds = torch.full((N, D), 7.0, device=cuda) if dsum else None
+    ops.tail_seg_reduce(tptr, None, W.float(), dO.float(), P.float(), dP, dWe, dsum=ds)
+    for r in range(R):
+        close(dP[r], torch.zeros(N, D, dtype=torch.float64, device=cuda).index_add_(0, tc, W[:, r:r + 1] * dO), 1e-5)
+        if T:
+            close(dWe[:, r], (dO * P[r][tc]).sum(-1), 1e-5)
+    if dsum:
+        close(ds, torch.zeros(N, D, dtype=torch.float64, device=cuda).index_add_(0, tc, dO), 1e-5)
+    ident = torch.arange(T, dtype=torch.int32, device=cuda)
+    dP1, dWe1 = torch.empty(R, N, D, device=cuda), torch.empty(T, R, device=cuda)
+    ds1 = torch.empty(N, D, device=cuda) if dsum else None
+    ops.tail_seg_reduce(tptr, ident, W.float(), dO.float(), P.float(), dP1, dWe1, dsum=ds1)
+    assert torch.equal(dP, dP1)
+    if dsum:
+        assert torch.equal(ds, ds1)
+    if T:
+        assert _maxrel(dWe, dWe1) <= 1e-6

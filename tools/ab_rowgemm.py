@@ -41,10 +41,19 @@ def main(paths, reps=10, rounds=3, only=None):
     dz = torch.randn(N, R, device=dev, generator=g)
     WaT = torch.randn(R, D, device=dev, generator=g)
     xin = x.clone()
+    xpl = ops.f32_to_planes(x)                # pre-split planes tables (IDDGCN_PLANES_*)
+    xpl_in = xpl.clone()
+    Cpl = torch.empty_like(xpl)
     cases = {
         "fwd": ("fwd_combine (T)", x, S, C, dict(coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)),
         "bwd": ("bwd_dsig separate C (T)", do, S, C, dict(b_trans=True, act=L.ACT_DSIGMOID, aux=x)),
         "bwdip": ("bwd_dsig C = aux (T)", do, S, xin, dict(b_trans=True, act=L.ACT_DSIGMOID, aux=xin)),
+        "bwdpl": ("bwd_dsig planes aux, C = aux (T)", do, S, xpl_in,
+                  dict(b_trans=True, act=L.ACT_DSIGMOID, aux=xpl_in, planes=L.PLANES_AUX)),
+        "fwdpl": ("fwd_combine planes A+C (T)", xpl, S, Cpl, dict(coef=W, V=P, v_idx=t, v_rel_stride=N * D,
+                                                                  act=L.ACT_SIGMOID, planes=L.PLANES_A | L.PLANES_C)),
+        "fwdpa": ("fwd_combine planes A (T)", xpl, S, C, dict(coef=W, V=P, v_idx=t, v_rel_stride=N * D,
+                                                              act=L.ACT_SIGMOID, planes=L.PLANES_A)),
         "nbd": ("node bcast+dsig (N)", dOn, S, Cn, dict(b_trans=True, coef=dz, V=WaT, v_rel_stride=D, v_row_stride=0,
                                                         act=L.ACT_DSIGMOID, aux=Xn)),
         "nb": ("node bcast (N)", dOn, S, Cn, dict(b_trans=True, coef=dz, V=WaT, v_rel_stride=D, v_row_stride=0)),
