@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID, ACT_DSIGMOID_COMBINE = 0, 1, 2, 3
 GEMM_EXACT_F32, GEMM_SPLIT_F16 = 0, 1
@@ -39,6 +39,14 @@ class RowGemmArgs(ctypes.Structure):
         ("v_runs_max", ci),
         ("planes", ci),
     ]
+
+
+class TnArgs(ctypes.Structure):
+    """Mirror of iddgcn_tn_t (ABI 5)."""
+    _fields_ = [("M", cll), ("A", vp), ("B", vp), ("C", vp), ("accumulate", ci)]
+
+
+TN_BATCH = 4
 
 
 # name -> (restype, argtypes)
@@ -76,6 +84,7 @@ SIGNATURES = {
     "iddgcn_combine_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_combine_planes_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_gemm_tn_planes_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
+    "iddgcn_gemm_tn_batched_f32": (ci, [vp, ci, ctypes.POINTER(TnArgs), ci, vp, cll]),
     "iddgcn_distmult_bce_bf16": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci]),
     "iddgcn_distmult_bce_heads_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
                                             vp, ci]),

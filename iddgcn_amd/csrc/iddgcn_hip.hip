@@ -1559,12 +1559,31 @@ __device__ __forceinline__ f16x8 tr_frag16(const char* p0, const char* p1) {
     const v4s16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)p1);
     return __builtin_shufflevector(__builtin_bit_cast(f16x4, a), __builtin_bit_cast(f16x4, b), 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// Batched launches (TnBatch.n > 0): up to TN_BATCH independent TN GEMMs of the same form in one launch,
+// blockIdx.y = entry, each with its own row range split, operands and slab region (the node-level dK_r
+// and dS partials of a layer: one launch of ~256 workgroups instead of three of 256 each).
+constexpr int TN_BATCH = 4;
+struct TnBatch {
+    int n;                                    // 0: the kernel's scalar arguments
+    int nb[TN_BATCH];                         // workgroups (slabs) of each entry; the launch has max(nb)
+    long long M[TN_BATCH], rpb[TN_BATCH];
+    const float* A[TN_BATCH];
+    const float* B[TN_BATCH];
+    float* slab[TN_BATCH];
+};
 template <bool SEG, bool PA = false>
-__global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M, long long rows_per_block,
-                                                            const float* __restrict__ A,
-                                                            const float* __restrict__ B,
-                                                            float* __restrict__ slab, TnSegP sp) {
+__global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long long rpb_, const float* __restrict__ A_,
+                                                            const float* __restrict__ B_, float* __restrict__ slab_,
+                                                            TnSegP sp, TnBatch tb) {
     using namespace tn3;
+    const bool bat = !SEG && tb.n > 0;
+    const int ent = bat ? (int)blockIdx.y : 0;
+    if (bat && (int)blockIdx.x >= tb.nb[ent]) return;     // past this entry's slabs (whole workgroup)
+    const long long M = bat ? tb.M[ent] : M_;
+    const long long rows_per_block = bat ? tb.rpb[ent] : rpb_;
+    const float* __restrict__ A = bat ? tb.A[ent] : A_;
+    const float* __restrict__ B = bat ? tb.B[ent] : B_;
+    float* __restrict__ slab = bat ? tb.slab[ent] : slab_;
     static_assert(!(SEG && PA), "planes A: unfused TN only");
     constexpr int LDRA = PA ? 272 : LDR;                 // A row pitch (floats)
     constexpr int TILE_A = TK * LDRA;
@@ -2717,6 +2736,71 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(int n_slabs, long lon
     s *= scale;
     out[i] = accumulate ? out[i] + s : s;
 }
+// The same sums for n % 4 == 0 and a 16-B aligned slab: lane = one float4 column group (1 KB per wave load
+// instead of 256 B), the 4 waves of a block take fixed quarters of the slab range, combined in wave order
+// through LDS (deterministic; the association differs from reduce_slabs_kernel's single chain).  `out` may
+// be only 4-B aligned (weights inside the flat gradient buffer): scalar stores.
+__global__ __launch_bounds__(256) void reduce_slabs4_kernel(int n_slabs, long long n4, const f32x4* __restrict__ slab,
+                                                            float* __restrict__ out, int accumulate, float scale) {
+    __shared__ f32x4 part[3][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long i = (long long)blockIdx.x * 64 + lane;
+    const int b0 = (int)((long long)n_slabs * w / 4), b1 = (int)((long long)n_slabs * (w + 1) / 4);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (i < n4) {
+#pragma unroll 8
+        for (int b = b0; b < b1; ++b) s += slab[(long long)b * n4 + i];
+    }
+    if (w > 0) part[w - 1][lane] = s;
+    __syncthreads();
+    if (w == 0 && i < n4) {
+        s += part[0][lane];
+        s += part[1][lane];
+        s += part[2][lane];
+        s *= scale;
+        float* o = out + 4 * i;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = accumulate ? o[q] + s[q] : s[q];
+    }
+}
+// Any n, many slabs (the W_alpha TN's 1024 partials of (D + 1) R floats, the DistMult loss / drel partials):
+// 64 outputs per 1024-thread block, the 16 waves take fixed sixteenths of the slab range (one chain each),
+// combined in wave order through LDS.
+__global__ __launch_bounds__(1024) void reduce_slabs_split_kernel(int n_slabs, long long n, const float* __restrict__ slab,
+                                                                  float* __restrict__ out, int accumulate, float scale) {
+    __shared__ float part[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long i = (long long)blockIdx.x * 64 + lane;
+    const int b0 = (int)((long long)n_slabs * w / 16), b1 = (int)((long long)n_slabs * (w + 1) / 16);
+    float s = 0.f;
+    if (i < n) {
+#pragma unroll 8
+        for (int b = b0; b < b1; ++b) s += slab[(long long)b * n + i];
+    }
+    part[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && i < n) {
+        float t = part[0][lane];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) t += part[q][lane];
+        t *= scale;
+        out[i] = accumulate ? out[i] + t : t;
+    }
+}
+void launch_reduce_slabs(hipStream_t st, int n_slabs, long long n, const float* slab, float* out, int accumulate,
+                         float scale) {
+    if (n % 4 == 0 && n_slabs >= 8 && (reinterpret_cast<uintptr_t>(slab) & 15) == 0) {
+        const long long n4 = n / 4;
+        hipLaunchKernelGGL(reduce_slabs4_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, n_slabs, n4,
+                           reinterpret_cast<const f32x4*>(slab), out, accumulate, scale);
+    } else if (n_slabs >= 64) {
+        hipLaunchKernelGGL(reduce_slabs_split_kernel, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, st, n_slabs, n,
+                           slab, out, accumulate, scale);
+    } else {
+        hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_slabs, n, slab,
+                           out, accumulate, scale);
+    }
+}
 
 __global__ __launch_bounds__(256) void adam_kernel(long long n, float* __restrict__ var, float* __restrict__ m,
                                                    float* __restrict__ v, const float* __restrict__ g, float alpha,
@@ -2827,7 +2911,9 @@ int check_rowgemm(const iddgcn_rowgemm_t& a) {
 // One launch of up to ROWGEMM_BATCH v3 GEMMs of the same variant (blockIdx.y = entry).  The persistent
 // grid is ~256 workgroups in all (one per CU: 131-155 KB of LDS each), shared out over the entries.
 void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel, bool bf = false) {
-    const long long per = n > 0 ? (256 + n - 1) / n : 256;
+    // floor: every workgroup of the launch resident at once (ceil gave 7 entries 37 x 7 = 259 > 256 CUs, so three
+    // workgroups ran in a second wave and the launch took ~2x)
+    const long long per = n > 0 ? (256 / n > 0 ? 256 / n : 1) : 256;
     long long nbmax = 0;
     for (int k = 0; k < n; ++k) {
         RowGemmP& p = pb.p[k];
@@ -3125,7 +3211,7 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
     if (d == 256 && g_gemm_split) {
         hipLaunchKernelGGL(gemm_tn256_x3_kernel<false>, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab,
-                           TnSegP{});
+                           TnSegP{}, TnBatch{});
     } else if (d == 256 && g_rowgemm_path != 1) {
         hipLaunchKernelGGL(gemm_tn256_dma_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
     } else switch (d) {
@@ -3138,8 +3224,63 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     int rc = launch_status();
     if (rc) return rc;
     const long long n = (long long)d * d;
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_blocks, n, slab, C,
-                       accumulate, 1.0f);
+    launch_reduce_slabs(st, n_blocks, n, slab, C, accumulate, 1.0f);
+    return launch_status();
+}
+
+int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n, float* slab, long long slab_floats) {
+    if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
+    if (n < 0 || n > IDDGCN_TN_BATCH || (n > 0 && (!e || !slab))) return IDDGCN_E_BAD_ARG;
+    for (int k = 0; k < n; ++k)
+        if (e[k].M < 0 || (e[k].M > 0 && (!e[k].A || !e[k].B)) || !e[k].C) return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const long long dd = (long long)d * d;
+    if (!(d == 256 && g_gemm_split)) {
+        // other widths and the exact mode: the single-call kernels one after another (slab reused in order)
+        for (int k = 0; k < n; ++k) {
+            if (e[k].M == 0) {                     // no rows: C = 0, or C unchanged when accumulating
+                if (!e[k].accumulate && hipMemsetAsync(e[k].C, 0, dd * sizeof(float), st) != hipSuccess)
+                    return launch_status();
+                continue;
+            }
+            long long nb = iddgcn_gemm_tn_blocks(e[k].M, d);
+            if (nb * dd > slab_floats) nb = slab_floats / dd;           // fewer partials, longer row ranges
+            if (nb < 1) return IDDGCN_E_BAD_ARG;
+            const int rc = iddgcn_gemm_tn_f32(stream, e[k].M, d, e[k].A, e[k].B, slab, (int)nb, e[k].C, e[k].accumulate);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    TnBatch tb{};
+    tb.n = n;
+    long long off = 0;
+    int nbk[IDDGCN_TN_BATCH] = {0};
+    unsigned nbmax = 1;
+    for (int k = 0; k < n; ++k) {
+        const long long tiles = (e[k].M + 31) / 32;
+        long long nb = 256 / n;                    // every workgroup of the launch resident at once
+        if (nb > tiles) nb = tiles;
+        if (nb < 1) nb = 1;
+        long long rpb = (e[k].M + nb - 1) / nb;
+        rpb = ((rpb + 31) / 32) * 32;
+        if (rpb < 32) rpb = 32;
+        nbk[k] = (int)nb;
+        tb.nb[k] = (int)nb;
+        if ((unsigned)nb > nbmax) nbmax = (unsigned)nb;
+        tb.M[k] = e[k].M;
+        tb.rpb[k] = rpb;
+        tb.A[k] = e[k].A;
+        tb.B[k] = e[k].B;
+        tb.slab[k] = slab + off;
+        off += nb * dd;
+    }
+    if (off > slab_floats) return IDDGCN_E_BAD_ARG;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(gemm_tn256_x3_kernel<false>, dim3(nbmax, (unsigned)n), dim3(512), 0, st, 0LL, 0LL, nullptr,
+                       nullptr, nullptr, TnSegP{}, tb);
+    int rc = launch_status();
+    if (rc) return rc;
+    for (int k = 0; k < n; ++k) launch_reduce_slabs(st, nbk[k], dd, tb.slab[k], e[k].C, e[k].accumulate, 1.0f);
     return launch_status();
 }
 
@@ -3152,12 +3293,11 @@ int iddgcn_gemm_tn_planes_f32(void* stream, long long M, int d, const void* A, c
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
     hipLaunchKernelGGL((gemm_tn256_x3_kernel<false, true>), dim3(n_blocks), dim3(512), 0, st, M, rpb,
-                       (const float*)A, B, slab, TnSegP{});
+                       (const float*)A, B, slab, TnSegP{}, TnBatch{});
     int rc = launch_status();
     if (rc) return rc;
     const long long n = (long long)d * d;
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_blocks, n, slab, C,
-                       accumulate, 1.0f);
+    launch_reduce_slabs(st, n_blocks, n, slab, C, accumulate, 1.0f);
     return launch_status();
 }
 
@@ -3172,12 +3312,11 @@ int iddgcn_gemm_tn_seg_f32(void* stream, long long M, int d, const float* A, con
         return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;
     const TnSegP sp{row_beg, tail, W, P, p_rel_stride, dP, dWedge, R};
-    hipLaunchKernelGGL(gemm_tn256_x3_kernel<true>, dim3(n_blocks), dim3(512), 0, st, M, 0LL, A, B, slab, sp);
+    hipLaunchKernelGGL(gemm_tn256_x3_kernel<true>, dim3(n_blocks), dim3(512), 0, st, M, 0LL, A, B, slab, sp, TnBatch{});
     int rc = launch_status();
     if (rc) return rc;
     const long long n = (long long)d * d;
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_blocks, n, slab, C,
-                       accumulate, 1.0f);
+    launch_reduce_slabs(st, n_blocks, n, slab, C, accumulate, 1.0f);
     return launch_status();
 }
 
@@ -3209,8 +3348,7 @@ int iddgcn_gemm_tn_narrow_f32(void* stream, long long M, int d, int R, const flo
     const long long stride = (long long)(d + 1) * R;
     // reduce with stride: reuse reduce_slabs on a strided view by reducing the whole row then copying
     // (n_blocks x (D+1)R is tiny), writing into dWa / dba through two launches.
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, st, n_blocks, stride,
-                       slab, slab + (long long)n_blocks * stride, 0, 1.0f);
+    launch_reduce_slabs(st, n_blocks, stride, slab, slab + (long long)n_blocks * stride, 0, 1.0f);
     rc = launch_status();
     if (rc) return rc;
     const float* red = slab + (long long)n_blocks * stride;
@@ -3435,8 +3573,7 @@ int iddgcn_reduce_slabs_f32(void* stream, int n_slabs, long long n, const float*
                             float scale) {
     if (n_slabs < 1 || n < 0 || !slab || !out) return IDDGCN_E_BAD_ARG;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       n_slabs, n, slab, out, accumulate, scale);
+    launch_reduce_slabs((hipStream_t)stream, n_slabs, n, slab, out, accumulate, scale);
     return launch_status();
 }
 
@@ -3496,8 +3633,7 @@ int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const v
     int rc = launch_status();
     if (rc) return rc;
     const long long n = (long long)d * d;
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n_blocks, n, slab, C,
-                       accumulate, 1.0f);
+    launch_reduce_slabs(st, n_blocks, n, slab, C, accumulate, 1.0f);
     return launch_status();
 }
 

@@ -198,7 +198,8 @@ class Workspace:
         self.WaT = e(R, D)
         self.drel_slab = e(self.nb_dm * R * D)
         self.loss_slab = e(self.nb_dm)
-        tn = max(ops.tn_blocks(T, D), ops.tn_blocks(N, D))
+        # partials of the edge TN, or of one batched launch of up to L.TN_BATCH node-level TNs
+        tn = max(ops.tn_blocks(T, D), min(256, L.TN_BATCH * ops.tn_blocks(N, D)), ops.tn_blocks(N, D))
         self.tn_slab = e(tn * D * D)
         self.narrow_slab = e((ops.tn_narrow_blocks(N) + 1) * (D + 1) * R)
 
@@ -401,21 +402,24 @@ class Engine:
             Xin = ws.X[l - 1] if l > 0 else P["E"]
             ws.WaT.copy_(P[f"Wa{l + 1}"].t())
             ops.gemm_tn_narrow(Xin, ws.dz, G[f"Wa{l + 1}"], G[f"ba{l + 1}"], ws.narrow_slab)
+            # node-level weight gradients of the layer, batched (one launch per L.TN_BATCH): the head-chain
+            # part of dS (added to the edge part, layers 2-3) or dS1, and dK_r = AE_r^T dP_r
+            K, dK = P[f"K{l + 1}"], G[f"K{l + 1}"]
+            sh = self.node_shard
+            tn = [(Xin, dOn, G[f"S{l + 1}"], True) if l > 0 else (P["E"], ws.dES, G["S1"], False)]
+            if sh is None:
+                tn += [(ws.AE[r], ws.dP[r], dK[r], False) for r in range(R)]
+            for i in range(0, len(tn), L.TN_BATCH):
+                ops.gemm_tn_batched(tn[i:i + L.TN_BATCH], ws.tn_slab)
             if l > 0:
-                ops.gemm_tn(Xin, dOn, G[f"S{l + 1}"], ws.tn_slab, accumulate=True)
                 ops.rowgemm(dOn, Sl, dOn_next, b_trans=True, coef=ws.dz, V=ws.WaT, v_rel_stride=D,
                             v_row_stride=0, act=L.ACT_DSIGMOID, aux=Xin)
             else:
-                ops.gemm_tn(P["E"], ws.dES, G["S1"], ws.tn_slab)
                 # dE (head input of layer 1 + x·S1 inputs of both sides)
                 ops.rowgemm(ws.dES, Sl, G["E"], b_trans=True, coef=ws.dz, V=ws.WaT, v_rel_stride=D,
                             v_row_stride=0)
-            # relation kernels: dK_r = AE_r^T dP_r ; dAE_r += dP_r K_r^T
-            K, dK = P[f"K{l + 1}"], G[f"K{l + 1}"]
-            sh = self.node_shard
+            # relation kernels: dK_r = AE_r^T dP_r (above) ; dAE_r += dP_r K_r^T
             if sh is None:
-                for r in range(R):
-                    ops.gemm_tn(ws.AE[r], ws.dP[r], dK[r], ws.tn_slab)
                 ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2)))
                                      for r in range(R)])
             else:

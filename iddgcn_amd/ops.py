@@ -202,6 +202,26 @@ def gemm_tn_seg(A, B, C, slab, row_beg, tail, W, P, dP, dWedge, max_tile_runs, a
             "gemm_tn_seg")
 
 
+def gemm_tn_batched(entries, slab):
+    """Up to L.TN_BATCH independent C (+)= A^T B, entries = [(A, B, C, accumulate), ...] (fp32, same D), in one
+    launch (iddgcn_gemm_tn_batched_f32, ABI 5); slab holds the partials of all entries."""
+    if not entries:
+        return
+    if len(entries) > L.TN_BATCH:
+        raise L.IddgcnError(f"gemm_tn_batched: at most {L.TN_BATCH} entries")
+    D = entries[0][0].shape[1]
+    arr = (L.TnArgs * len(entries))()
+    for k, (A, B, C, acc) in enumerate(entries):
+        M = A.shape[0]
+        _req(A, _F32, (M, D), "A")
+        _req(B, _F32, (M, D), "B")
+        _req(C, _F32, (D, D), "C")
+        arr[k] = L.TnArgs(M, _ptr(A), _ptr(B), _ptr(C), int(bool(acc)))
+    _req(slab, _F32, None, "slab")
+    L.check(L.lib().iddgcn_gemm_tn_batched_f32(_stream(), D, arr, len(entries), _ptr(slab), slab.numel()),
+            "gemm_tn_batched")
+
+
 def tn_narrow_blocks(M):
     return int(L.lib().iddgcn_gemm_tn_narrow_blocks(int(M)))
 

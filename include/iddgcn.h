@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 4
+#define IDDGCN_ABI_VERSION 5
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -133,6 +133,21 @@ int iddgcn_set_gemm_precision(int mode);
 int iddgcn_gemm_tn_blocks(long long M, int d);
 int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const float* B,
                        float* slab, int n_blocks, float* C, int accumulate);
+/* Up to IDDGCN_TN_BATCH independent C_k (+)= A_k^T B_k (fp32, same D) in one launch (ABI 5): at D = 256 in the
+ * split-fp16 mode one launch of ~256 workgroups shared out over the entries (blockIdx.y = entry), then each
+ * entry's partials summed in block order; otherwise the single-call kernels in turn.  slab: slab_floats floats,
+ * at least sum_k min(256 / n, ceil(M_k / 32)) * D * D (the single-call fallback uses up to
+ * iddgcn_gemm_tn_blocks(M_k, D) partials, fewer when the slab is smaller, at least one D * D).  The node-level weight gradients of one layer: dK_r = AE_r^T dP_r
+ * and the head-chain part of dS (tape.gradient, IDDGCN.py:172, of :62-63 and :71-77). */
+#define IDDGCN_TN_BATCH 4
+typedef struct {
+    long long M;
+    const float* A;
+    const float* B;
+    float* C;
+    int accumulate;
+} iddgcn_tn_t;
+int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n, float* slab, long long slab_floats);
 /* iddgcn_gemm_tn_f32 with A a planes table (IDDGCN_PLANES_A; D = 256, split-fp16 mode): dS = x^T do
  * with x^{l} pre-split by its producer (IDDGCN.py:62-63 autodiff). */
 int iddgcn_gemm_tn_planes_f32(void* stream, long long M, int d, const void* A, const float* B, float* slab,

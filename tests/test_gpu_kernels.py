@@ -886,3 +886,41 @@ def test_tail_seg_per_edge_w(R, case, dsum, cuda):
         assert torch.equal(ds, ds1)
     if T:
         assert _maxrel(dWe, dWe1) <= 1e-6
+
+
+@pytest.mark.parametrize("D,mode", [(256, "split"), (256, "exact"), (64, "exact")])
+def test_gemm_tn_batched(D, mode, cuda):
+    """iddgcn_gemm_tn_batched_f32 (one launch, blockIdx.y = entry, at D = 256 split; the single-call kernels in
+    turn otherwise) against float64 references and the single-call results: entries of different row counts
+    (one empty), accumulate on / off, up to TN_BATCH entries; the batched launch is deterministic."""
+    g = torch.Generator().manual_seed(D + len(mode))
+    Ms = [30_001, 4_100, 0, 777]
+    ents, refs, singles = [], [], []
+    with _gemm_mode(L.GEMM_SPLIT_F16 if mode == "split" else L.GEMM_EXACT_F32):
+        for k, M in enumerate(Ms):
+            A = torch.randn(M, D, generator=g, dtype=torch.float64)
+            B = torch.randn(M, D, generator=g, dtype=torch.float64) * 10 ** (-3 * k)
+            C0 = torch.randn(D, D, generator=g, dtype=torch.float64)
+            acc = k % 2 == 1
+            Af, Bf = A.float().to(cuda), B.float().to(cuda)
+            C = C0.float().to(cuda)
+            ents.append((Af, Bf, C, acc))
+            refs.append(A.t() @ B + (C0.float().double() if acc else 0))
+            Cs = C0.float().to(cuda)
+            if M:                                  # (the single-call entry takes no empty operands)
+                slab1 = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
+                ops.gemm_tn(Af, Bf, Cs, slab1, accumulate=acc)
+            singles.append(Cs)
+        Cinit = [c.clone() for _, _, c, _ in ents]
+        slab = torch.empty(256 * D * D, device=cuda)
+        ops.gemm_tn_batched(ents, slab)
+        again = [c.clone() for c in Cinit]
+        ops.gemm_tn_batched([(a, b, c2, acc) for (a, b, _, acc), c2 in zip(ents, again)], slab)
+    for (_, _, C, _), C2, ref, Cs, M in zip(ents, again, refs, singles, Ms):
+        assert torch.equal(C, C2)
+        ref = ref.to(cuda)
+        if M == 0:
+            assert torch.equal(C.double(), ref)
+            continue
+        bar = max(2 * _maxrel(Cs, ref), 2e-6)
+        assert _maxrel(C, ref) <= bar
