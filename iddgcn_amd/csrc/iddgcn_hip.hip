@@ -1787,18 +1787,23 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
         __syncthreads();
         if constexpr (SEG) seg_scan(0, 0);
         convert(0);
+        if (nt > 1) {                                // tile 1 in flight while tile 0's MFMAs run
+            stage(1, 1);
+            if constexpr (SEG) {
+                seg_stage(tnext, 1, 1);
+                tnext = load_tails(2);
+            }
+        }
         __syncthreads();
     }
+    // Tile t+2's DMA is issued as soon as every wave's MFMAs of tile t are done (the barrier after them
+    // frees buffer b), so it is in flight during tile t+1's conversion AND its MFMAs; issued at the top of
+    // the iteration instead (round 2 until here), nothing was in flight during the conversions and
+    // barriers and the TN ran at the sum of its DMA time and its compute time (ablations,
+    // profiles/r02/ablations/tn_abl.txt).
     int b = 0;
     for (long long t = 0; t < nt; ++t, b ^= 1) {
         if constexpr (SEG) seg_dwedge(t);
-        if (t + 1 < nt) {
-            stage(t + 1, b ^ 1);
-            if constexpr (SEG) {
-                seg_stage(tnext, t + 1, b ^ 1);
-                tnext = load_tails(t + 2);
-            }
-        }
         // B-side scales of this tile: rescale the accumulators whose block scale dropped
 #pragma unroll
         for (int cj = 0; cj < 8; ++cj) {
@@ -1834,8 +1839,15 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
                 acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[cj], 0, 0, 0);
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // tile t+1 landed (issued one tile ago)
+        __syncthreads();                                         // buffer b free
+        if (t + 2 < nt) {
+            stage(t + 2, b);
+            if constexpr (SEG) {
+                seg_stage(tnext, t + 2, b);
+                tnext = load_tails(t + 3);
+            }
+        }
         if (t + 1 < nt) {
             if constexpr (SEG) seg_scan(t + 1, b ^ 1);
             convert(b ^ 1);
