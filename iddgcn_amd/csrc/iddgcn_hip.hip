@@ -87,75 +87,54 @@ __device__ __forceinline__ float group_sum(float v) {
 // butterfly that halves the value set at each level: K-1 + log2(LPR/K) ... shuffles instead of
 // K*log2(LPR).  On return v[0] holds, in every lane, the full sum of value index
 // sub / (LPR/K).  LPR == 64 and 32 use the permlane/DPP exchanges above (no LDS crossbar).
+// The levels are a compile-time recursion (M = lane distance, KC = values still held): with the live
+// count as a run-time variable the compiler indexed v[] dynamically (a v_cmp/v_cndmask/s_nop chain per
+// element: ~1300 extra instructions per edge group in the R = 8 tail reduction).
+template <int LPR, int K, int KC, int M>
+__device__ __forceinline__ void multi_reduce_level(float (&v)[K], int sub) {
+    if constexpr (M >= 1) {
+        constexpr bool PERM = LPR == 64 || LPR == 32;        // permlane / DPP exchanges
+        constexpr bool SWAP = (LPR == 64 && M == 32) || (PERM && M == 16);
+        if constexpr (KC > 1) {
+            constexpr int half = KC / 2;
+            if constexpr (SWAP) {      // one register swap exchanges the kept/sent halves of a value pair
+#pragma unroll
+                for (int j = 0; j < half; ++j) {
+                    float a = v[j], b = v[half + j];
+                    if constexpr (M == 32) pl_swap32(a, b);
+                    else pl_swap16(a, b);
+                    v[j] = a + b;
+                }
+            } else {
+                const bool up = (sub & M) != 0;
+#pragma unroll
+                for (int j = 0; j < half; ++j) {
+                    const float keep = up ? v[half + j] : v[j];
+                    const float send = up ? v[j] : v[half + j];
+                    if constexpr (PERM) v[j] = keep + xpartner_dpp<M>(send);
+                    else v[j] = keep + __shfl_xor(send, M, 64);
+                }
+            }
+            multi_reduce_level<LPR, K, half, M / 2>(v, sub);
+        } else {
+            if constexpr (SWAP) {
+                float a = v[0], b = v[0];
+                if constexpr (M == 32) pl_swap32(a, b);
+                else pl_swap16(a, b);
+                v[0] = a + b;
+            } else if constexpr (PERM) {
+                v[0] += xpartner_dpp<M>(v[0]);
+            } else {
+                v[0] += __shfl_xor(v[0], M, 64);
+            }
+            multi_reduce_level<LPR, K, 1, M / 2>(v, sub);
+        }
+    }
+}
 template <int LPR, int K>
 __device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
     static_assert((K & (K - 1)) == 0 && K <= LPR, "K must be a power of two <= LPR");
-    if constexpr (LPR == 64 || LPR == 32) {
-        // levels 32 and 16: one register swap exchanges the kept/sent halves of a value pair
-        int kc = K;
-        auto swap_level = [&](auto swapper) {
-            if (kc > 1) {
-                const int half = kc / 2;
-#pragma unroll
-                for (int j = 0; j < K / 2; ++j) {
-                    if (j < half) {
-                        float a = v[j], b = v[half + j];
-                        swapper(a, b);
-                        v[j] = a + b;
-                    }
-                }
-                kc = half;
-            } else {
-                float a = v[0], b = v[0];
-                swapper(a, b);
-                v[0] = a + b;
-            }
-        };
-        if constexpr (LPR == 64) swap_level([](float& a, float& b) { pl_swap32(a, b); });
-        swap_level([](float& a, float& b) { pl_swap16(a, b); });
-        auto dpp_level = [&](auto mtag) {
-            constexpr int m = decltype(mtag)::value;
-            if (kc > 1) {
-                const bool up = (sub & m) != 0;
-                const int half = kc / 2;
-#pragma unroll
-                for (int j = 0; j < K / 2; ++j) {
-                    if (j < half) {
-                        const float keep = up ? v[half + j] : v[j];
-                        const float send = up ? v[j] : v[half + j];
-                        v[j] = keep + xpartner_dpp<m>(send);
-                    }
-                }
-                kc = half;
-            } else {
-                v[0] += xpartner_dpp<m>(v[0]);
-            }
-        };
-        dpp_level(std::integral_constant<int, 8>{});
-        dpp_level(std::integral_constant<int, 4>{});
-        dpp_level(std::integral_constant<int, 2>{});
-        dpp_level(std::integral_constant<int, 1>{});
-        return v[0];
-    }
-    int kc = K;
-#pragma unroll
-    for (int m = LPR / 2; m >= 1; m >>= 1) {
-        if (kc > 1) {
-            const bool up = (sub & m) != 0;
-            const int half = kc / 2;
-#pragma unroll
-            for (int j = 0; j < K / 2; ++j) {
-                if (j < half) {
-                    const float keep = up ? v[half + j] : v[j];
-                    const float send = up ? v[j] : v[half + j];
-                    v[j] = keep + __shfl_xor(send, m, 64);
-                }
-            }
-            kc = half;
-        } else {
-            v[0] += __shfl_xor(v[0], m, 64);
-        }
-    }
+    multi_reduce_level<LPR, K, K, LPR / 2>(v, sub);
     return v[0];
 }
 
@@ -2413,27 +2392,10 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
         const int len = end - beg;
         const f32x4 a = live ? ld4(Xh + n * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        // slot s takes edge groups k = (it*SLOTS + s)*U: same trip count for the whole wave
-        const int iters = (len + SLOTS * U - 1) / (SLOTS * U);
-        for (int it = 0; it < iters; ++it) {
-            const int k = (it * SLOTS + slot) * U;
-            long long e[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                e[u] = (k + u < len) ? (long long)perm[beg + k + u] : -1;
-                if constexpr (SCALAR) e[u] = __builtin_amdgcn_readfirstlane((int)e[u]);   // scalar loads below
-            }
-            int rr[U];
-            float yy[U];
-            f32x4 b[U], rho[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool ok = e[u] >= 0;
-                rr[u] = ok ? r_idx[e[u]] : 0;
-                yy[u] = (ok && y) ? y[e[u]] : 0.f;
-                if constexpr (SCALAR) rr[u] = __builtin_amdgcn_readfirstlane(rr[u]);
-                b[u] = ok ? ld4e<BF>(Xt, e[u] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+        // one group of U edges: e[u] (-1 past the segment), their relations, labels and tail rows
+        auto body = [&](const long long (&e)[U], const int (&rr)[U], const float (&yy)[U],
+                        const f32x4 (&b)[U]) __attribute__((always_inline)) {
+            f32x4 rho[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) rho[u] = ld4(rel + (long long)rr[u] * D + sub * 4);
             float sc[U];
@@ -2473,6 +2435,78 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 for (int r = 0; r < RT; ++r)
                     if (r == rr[u]) dr[r] += dre;
                 acc = fma4(b[u] * ds, rho[u], acc);     // same explicit fma as seg_gather_reduce
+            }
+        };
+        if constexpr (SCALAR) {
+            // many relations (one head per wave): a software pipeline over edge groups — the perm entries of
+            // group i+2 and the relations, labels and rows of group i+1 load while group i is computed.  Every
+            // index goes through a VECTOR load (lane u < U: edge u of the group) and is broadcast with readlane:
+            // the scalar loads of the previous form return out of order, so each wait for one of them was an
+            // lgkmcnt(0) on everything in flight (a full memory latency, twice per group: perm, then r_idx).
+            // Rows stay in their storage type until used.
+            using RawT = typename std::conditional<BF, bf16x4, f32x4>::type;
+            auto load_perm = [&](int k) __attribute__((always_inline)) {
+                return (sub < U && k + sub < len) ? perm[beg + k + sub] : -1;
+            };
+            int evn = -1, rvn = 0;
+            float yvn = 0.f;
+            RawT bn[U];
+            auto load_group = [&](int ev) __attribute__((always_inline)) {
+                rvn = ev >= 0 ? r_idx[ev] : 0;
+                yvn = (ev >= 0 && y) ? y[ev] : 0.f;
+                evn = ev;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int eu = __builtin_amdgcn_readlane(ev, u);
+                    const RawT* src = reinterpret_cast<const RawT*>(reinterpret_cast<const char*>(Xt) +
+                                                                   ((long long)eu * D + sub * 4) * (BF ? 2 : 4));
+                    if (eu >= 0) bn[u] = *src;
+                    else bn[u] = RawT{};
+                }
+            };
+            int ev2 = -1;
+            if (len > 0) {
+                const int ev1 = load_perm(0);
+                ev2 = load_perm(U);
+                load_group(ev1);
+            }
+            for (int k0 = 0; k0 < len; k0 += U) {
+                long long e[U];
+                int rr[U];
+                float yy[U];
+                f32x4 b[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    e[u] = __builtin_amdgcn_readlane(evn, u);
+                    rr[u] = __builtin_amdgcn_readlane(rvn, u);
+                    yy[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, yvn), u));
+                    if constexpr (BF) b[u] = bf4_to_f32(bn[u]);
+                    else b[u] = bn[u];
+                }
+                const int ev3 = load_perm(k0 + 2 * U);
+                if (k0 + U < len) load_group(ev2);
+                ev2 = ev3;
+                body(e, rr, yy, b);
+            }
+        } else {
+            // slot s takes edge groups k = (it*SLOTS + s)*U: same trip count for the whole wave
+            const int iters = (len + SLOTS * U - 1) / (SLOTS * U);
+            for (int it = 0; it < iters; ++it) {
+                const int k = (it * SLOTS + slot) * U;
+                long long e[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) e[u] = (k + u < len) ? (long long)perm[beg + k + u] : -1;
+                int rr[U];
+                float yy[U];
+                f32x4 b[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const bool ok = e[u] >= 0;
+                    rr[u] = ok ? r_idx[e[u]] : 0;
+                    yy[u] = (ok && y) ? y[e[u]] : 0.f;
+                    b[u] = ok ? ld4e<BF>(Xt, e[u] * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+                body(e, rr, yy, b);
             }
         }
 #pragma unroll
@@ -2586,12 +2620,8 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     }
     f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
     const int len = end - beg;
-    // slot s takes edge groups k = k0 + s*U, k0 = 0, SLOTS*U, ...: the whole wave is one node and every
-    // slot runs the same trip count (wave-uniform).  The k0 < len form (not an iteration count) keeps
-    // the D = 256 loop (SLOTS = 1) as fast as the pre-slot kernel: 0.92 vs 1.01 ms per config-3 launch.
-    for (int k0 = 0; k0 < len; k0 += SLOTS * U) {
-        const int k = k0 + slot * U;
-        f32x4 d[U];
+    // One edge group: its rows d[U] and coefficients w[U][R] (zeros past the segment), then the sums.
+    auto load_group = [&](int k, f32x4 (&d)[U], float (&w)[U][R]) __attribute__((always_inline)) {
         int hh[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -2601,11 +2631,12 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             if constexpr (SCALAR) hh[u] = __builtin_amdgcn_readfirstlane(hh[u]);     // scalar W loads
             d[u] = a ? ld4e<BF>(dO, (long long)(beg + k + u) * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        float w[U][R];
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int r = 0; r < R; ++r) w[u][r] = (k + u < len) ? W[(long long)hh[u] * R + r] : 0.f;
+    };
+    auto group = [&](int k, const f32x4 (&d)[U], const float (&w)[U][R]) __attribute__((always_inline)) {
         constexpr int KV = U * R;
         constexpr int KP = KV <= 4 ? 4 : KV <= 8 ? 8 : KV <= 16 ? 16 : 32;   // padded to a power of two
         float dw[KP];
@@ -2637,6 +2668,60 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
                 for (int j = 0; j < KV; ++j)
                     if (k + j / R < len) dWedge[(long long)(beg + k + j / R) * R + j % R] = dw[j];
             }
+        }
+    };
+    if constexpr (SCALAR) {
+        // many relations (R >= 4, one node per wave): ~150 VGPRs leave 3 waves per SIMD, and one group
+        // of U rows in flight per wave did not cover the memory latency (R = 8 bf16: 1.4 TB/s).  The next
+        // group's rows and coefficients are loaded while this group is summed (same sums, same order).
+        // Rows stay in their storage type (bf16 or fp32) until used: a conversion next to the load would
+        // make the compiler wait for it there.  The group's U x R coefficients arrive by ONE vector load
+        // (lane j: coefficient j, contiguous for per-edge W) and are broadcast with readlane: scalar loads
+        // (the previous form) return out of order, so waiting for this group's coefficients meant
+        // lgkmcnt(0), i.e. also for the next group's, a full memory latency per group.
+        static_assert(U * R <= 64, "one coefficient per lane");
+        using RawT = typename std::conditional<BF, bf16x4, f32x4>::type;
+        RawT dn[U];
+        float wvn;
+        auto load_raw = [&](int k) __attribute__((always_inline)) {
+            const int u = sub / R, r = sub - u * R;          // this lane's coefficient (sub < U * R)
+            const bool wa = sub < U * R && k + u < len;
+            const long long we = h_idx ? (wa ? (long long)h_idx[beg + k + u] : 0) : (long long)(beg + k + u);
+            wvn = wa ? W[we * R + r] : 0.f;
+#pragma unroll
+            for (int uu = 0; uu < U; ++uu) {
+                const RawT* src = reinterpret_cast<const RawT*>(reinterpret_cast<const char*>(dO) +
+                                                               ((long long)(beg + k + uu) * D + sub * 4) * (BF ? 2 : 4));
+                if (k + uu < len) dn[uu] = *src;
+                else dn[uu] = RawT{};
+            }
+        };
+        if (len > 0) load_raw(0);
+        for (int k0 = 0; k0 < len; k0 += U) {
+            f32x4 dc[U];
+            float wc[U][R];
+            const float wv = wvn;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if constexpr (BF) dc[u] = bf4_to_f32(dn[u]);
+                else dc[u] = dn[u];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    wc[u][r] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wv), u * R + r));
+            }
+            if (k0 + U < len) load_raw(k0 + U);
+            group(k0, dc, wc);
+        }
+    } else {
+        // slot s takes edge groups k = k0 + s*U, k0 = 0, SLOTS*U, ...: the whole wave is one node and every
+        // slot runs the same trip count (wave-uniform).  The k0 < len form (not an iteration count) keeps
+        // the D = 256 loop (SLOTS = 1) as fast as the pre-slot kernel: 0.92 vs 1.01 ms per config-3 launch.
+        for (int k0 = 0; k0 < len; k0 += SLOTS * U) {
+            const int k = k0 + slot * U;
+            f32x4 d[U];
+            float w[U][R];
+            load_group(k, d, w);
+            group(k, d, w);
         }
     }
     // slot partials, fixed order: pairs (s, s ^ 1), then (s, s ^ 2), ... (lane distance LPR * m)

@@ -845,14 +845,15 @@ def test_rowgemm256_batched_one_launch_bitwise(gm, cuda):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("R", [1, 2])
+@pytest.mark.parametrize("R", [1, 2, 4, 8])
 @pytest.mark.parametrize("case", ["uniform", "hub", "sparse", "empty", "tiny"])
 @pytest.mark.parametrize("dsum", [False, True])
 def test_tail_seg_per_edge_w(R, case, dsum, cuda):
     """tail_seg_reduce at D = 256 with per-edge W (h_idx = NULL, the training step's form) against float64
     index_add references, and against the same call with h_idx = arange (W[h_idx[e]] = W[e]): dP and dsum
     bitwise equal, dWedge within 1e-6.  Cases: runs of tails with and without edges, a hub tail with a
-    third of the edges, almost every tail without edges (3 edges on 300 tails), tiny graphs."""
+    third of the edges, almost every tail without edges (3 edges on 300 tails), tiny graphs.  R >= 4 runs the
+    software-pipelined one-node-per-wave loop (scalar coefficient loads, next edge group in flight)."""
     g = torch.Generator().manual_seed(11 * R + len(case) + dsum)
     D = 256
     N = {"tiny": 5, "empty": 300}.get(case, 1000 + 7)
