@@ -1,6 +1,7 @@
 """Run one edge-GEMM case a few times at config-3 shape (for rocprofv3 --pmc passes).
 
-usage: python tools/gemm_probe.py {fwd,bwd,plain,tn} {split,exact} [reps]
+usage: python tools/gemm_probe.py {fwd,bwd,plain,tn,fwd8} {split,exact} [reps]
+fwd8: the config-5 form (R = 8 relations, bf16 edge tables, degree 50) at T = 10M, N = 200k
 """
 import sys
 
@@ -14,11 +15,20 @@ from iddgcn_amd import ops  # noqa: E402
 def main(case, mode, reps=3, T=4_000_000, N=100_000, D=256, R=2):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
+    if case == "fwd8":
+        T, N, R = 10_000_000, 200_000, 8
     A = torch.rand(T, D, device=dev, generator=g)
     S = torch.randn(D, D, device=dev, generator=g)
     C = torch.empty(T, D, device=dev)
     L.lib().iddgcn_set_gemm_precision(L.GEMM_SPLIT_F16 if mode == "split" else L.GEMM_EXACT_F32)
-    if case == "fwd":
+    if case == "fwd8":
+        A = A.bfloat16()
+        C = C.bfloat16()
+        W = torch.rand(T, R, device=dev, generator=g)
+        P = torch.randn(R, N, D, device=dev, generator=g)
+        t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
+        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)  # noqa
+    elif case == "fwd":
         W = torch.rand(T, R, device=dev, generator=g)
         P = torch.randn(R, N, D, device=dev, generator=g)
         t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
