@@ -733,6 +733,10 @@ constexpr int REC_CAP = 8;
 template <int NV, bool AUX, bool HAS_COEF, bool X3, bool REC = false, bool CW = false, bool BF = false, bool PL = false>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     using namespace r3;
+    // A row pitch: bf16 rows (BF) need 512 B of the 1040-B fp32 row; a 528-B pitch keeps the same bank
+    // pattern for the fragment reads (4i mod 64) and lets the wide R = 8 form keep three A buffers
+    constexpr int LDA = BF ? 132 : r3::LDA;
+    constexpr int A_FLOATS = TR * LDA;
     const RowGemmP p = pb.p[blockIdx.y];
     static_assert(!PL || (X3 && !BF && !REC && !CW && ((AUX && NV == 0) || (!AUX && (NV == 1 || NV == 2)))),
                   "PL: split-mode sigma' backward or R <= 2 gathered forward");
