@@ -94,6 +94,23 @@ def _glorot_uniform(rng, shape):
     return rng.uniform(-lim, lim, shape)
 
 
+# Initialisation schemes.  TF's bits cannot be replayed, but the reference's seeding STRUCTURE can:
+# Keras 2.7's seeded initialisers (RandomNormal / RandomUniform with seed=...) run stateless ops keyed on
+# [seed, 0], so every seeded call draws the SAME stream, element i depending only on (seed, i).  All three
+# IDDGCN_Layers get seed=SEED (IDDGCN.py:238-274), hence in the reference
+#   relation_kernels = N[:R*D*D],  self_kernel = N[:D*D] (== relation_kernels[0]),  DistMult rel = N[:R*D]
+# for one normal stream N, identical in the three layers, while the unseeded initialisers (W_alpha
+# glorot_uniform, relation_weights 'uniform') draw fresh values per layer from the global seed.
+#   "stateless" (default): that structure, numpy's seeded streams standing in for Philox;
+#   "independent": every weight an independent draw from the layer's seeded generator (round 1).
+INIT_SCHEMES = ("stateless", "independent")
+
+
+def _normal_prefix(seed, n):
+    """The first n values of the seeded standard-normal stream (prefix-consistent, as a stateless op)."""
+    return np.random.default_rng([int(seed), 0]).standard_normal(n)
+
+
 class Layer:
     def __init__(self, name):
         self.name = name
@@ -114,9 +131,9 @@ class Layer:
 class Embedding(Layer):
     """Keras Embedding(input_dim=N, output_dim=D), RandomUniform(0, 1) init (IDDGCN.py:215-225)."""
 
-    def __init__(self, input_dim, output_dim, seed=None, name="entity_embeddings"):
+    def __init__(self, input_dim, output_dim, seed=None, name="entity_embeddings", init="stateless"):
         super().__init__(name)
-        rng = np.random.default_rng(seed)
+        rng = np.random.default_rng([int(seed), 1] if init == "stateless" and seed is not None else seed)
         self._weights = [rng.random((input_dim, output_dim)).astype(np.float32)]
 
 
@@ -126,17 +143,26 @@ class IDDGCN_Layer(Layer):
     ``relation_weights`` is created (it occupies a slot of the h5 layout) but,
     as in the reference, never used by ``call`` and never trained."""
 
-    def __init__(self, num_entities, num_relations, output_dim, seed, name="iddgcn__layer", **kwargs):
+    def __init__(self, num_entities, num_relations, output_dim, seed, name="iddgcn__layer", init="stateless",
+                 layer_index=0, **kwargs):
         super().__init__(kwargs.get("name", name))
         self.num_entities, self.num_relations, self.output_dim, self.seed = (num_entities, num_relations,
                                                                              output_dim, seed)
-        rng = np.random.default_rng(seed)
+        if init not in INIT_SCHEMES:
+            raise ValueError(f"init must be one of {INIT_SCHEMES}")
         R, D = num_relations, output_dim
-        K = rng.standard_normal((R, D, D))       # RandomNormal(0, 1) (:29)
-        S = rng.standard_normal((D, D))          # RandomNormal(0, 1) (:35)
+        if init == "stateless":
+            K = _normal_prefix(seed, R * D * D).reshape(R, D, D)     # RandomNormal(0, 1, seed) (:26-30)
+            S = _normal_prefix(seed, D * D).reshape(D, D)            # the same stream (:31-36): == K[0]
+            rng = np.random.default_rng([int(seed), 2, int(layer_index)])   # unseeded: fresh per layer
+        else:
+            rng = np.random.default_rng(seed)
+            K = rng.standard_normal((R, D, D))
+            S = rng.standard_normal((D, D))
         self._weights = [K.astype(np.float32), S.astype(np.float32),
-                         rng.uniform(-0.05, 0.05, (R,)).astype(np.float32),
-                         _glorot_uniform(rng, (D, R)).astype(np.float32), np.zeros((R,), np.float32)]
+                         rng.uniform(-0.05, 0.05, (R,)).astype(np.float32),       # 'uniform' (:39-44)
+                         _glorot_uniform(rng, (D, R)).astype(np.float32),          # glorot_uniform (:47-52)
+                         np.zeros((R,), np.float32)]
 
     def __call__(self, inputs, weights=None):
         """IDDGCN.py:60-79 on GPU tensors: inputs = [embeddings (N,D), head_idx (B,), head_e (B,D),
@@ -167,16 +193,20 @@ class IDDGCN_Layer(Layer):
 class DistMult(Layer):
     """IDDGCN.py:82-109: rel_embedding (R, D) ~ N(0,1); score = sigmoid(sum h*r*t), shape (1, B)."""
 
-    def __init__(self, num_relations, seed, name="DistMult", embedding_dim=None, **kwargs):
+    def __init__(self, num_relations, seed, name="DistMult", embedding_dim=None, init="stateless", **kwargs):
         super().__init__(name)
-        self.num_relations, self.seed = num_relations, seed
+        self.num_relations, self.seed, self.init = num_relations, seed, init
         self._weights = []
         if embedding_dim is not None:
             self.build(embedding_dim)
 
     def build(self, embedding_dim):
-        rng = np.random.default_rng(self.seed)
-        self._weights = [rng.standard_normal((self.num_relations, embedding_dim)).astype(np.float32)]
+        R, D = self.num_relations, embedding_dim
+        if self.init == "stateless":      # RandomNormal(0, 1, seed) (:90-99): the layers' stream, first R*D values
+            w = _normal_prefix(self.seed, R * D).reshape(R, D)
+        else:
+            w = np.random.default_rng(self.seed).standard_normal((R, D))
+        self._weights = [w.astype(np.float32)]
 
     def __call__(self, inputs, logits=False, rel_embedding=None):
         """sigmoid(sum head_e * rel[rel_idx] * tail_e) as (1, B), differentiable (autograd.DistMultFunction)
@@ -221,15 +251,15 @@ class IDDGCN_Model:
     """IDDGCN.py:112-178 (custom train_step) + get_IDDGCN_Model wiring (:201-285)."""
 
     def __init__(self, num_entities, num_relations, embedding_dim, output_dim, seed, mode=0, fold=0,
-                 neg_weight=1.0):
+                 neg_weight=1.0, init="stateless"):
         if embedding_dim != output_dim:
             raise ValueError("embedding_dim must equal output_dim (IDDGCN.py:307-308)")
         self.num_entities, self.num_relations, self.dim = num_entities, num_relations, embedding_dim
         self.seed, self.mode, self.fold, self.neg_weight = seed, mode, fold, neg_weight
-        self.entity_embeddings = Embedding(num_entities, embedding_dim, seed)
-        self.gcn_layers = [IDDGCN_Layer(num_entities, num_relations, output_dim, seed,
+        self.entity_embeddings = Embedding(num_entities, embedding_dim, seed, init=init)
+        self.gcn_layers = [IDDGCN_Layer(num_entities, num_relations, output_dim, seed, init=init, layer_index=i,
                                         name="iddgcn__layer" + ("" if i == 0 else f"_{i}")) for i in range(3)]
-        self.distmult = DistMult(num_relations, seed, embedding_dim=embedding_dim)
+        self.distmult = DistMult(num_relations, seed, embedding_dim=embedding_dim, init=init)
         self.layers = [self.entity_embeddings, *self.gcn_layers, self.distmult]
         self.neg_triples = None         # set to override the reference's .npy negatives
         self.neg_path_template = "../datasets/prediction_datasets/mode{mode}_fold{fold}_X_train_neg.npy"
@@ -444,7 +474,7 @@ class IDDGCN_Model:
 
 
 def get_IDDGCN_Model(num_entities, num_relations, embedding_dim, output_dim, seed, all_feature_matrix=None, mode=0,
-                     fold=0):
+                     fold=0, init="stateless"):
     """IDDGCN.py:201-285.  ``all_feature_matrix`` is accepted and unused, as in the
     reference (the Embedding's ``weights=`` argument is commented out, :219)."""
-    return IDDGCN_Model(num_entities, num_relations, embedding_dim, output_dim, seed, mode=mode, fold=fold)
+    return IDDGCN_Model(num_entities, num_relations, embedding_dim, output_dim, seed, mode=mode, fold=fold, init=init)

@@ -8,7 +8,8 @@ through the Keras-shaped API.  Fold data are the reference's bundled files (test
 TF's seeded initializers cannot be replayed, so each (fold, seed) starts from this package's seeded
 initialisation of the same distributions; the published-weights AUCs are the yardstick.
 
-usage: python tools/train_folds.py [--folds 0,1,2,3,4] [--seeds 89,1,2] [--epochs 5000] [--out FILE]
+usage: python tools/train_folds.py [--folds 0,1,2,3,4] [--seeds 89,1,2] [--epochs 5000] [--init stateless]
+                                  [--out FILE]
 """
 import argparse
 import json
@@ -33,9 +34,9 @@ N_ENT, N_REL, DIM = 845, 4, 64
 REFERENCE_WEIGHTS_AUC = {0: 0.9072, 1: 0.8841, 2: 0.8832, 3: 0.9148, 4: 0.9068}
 
 
-def run(fold, seed, epochs):
+def run(fold, seed, epochs, init="stateless"):
     d = np.load(os.path.join(ROOT, "tests", "golden", f"fold{fold}_data.npz"))
-    model = get_IDDGCN_Model(N_ENT, N_REL, DIM, DIM, seed, None, 0, fold)
+    model = get_IDDGCN_Model(N_ENT, N_REL, DIM, DIM, seed, None, 0, fold, init=init)
     model.neg_triples = d["X_train_neg"][None]
     model.compile(loss=BinaryCrossentropy(), optimizer=Adam(learning_rate=0.001))
     X = d["X_train"][None]
@@ -50,7 +51,7 @@ def run(fold, seed, epochs):
     y = np.concatenate([np.ones(len(d["X_test"])), np.zeros(len(d["neg_X_test"]))])
     p = model.predict(x=[np.arange(N_ENT)[None], Xt[:, :, 0], Xt[:, :, 1], Xt[:, :, 2], adj_eval])[0]
     prec, reca, _ = precision_recall_curve(y, p)
-    return {"fold": fold, "seed": seed, "epochs": epochs, "train_s": train_s,
+    return {"fold": fold, "seed": seed, "init": init, "epochs": epochs, "train_s": train_s,
             "ms_per_epoch": train_s / epochs * 1e3, "final_loss": hist.history["loss"][-1],
             "roc_auc": float(roc_auc_score(y, p)), "aupr": float(auc(reca, prec)),
             "accuracy": float(((p > 0.5) == (y > 0.5)).mean()), "reference_weights_auc_restated": REFERENCE_WEIGHTS_AUC[fold]}
@@ -62,11 +63,13 @@ def main():
     ap.add_argument("--seeds", default="89,1,2")
     ap.add_argument("--epochs", type=int, default=5000)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--init", default="stateless", choices=["stateless", "independent"],
+                    help="weight-initialisation scheme (iddgcn_amd.model.INIT_SCHEMES)")
     a = ap.parse_args()
     runs = []
     for fold in map(int, a.folds.split(",")):
         for seed in map(int, a.seeds.split(",")):
-            r = run(fold, seed, a.epochs)
+            r = run(fold, seed, a.epochs, a.init)
             runs.append(r)
             print(json.dumps(r), flush=True)
     summary = {}
