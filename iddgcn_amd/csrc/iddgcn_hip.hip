@@ -2611,7 +2611,10 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
     // D = 256 with many relations: one node per wave, its edge rows (and W rows) wave-uniform, the R
     // coefficients of an edge through scalar loads (R = 8: -39%; at R <= 2 the vector loads are faster)
-    constexpr bool SCALAR = SLOTS == 1 && R >= 4;
+#ifndef TS_PF_MINR
+#define TS_PF_MINR 4
+#endif
+    constexpr bool SCALAR = SLOTS == 1 && R >= TS_PF_MINR;
     if constexpr (SCALAR) {
         beg = __builtin_amdgcn_readfirstlane(beg);
         end = __builtin_amdgcn_readfirstlane(end);
