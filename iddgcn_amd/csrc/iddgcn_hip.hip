@@ -602,6 +602,9 @@ __global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi
 #ifndef V3_CAP2
 #define V3_CAP2 0
 #endif
+#ifndef V3_COEF16
+#define V3_COEF16 1
+#endif
 namespace r3 {
 constexpr int D = 256, NW = 8, TR = 32;
 constexpr int ROWS_PER_WAVE = TR / NW;                 // A rows each wave stages
@@ -927,7 +930,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     int* cmpw = idxw + r3::IDX;
     auto dma_slabs = [&](long long t) __attribute__((always_inline)) {
         if (V3_ABL & 1) return;
-        if (NV > 0) {
+        if (NV > 0 && !(V3_ABL & 256)) {
             int vi = 0;
             bool start = false;
             if (lane < 32) {
@@ -982,7 +985,16 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                 }
             }
         }
-        if (HAS_COEF) {
+        if (HAS_COEF && !(V3_ABL & 128) && COEF_WIDE && V3_COEF16 && (R == 4 || R == 8) && !p.coef_idx) {
+            // per-edge coefficients (no coef_idx): the tile's 32 x R values are one contiguous block, one
+            // 16-B DMA per lane (R = 8: 1 instruction instead of 4, and no per-lane q / R divisions); lanes
+            // past the array's end re-read its last 16 B (those rows are past M and never stored)
+            const long long last = (long long)(p.M - 1) * R + R - 4;
+            long long off = t * TR * R + 4 * lane;
+            if (off > last) off = last;
+            if (lane < 8 * R)
+                __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + off), (lds_vptr)coefw, 16, 0, 0);
+        } else if (HAS_COEF && !(V3_ABL & 128)) {
             // 32 x R coefficients, 64 per DMA instruction (R <= 2: one instruction)
             for (int k0 = 0; k0 < TR * R; k0 += 64) {
                 const float* g = p.coef;             // lanes past 32*R read a valid dummy
