@@ -28,6 +28,11 @@ SYMBOLS = {
               "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, false, false, false, false>",
               "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, false, true, false, false>",
               "tail_dS_tn": "gemm_tn256_dma_kernel"},
+    # the bf16-feature mode (config 5: R = 8 gathered relations, bf16 edge tables); recorded under the
+    # bench's gemm key ("split") with `python tools/pmc_traffic.py ... split synthetic-5 1 profiles/r02 bf16`
+    "bf16": {"tail_fwd_gemm": "rowgemm256_v3_kernel<8, false, true, true, false, false, true, false>",
+             "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, false, true, false>",
+             "tail_dS_tn": "gemm_tn256_bf16_kernel"},
 }
 
 
@@ -44,11 +49,11 @@ def edge_launches(df, sym):
     return k[k["dur_ms"] >= 0.5 * k["dur_ms"].max()]
 
 
-def main(fetch_dir, write_dir, gemm, workload, world, outdir):
+def main(fetch_dir, write_dir, gemm, workload, world, outdir, symset=None):
     f, w = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
     out_path = os.path.join(outdir, "pmc_traffic.json")
     rec = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    for name, sym in SYMBOLS[gemm].items():
+    for name, sym in SYMBOLS[symset or gemm].items():
         fe, we = edge_launches(f, sym), edge_launches(w, sym)
         if fe.empty or we.empty:
             continue
@@ -65,4 +70,5 @@ def main(fetch_dir, write_dir, gemm, workload, world, outdir):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6])
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6],
+         sys.argv[7] if len(sys.argv) > 7 else None)
