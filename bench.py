@@ -384,6 +384,11 @@ def main():
         except torch.OutOfMemoryError as e:      # a secondary workload never costs the headline line
             torch.cuda.empty_cache()
             o = {"config": {"workload": CONFIGS[cid]["name"]}, "error": f"out of memory: {e}"[:300]}
+        except Exception as e:                   # nor does any other failure of one (reported, not raised)
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            o = {"config": {"workload": CONFIGS[cid]["name"] + ("+relation-sharded" if shard == "relation" else "")},
+                 "error": f"{type(e).__name__}: {e}"[:300]}
         also.append(o)
     if also:
         result["also"] = also
