@@ -250,6 +250,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     comm = BucketedAllReduce() if world > 1 else None
     if shard == "relation" and world > 1:
         eng.node_shard = RelationShard(R, N)     # SURVEY §8(e) alternative: node tables split by relation
+    elif shard == "spmm" and world > 1:
+        eng.spmm_shard = RelationShard(R, N)     # row-partitioned SpMMs, node GEMMs replicated
 
     def timed_run(mode, probe):
         """W warm-up steps, then K timed steps between barriers + synchronize; max over ranks."""
@@ -283,7 +285,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
            "gemm_operands": GEMM_NOTE[gemm] + ("; edge GEMMs bf16 (features=bf16)" if feat == "bf16" else ""),
            "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
                       "scored_edges": T, "scored_edges_per_gpu": ed.T, "feat_dim": D,
-                      "parallelism": f"edge-dp{world}" + ("+relation-sharded-nodes" if eng.node_shard else ""),
+                      "parallelism": f"edge-dp{world}" + ("+relation-sharded-nodes" if eng.node_shard else "")
+                      + ("+row-partitioned-spmm" if eng.spmm_shard else ""),
                       "gemm": gemm, "features": feat},
            "scored_edges_per_s": T / (elapsed / steps), "loss": loss_val, "steps": steps, "warmup": warmup}
     if other_mode and feat == "f32":
@@ -314,13 +317,15 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--also", nargs="*", default=None,
                     help="further workloads timed in the same run (min(steps, 5) steps, 1 warm-up), reported "
-                         "under 'also': config ids, 'Nr' = config N with relation-sharded node tables; default "
-                         "4 5 (BASELINE configs 4 and 5), plus 4r with more than one GPU; none to skip")
+                         "under 'also': config ids, 'Nr' = config N with relation-sharded node tables, 'Ns' = "
+                         "with row-partitioned SpMMs; default 4 5 (BASELINE configs 4 and 5), plus 3s 4r with "
+                         "more than one GPU; none to skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-planes", action="store_true",
                     help="fp32 tail tables x^1, x^2 instead of the pre-split planes form (A/B)")
-    ap.add_argument("--shard", default="edge", choices=["edge", "relation"],
-                    help="multi-GPU: edge partitioning only (default) or also relation-sharded node tables")
+    ap.add_argument("--shard", default="edge", choices=["edge", "relation", "spmm"],
+                    help="multi-GPU: edge partitioning only (default), also relation-sharded node tables, or also "
+                         "row-partitioned SpMMs (A_r E all-gathered, dAE reduce-scattered; node GEMMs replicated)")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],
                     help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
     ap.add_argument("--gemm", default="split", choices=["split", "exact"],
@@ -372,10 +377,11 @@ def main():
     }
     result.update(main_out)
     also = []
-    todo = (["4", "5"] + (["4r"] if world > 1 else [])) if args.also is None else \
+    todo = (["4", "5"] + (["3s", "4r"] if world > 1 else [])) if args.also is None else \
         [a for a in args.also if a != "none"]
     for item in todo:
-        cid, shard = int(item.rstrip("r")), ("relation" if item.endswith("r") else "edge")
+        cid = int(item.rstrip("rs"))
+        shard = "relation" if item.endswith("r") else ("spmm" if item.endswith("s") else "edge")
         if cid == args.config and shard == args.shard:
             continue
         try:
@@ -387,7 +393,8 @@ def main():
         except Exception as e:                   # nor does any other failure of one (reported, not raised)
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
-            o = {"config": {"workload": CONFIGS[cid]["name"] + ("+relation-sharded" if shard == "relation" else "")},
+            o = {"config": {"workload": CONFIGS[cid]["name"] + {"relation": "+relation-sharded",
+                                                                "spmm": "+row-partitioned-spmm"}.get(shard, "")},
                  "error": f"{type(e).__name__}: {e}"[:300]}
         also.append(o)
     if also:

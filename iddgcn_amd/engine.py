@@ -299,12 +299,23 @@ class Engine:
 
     # -- forward ------------------------------------------------------------
     node_shard = None      # parallel.RelationShard: per-relation node tables split over the ranks
+    # parallel.RelationShard used for the two SpMMs only (node GEMMs replicated): A_r·E row-partitioned and
+    # all-gathered, dAE reduce-scattered to the row owners before a transposed SpMM over their columns
+    spmm_shard = None
 
     def forward(self, P, adj, ed, ws, train):
         N, R, D, T = self.N, self.R, self.D, ed.T
         E = P["E"]
         sh = self.node_shard
-        if sh is None:
+        if sh is None and self.spmm_shard is not None:
+            # row-partitioned A_r·E (every rank holds E): this rank's (relation, row) pieces, then all-gather
+            ss = self.spmm_shard
+            for r, n0, n1 in ss.pieces():
+                ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + n0:r * (N + 1) + n1 + 1], adj.fwd_col, adj.fwd_val, E,
+                             ws.AE[r][n0:n1].view(1, n1 - n0, D), 1, n1 - n0)
+            ss.all_gather(ws.AE.view(R * N, D))
+            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], {}) for l in range(NUM_LAYERS) for r in range(R)]
+        elif sh is None:
             # AE_r = A_r·E, all relations in one launch (IDDGCN.py:69-70)
             ops.spmm_csr(adj.fwd_ptr, adj.fwd_col, adj.fwd_val, E, ws.AE, R, N)
             # P_r^l = AE_r·K_r^l (node-level form of IDDGCN.py:71-72,76-77) and, layer 1, x·S1 at node
@@ -439,9 +450,15 @@ class Engine:
             comm.ready(G.buf[N * D:])
         # dE += sum_r A_r^T dAE_r  (gradient through all_e -> sparse_dense_matmul); per-row sums, so a
         # row-chunked launch sequence is bitwise the single launch
+        bptr, bcol, bval = adj.bwd_ptr, adj.bwd_col, adj.bwd_val
+        if self.spmm_shard is not None and self.node_shard is None:
+            # the owners of dAE's (relation, row) range get its sums over the ranks; each rank's transposed
+            # SpMM runs over the entries in its range only, and dE's all-reduce below adds the ranks' parts
+            self.spmm_shard.reduce_scatter(ws.dAE.view(R * N, D))
+            bptr, bcol, bval = adj.bwd_columns(self.spmm_shard.a, self.spmm_shard.b)
         chunks = comm.row_chunks(N) if comm is not None else [(0, N)]
         for n0, n1 in chunks:
-            ops.spmm_csr(adj.bwd_ptr[n0:n1 + 1], adj.bwd_col, adj.bwd_val, ws.dAE.view(R * N, D),
+            ops.spmm_csr(bptr[n0:n1 + 1], bcol, bval, ws.dAE.view(R * N, D),
                          G["E"][n0:n1].view(1, n1 - n0, D), 1, n1 - n0, accumulate=True)
             if comm is not None:
                 comm.ready(G["E"][n0:n1].reshape(-1))

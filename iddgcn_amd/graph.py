@@ -206,6 +206,28 @@ class DeviceAdjacency:
         self.fwd_val = v[self.fwd_src].contiguous()
         self.bwd_val = v[self.bwd_src].contiguous()
 
+    def bwd_columns(self, a, b):
+        """The merged transposed CSR restricted to the entries whose column (flat relation-row r*N + i of
+        dAE) lies in [a, b): (ptr, col, val) with every row's entries in their original order.  The
+        row-partitioned transposed SpMM of data parallelism (Engine.spmm_shard) runs over it; cached per
+        range (values refreshed by set_values are re-filtered)."""
+        key = (int(a), int(b))
+        cached = getattr(self, "_bwd_cols", None)
+        if cached is not None and cached[0] == key and cached[1] is self.bwd_val:
+            return cached[2]
+        N = self.num_entities
+        col = self.bwd_col.long()
+        keep = (col >= a) & (col < b)
+        rows = torch.repeat_interleave(torch.arange(N, device=col.device),
+                                       (self.bwd_ptr[1:] - self.bwd_ptr[:-1]).long())
+        counts = torch.bincount(rows[keep], minlength=N)
+        ptr = torch.zeros(N + 1, dtype=torch.int32, device=col.device)
+        ptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+        out = (ptr, self.bwd_col[keep].contiguous(),
+               None if self.bwd_val is None else self.bwd_val[keep].contiguous())
+        self._bwd_cols = (key, self.bwd_val, out)
+        return out
+
     def to_entry_order(self, csr_vals):
         """Per-entry quantity in forward-CSR order -> list of per-relation tensors in entry order."""
         flat = csr_vals[self.fwd_pos]

@@ -137,6 +137,8 @@ def _step_worker(rank, world, port, q, mode, N, R, D):
         eng = Engine(N, R, D, dev)
         if mode == "relation":
             eng.node_shard = RelationShard(R, N)
+        elif mode == "spmm":
+            eng.spmm_shard = RelationShard(R, N)
         P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
         P.load(_mild(N, R, D, 9))
         adj = eng.adjacency(get_adj_mats(pos, N, R))
@@ -157,9 +159,11 @@ def _step_worker(rank, world, port, q, mode, N, R, D):
 @pytest.mark.parametrize("N,R,D", [(600, 2, 64), (601, 3, 256)])
 def test_relation_sharded_step_equals_full_batch(N, R, D, cuda):
     """SURVEY §8(e)'s relation-sharded alternative (RelationShard: per-relation node tables split over the
-    ranks by (relation, row), all-gather of P^l, reduce-scatter of dP^l), 2 ranks on one GPU over gloo:
-    the step's loss and every gradient equal the single-process full batch and the edge-partitioned
-    2-rank step (1e-5 of max|g|).  (601, 3): R*N not divisible by the world size (padded collectives)."""
+    ranks by (relation, row), all-gather of P^l, reduce-scatter of dP^l) and the row-partitioned SpMMs
+    (Engine.spmm_shard: A_r E all-gathered, dAE reduce-scattered, the transposed SpMM over each rank's
+    columns via DeviceAdjacency.bwd_columns), 2 ranks on one GPU over gloo: the step's loss and every
+    gradient equal the single-process full batch and the edge-partitioned 2-rank step (1e-5 of max|g|).
+    (601, 3): R*N not divisible by the world size (padded collectives)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     pos, neg = synthetic_graph(N, R, 9000, seed=77)
@@ -172,7 +176,7 @@ def test_relation_sharded_step_equals_full_batch(N, R, D, cuda):
     full, full_loss = G.to_numpy(), float(loss.item())
     del eng, P, G
     res = {}
-    for mode in ("edge", "relation"):
+    for mode in ("edge", "relation", "spmm"):
         port = _free_port()
         procs = [ctx.Process(target=_step_worker, args=(r, 2, port, q, mode, N, R, D)) for r in range(2)]
         for p in procs:
@@ -188,3 +192,27 @@ def test_relation_sharded_step_equals_full_batch(N, R, D, cuda):
         assert abs(l - full_loss) <= 1e-6 * full_loss, mode
         for k, v in full.items():
             assert np.abs(g[k] - v).max() <= 1e-5 * np.abs(v).max() + 1e-30, (mode, k)
+
+
+def test_bwd_columns_partition_sums_to_full(cuda):
+    """DeviceAdjacency.bwd_columns: the per-range restrictions of the merged transposed CSR partition its
+    entries (each row's entries in the original order), so the transposed SpMMs over them sum to the full
+    one — bitwise per range where a row's entries all fall in one range."""
+    from iddgcn_amd import ops
+    N, R, D = 700, 3, 64
+    pos, _ = synthetic_graph(N, R, 8000, seed=5)
+    adj = Engine(N, R, D, cuda).adjacency(get_adj_mats(pos, N, R))
+    dAE = torch.randn(R * N, D, device=cuda)
+    full = torch.zeros(1, N, D, device=cuda)
+    ops.spmm_csr(adj.bwd_ptr, adj.bwd_col, adj.bwd_val, dAE, full, 1, N)
+    bounds = [0, 500, 1400, R * N]
+    acc = torch.zeros(1, N, D, device=cuda)
+    nnz = 0
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        ptr, col, val = adj.bwd_columns(a, b)
+        assert int(ptr[-1]) == col.numel() and bool(((col >= a) & (col < b)).all())
+        nnz += col.numel()
+        ops.spmm_csr(ptr, col, val, dAE, acc, 1, N, accumulate=True)
+    assert nnz == adj.bwd_col.numel()
+    torch.cuda.synchronize()
+    assert (acc - full).abs().max().item() <= 1e-5 * full.abs().max().item()
