@@ -2905,7 +2905,10 @@ __global__ __launch_bounds__(1024) void reduce_slabs_split_kernel(int n_slabs, l
 }
 void launch_reduce_slabs(hipStream_t st, int n_slabs, long long n, const float* slab, float* out, int accumulate,
                          float scale) {
-    if (n % 4 == 0 && n_slabs >= 8 && (reinterpret_cast<uintptr_t>(slab) & 15) == 0) {
+    // the float4 form gives one 64-output block per 256 threads: below ~64 blocks (e.g. DistMult's R x D drel
+    // partials, 2 blocks summing 2048 slabs in 43 us) the 16-wave split form spreads the slabs wider
+    const bool few_blocks = n / 4 < 64 * 64 && n_slabs >= 64;
+    if (n % 4 == 0 && n_slabs >= 8 && !few_blocks && (reinterpret_cast<uintptr_t>(slab) & 15) == 0) {
         const long long n4 = n / 4;
         hipLaunchKernelGGL(reduce_slabs4_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st, n_slabs, n4,
                            reinterpret_cast<const f32x4*>(slab), out, accumulate, scale);
