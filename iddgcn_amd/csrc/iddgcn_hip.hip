@@ -365,14 +365,28 @@ __global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmBatch pb
                 const long long ci = p.coef_idx ? (long long)p.coef_idx[e] : e;
                 const long long vi = p.v_idx ? (long long)p.v_idx[e] : e;
                 const float* vb = p.V + vi * p.v_row_stride + c;
-                if (p.act == IDDGCN_ACT_DSIGMOID_COMBINE) {
+                // every coefficient and V value of the row is loaded before the first fma (a compile-time
+                // bounded, guarded loop instead of a run-time trip count that waited on each pair in turn)
+                float cfv[MAX_R], vv[MAX_R + 1];
+                const bool comb = p.act == IDDGCN_ACT_DSIGMOID_COMBINE;
+#pragma unroll
+                for (int r = 0; r < MAX_R; ++r) {
+                    cfv[r] = r < p.R ? p.coef[ci * p.R + r] : 0.f;
+                    vv[r] = r < p.R + (comb ? 1 : 0) ? vb[r * p.v_rel_stride] : 0.f;
+                }
+                vv[MAX_R] = comb && p.R == MAX_R ? vb[MAX_R * p.v_rel_stride] : 0.f;
+                if (comb) {
                     // x = sigmoid(V_0 + sum_r coef_r V_{r+1}): the same arithmetic as combine_kernel
-                    float xs = vb[0];
-                    for (int r = 0; r < p.R; ++r) xs = fmaf(p.coef[ci * p.R + r], vb[(r + 1) * p.v_rel_stride], xs);
+                    float xs = vv[0];
+#pragma unroll
+                    for (int r = 0; r < MAX_R; ++r)
+                        if (r < p.R) xs = fmaf(cfv[r], vv[r + 1], xs);
                     const float x = sigmoid_fast(xs);
                     v = v * (x * (1.0f - x));
                 } else {
-                    for (int r = 0; r < p.R; ++r) v = fmaf(p.coef[ci * p.R + r], vb[r * p.v_rel_stride], v);
+#pragma unroll
+                    for (int r = 0; r < MAX_R; ++r)
+                        if (r < p.R) v = fmaf(cfv[r], vv[r], v);
                 }
             }
             if (p.act == IDDGCN_ACT_SIGMOID) {
