@@ -2610,7 +2610,8 @@ __global__ __launch_bounds__(256) void seg_gather_reduce_kernel(int n_nodes, con
 // One node per group of D/4 lanes; the node's edges are contiguous rows of dO,
 // walked 4 at a time with all 4 row loads (and their W[h] loads) issued before
 // any use, so each wave keeps 4 KiB in flight.  R is a template parameter so
-// the per-relation state stays in a handful of registers (occupancy 8).
+// the per-relation state stays in a handful of registers (R = 2: 76 VGPRs, 6 waves per SIMD;
+// forcing 7 or 8 waves is slower, profiles/r02/ablations/tail_seg_depth_ab.txt).
 // D < 256: a node gets the whole wave, 64 / (D/4) edge SLOTS of D/4 lanes each walking every
 // SLOTS-th group of U edges (graphs with few nodes, e.g. the reference's 845, would otherwise
 // leave most of the chip idle behind a few long serial segments); the slot partials are summed
