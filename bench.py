@@ -39,10 +39,10 @@ MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md, f32-input MFMA dense pea
 MFMA_F16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md, bf16/f16 MFMA dense peak (16x the f32 rate)
 HBM_PEAK_GBS = 8000.0
 GEMM_NOTE = {
-    "split": "D=256 GEMM operands split hi+lo fp16 (22 significant bits, power-of-two row/column scales), "
-             "3 f16 MFMAs per k-step, fp32 accumulation; every other kernel exact f32 "
-             "(include/iddgcn.h iddgcn_set_gemm_precision)",
-    "exact": "exact f32 MFMA (v_mfma_f32_32x32x2_f32, bitwise an fmaf chain) everywhere",
+    "split": "opt-in mode: D=256 GEMM operands split hi+lo fp16 (22-23 significant bits, power-of-two row/column "
+             "scales), 3 f16 MFMAs per k-step, fp32 accumulation; every other kernel exact f32 "
+             "(include/iddgcn.h IDDGCN_GEMM_SPLIT_F16, per call)",
+    "exact": "exact f32 MFMA (v_mfma_f32_32x32x2_f32, bitwise an fmaf chain) for every GEMM, exact f32 elsewhere",
 }
 # the arithmetic the path computes in, per GEMM mode (the bench line's "dtype")
 DTYPE = {"split": "f32 (D=256 GEMMs on split-fp16x2 operands, fp32 accumulate)", "exact": "f32"}
@@ -53,7 +53,7 @@ CONFIGS = {
     2: dict(name="synthetic-fold0-shape", N=845, R=4, M=37_510, D=64, scaling="weak"),
     3: dict(name="synthetic-3", N=100_000, R=2, M=2_000_000, D=256, scaling="weak"),
     4: dict(name="synthetic-4", N=1_000_000, R=2, M=20_000_000, D=256, scaling="strong"),
-    # 40M positives, 10M negatives (one per 4 positives)
+    # 40M positives, 10M negatives (one per 4 positives), generated on the device
     5: dict(name="synthetic-5", N=1_000_000, R=8, M=40_000_000, D=256, scaling="strong", neg_every=4,
             features="bf16"),
 }
@@ -155,6 +155,22 @@ def pmc_traffic(kernel, gemm, workload, world):
     return None, None
 
 
+def workload_bytes(cid, world, features):
+    """Upper estimate of one rank's device memory for a workload (engine.Workspace, graph, parameters with
+    gradients and Adam moments, + the device graph build's sort buffers), for the multi-rank fit check."""
+    cfg = CONFIGS[cid]
+    N, R, D = cfg["N"], cfg["R"], cfg["D"]
+    M = cfg["M"] * (world if cfg["scaling"] == "weak" else 1)
+    T = M + M // cfg.get("neg_every", 1)
+    Tr = -(-T // world)
+    eb = 2 if features == "bf16" else 4
+    edge = 3 * Tr * D * eb + Tr * (4 * 4 + 8 + 4 + 4 * 4 * R + 8)
+    node = 4 * N * D * (6 * R + 7) + 4 * N * R * 8
+    params = 4 * 4 * (N * D + 3 * (R + 1) * D * D + R * D)
+    graph = 32 * M + 40 * T
+    return int(1.15 * (edge + node + params + graph)) + (2 << 30)
+
+
 def reference_init(np, N, R, D, seed):
     """Reference-distribution init (IDDGCN.py:25-58, 92-101, 221-224)."""
     rng = np.random.default_rng(seed)
@@ -169,24 +185,25 @@ def reference_init(np, N, R, D, seed):
     return p
 
 
-def cpu_baseline(cfg, budget_s=25.0):
+def cpu_baseline(cfg, frac=0.1, budget_s=30.0):
     """The reference formulation on the host cores (one full step: pos + neg forward, autograd backward,
-    Keras Adam), on a bounded sample of the same workload."""
+    Keras Adam), on a bounded sample of the same workload: the same N, D, R and a `frac` share of its
+    adjacency edges (and as many negatives).  The reference formulation's cost is linear in the edges
+    (per-edge GEMMs, SpMM per layer), so edges/s on the sample is the full step's rate."""
     import numpy as np
     import torch
     from oracle.ref_model import KerasAdam, adj_to_torch, keras_bce, model_forward, to_torch_params
     from oracle.ref_utils import get_adj_coo
     from iddgcn_amd.utils import synthetic_graph
     N, R, D = cfg["N"], cfg["R"], cfg["D"]
-    M_s = 40_000 if cfg["M"] > 40_000 else cfg["M"]
-    pos, neg = synthetic_graph(N, R, M_s, seed=11)
-    params = {k: v for k, v in reference_init(np, N, R, D, 89).items()}
-    adj = adj_to_torch(get_adj_coo(pos, N, R), N, torch.float32)
-    opt = KerasAdam()
     threads = torch.get_num_threads()
 
-    def step():
-        nonlocal params
+    def make(M_s):
+        pos, neg = synthetic_graph(N, R, M_s, seed=11)
+        params = {k: v for k, v in reference_init(np, N, R, D, 89).items()}
+        return pos, neg, params, adj_to_torch(get_adj_coo(pos, N, R), N, torch.float32), KerasAdam()
+
+    def step(pos, neg, params, adj, opt):
         P = to_torch_params(params, torch.float32)
         y_pos = model_forward(P, pos[:, 0], pos[:, 1], pos[:, 2], adj)
         y_neg = model_forward(P, neg[:, 0], neg[:, 1], neg[:, 2], adj)
@@ -194,23 +211,26 @@ def cpu_baseline(cfg, budget_s=25.0):
         loss = keras_bce(torch.cat([torch.ones_like(y_pos), torch.zeros_like(y_neg)]), y) / N
         keys = [k for k in P if P[k].requires_grad]
         grads = torch.autograd.grad(loss, [P[k] for k in keys])
-        params = opt.step(params, {k: g.numpy() for k, g in zip(keys, grads)}, dtype=np.float32)
+        return opt.step(params, {k: g.numpy() for k, g in zip(keys, grads)}, dtype=np.float32)
 
-    t0 = time.perf_counter()
-    step()
-    first = time.perf_counter() - t0
+    M_s = max(1, int(round(cfg["M"] * frac)))
+    # warm-up (thread pool, allocator) on a 2% graph, then the timed steps on the frac sample
+    step(*make(max(1, min(M_s, int(cfg["M"] * 0.02)))))
+    pos, neg, params, adj, opt = make(M_s)
     times = []
-    n = max(1, min(3, int(budget_s / max(first, 1e-3))))
-    for _ in range(n):
+    while True:
         t0 = time.perf_counter()
-        step()
+        params = step(pos, neg, params, adj, opt)
         times.append(time.perf_counter() - t0)
+        if len(times) >= 3 or sum(times) + times[-1] > budget_s:
+            break
     t = statistics.median(times)
     return {"value": M_s / t, "unit": "adjacency edges/s", "cores": threads, "kind": "port",
+            "fraction_of_workload": M_s / cfg["M"],
             "sample": (f"oracle/ref_model.py reference formulation (torch-CPU fp32: per-edge GEMMs, A_r.E per layer, "
-                       f"Keras BCE, autograd backward, Keras Adam), N={N} D={D} R={R}, M={M_s} edges + {M_s} "
-                       f"negatives (bounded sample of the workload); median of {n} steps after 1 warm-up, "
-                       f"{t:.2f} s/step")}
+                       f"Keras BCE, autograd backward, Keras Adam), N={N} D={D} R={R}, {M_s} of the workload's "
+                       f"{cfg['M']} adjacency edges ({100 * M_s / cfg['M']:.0f}%) + {M_s} negatives; median of "
+                       f"{len(times)} step(s) after a warm-up step, {t:.2f} s/step")}
 
 
 def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=True, shard=None, steps=None,
@@ -232,7 +252,11 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     weak = cfg["scaling"] == "weak"
     M = cfg["M"] * world if weak else cfg["M"]            # weak: per-GPU work fixed
     pos, neg = synthetic_graph(N, R, M, seed=0)           # identical on every rank (seeded)
-    neg = neg[::cfg.get("neg_every", 1)]
+    if cfg.get("neg_every", 1) > 1:
+        # one negative per neg_every positives, drawn ON THE DEVICE with the reference's recipe
+        # (utils1.py:646-655, MT19937 stream bit-exact to numpy's, csrc/sampling.hip)
+        from iddgcn_amd.sampling import negative_samples
+        neg = negative_samples(pos[::cfg["neg_every"]], N, 89, device=dev)
     T = len(pos) + len(neg)
     lo, hi = shard_range(T, rank, world)                  # this rank's contiguous shard (pos ++ neg)
     npos = len(pos)
@@ -240,8 +264,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     lab = np.concatenate([np.ones(max(0, min(hi, npos) - lo), np.float32),
                           np.zeros(max(0, hi - max(lo, npos)), np.float32)])
     feat = args.features or cfg.get("features", "f32")
-    eng = Engine(N, R, D, dev, gemm=gemm, recompute_x1=args.recompute_x1, fuse_tail_seg=args.fuse_tail_seg,
-                 features=feat, planes=not args.no_planes)
+    eng = Engine(N, R, D, dev, gemm=gemm, features=feat, planes=not args.no_planes)
     adj = get_adj_mats(pos, N, R, device=dev)            # device graph build (bit-identical to the host's)
     ed = eng.edges(tri, lab)
     del pos, neg, tri, lab
@@ -279,7 +302,20 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         probe_out, eng.probe = eng.probe, None
         return elapsed, float(loss.item()) / T, probe_out
 
+    def rank_consistency():
+        """After the timed steps: the largest |params - rank 0's params| over all ranks (0.0 when every rank
+        holds bitwise the same parameters, as the replicated Adam on all-reduced gradients must)."""
+        ref = P.buf.clone()
+        dist.broadcast(ref, 0)
+        d = (P.buf - ref).abs().max().reshape(1)
+        if dist.get_backend() != "nccl":
+            d = d.cpu()
+        dist.all_reduce(d, op=dist.ReduceOp.MAX)
+        del ref
+        return float(d.item())
+
     elapsed, loss_val, probe = timed_run(gemm, probe_kernels)
+    consist = rank_consistency() if world > 1 else None
     out = {"value": M / (elapsed / steps), "ms_per_step": elapsed / steps * 1e3,
            "scaling": cfg["scaling"], "dtype": DTYPE_BF16 if feat == "bf16" else DTYPE[gemm],
            "gemm_operands": GEMM_NOTE[gemm] + ("; edge GEMMs bf16 (features=bf16)" if feat == "bf16" else ""),
@@ -289,6 +325,9 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
                       + ("+row-partitioned-spmm" if eng.spmm_shard else ""),
                       "gemm": gemm, "features": feat},
            "scored_edges_per_s": T / (elapsed / steps), "loss": loss_val, "steps": steps, "warmup": warmup}
+    if world > 1:
+        out["ranks_consistent"] = consist == 0.0
+        out["params_max_abs_diff_vs_rank0"] = consist
     if other_mode and feat == "f32":
         mode2 = "exact" if gemm == "split" else "split"
         el2, loss2, _ = timed_run(mode2, False)
@@ -328,13 +367,10 @@ def main():
                          "row-partitioned SpMMs (A_r E all-gathered, dAE reduce-scattered; node GEMMs replicated)")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],
                     help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
-    ap.add_argument("--gemm", default="split", choices=["split", "exact"],
-                    help="operand precision of the D=256 MFMA GEMMs (the other mode is timed too)")
+    ap.add_argument("--gemm", default="exact", choices=["exact", "split"],
+                    help="operand precision of the D=256 MFMA GEMMs: exact f32 (the reference's arithmetic, the "
+                         "headline) or the opt-in split-fp16 operands (timed too, under other_gemm_mode)")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")
-    ap.add_argument("--fuse-tail-seg", action="store_true",
-                    help="layers 2-3: tail segmented reduction fused into the dS pass (A/B)")
-    ap.add_argument("--recompute-x1", action="store_true",
-                    help="layer-2 backward rebuilds x^1 on chip instead of re-reading it (A/B)")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
@@ -376,6 +412,9 @@ def main():
         "config": main_out.pop("config"),
     }
     result.update(main_out)
+    if world > 1:
+        result["world"] = world
+        result["backend"] = dist.get_backend()
     also = []
     todo = (["4", "5"] + (["3s", "4r"] if world > 1 else [])) if args.also is None else \
         [a for a in args.also if a != "none"]
@@ -384,18 +423,32 @@ def main():
         shard = "relation" if item.endswith("r") else ("spmm" if item.endswith("s") else "edge")
         if cid == args.config and shard == args.shard:
             continue
+        name = CONFIGS[cid]["name"] + {"relation": "+relation-sharded", "spmm": "+row-partitioned-spmm"}.get(shard, "")
+        if world > 1:
+            # ranks decide TOGETHER whether the workload fits (a rank that ran out of memory alone would leave the
+            # others waiting in a collective), then run it without recovery: any failure ends every rank
+            torch.cuda.empty_cache()
+            need = workload_bytes(cid, world, args.features or CONFIGS[cid].get("features", "f32"))
+            fits = torch.tensor([1.0 if torch.cuda.mem_get_info(dev)[0] >= need else 0.0], device=dev)
+            if dist.get_backend() != "nccl":
+                fits = fits.cpu()
+            dist.all_reduce(fits, op=dist.ReduceOp.MIN)
+            if fits.item() < 1.0:
+                also.append({"config": {"workload": name}, "skipped": f"does not fit every rank ({need / 2**30:.0f} GiB)"})
+                continue
+            also.append(run_workload(cid, args, world, rank, dev, args.gemm, False, shard=shard,
+                                     steps=min(args.steps, 5), warmup=1))
+            continue
         try:
             o = run_workload(cid, args, world, rank, dev, args.gemm, False, shard=shard,
                              steps=min(args.steps, 5), warmup=1)
-        except torch.OutOfMemoryError as e:      # a secondary workload never costs the headline line
+        except torch.OutOfMemoryError as e:      # one process: a secondary workload never costs the headline line
             torch.cuda.empty_cache()
-            o = {"config": {"workload": CONFIGS[cid]["name"]}, "error": f"out of memory: {e}"[:300]}
+            o = {"config": {"workload": name}, "error": f"out of memory: {e}"[:300]}
         except Exception as e:                   # nor does any other failure of one (reported, not raised)
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
-            o = {"config": {"workload": CONFIGS[cid]["name"] + {"relation": "+relation-sharded",
-                                                                "spmm": "+row-partitioned-spmm"}.get(shard, "")},
-                 "error": f"{type(e).__name__}: {e}"[:300]}
+            o = {"config": {"workload": name}, "error": f"{type(e).__name__}: {e}"[:300]}
         also.append(o)
     if also:
         result["also"] = also

@@ -12,9 +12,9 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 5
+ABI_VERSION = 6
 
-ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID, ACT_DSIGMOID_COMBINE = 0, 1, 2, 3
+ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
 GEMM_EXACT_F32, GEMM_SPLIT_F16 = 0, 1
 PLANES_A, PLANES_C, PLANES_AUX = 1, 2, 4          # iddgcn_rowgemm_t.planes (pre-split edge tables, ABI 4)
 
@@ -36,8 +36,8 @@ class RowGemmArgs(ctypes.Structure):
         ("V", vp), ("v_idx", vp),
         ("v_rel_stride", cll), ("v_row_stride", cll),
         ("act", ci), ("aux", vp),
-        ("v_runs_max", ci),
         ("planes", ci),
+        ("precision", ci),     # ABI 6: GEMM operand precision per call (GEMM_EXACT_F32 / GEMM_SPLIT_F16)
     ]
 
 
@@ -55,15 +55,12 @@ SIGNATURES = {
     "iddgcn_spmm_csr_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, ci]),
     "iddgcn_sddmm_csr_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
     "iddgcn_rowgemm_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
-    "iddgcn_set_rowgemm_path": (ci, [ci]),
-    "iddgcn_set_gemm_precision": (ci, [ci]),
     "iddgcn_gemm_tn_blocks": (ci, [cll, ci]),
-    "iddgcn_gemm_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
+    "iddgcn_gemm_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci, ci]),
     "iddgcn_rowgemm_batched_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs), ci]),
     "iddgcn_rowgemm_kernel_id": (ci, [ctypes.POINTER(RowGemmArgs)]),
     "iddgcn_adam_table_f32": (ci, [vp, cll, vp, vp, vp, vp, vp, vp, cf, cf, cf, ci]),
     "iddgcn_step_advance": (ci, [vp, vp, vp, vp]),
-    "iddgcn_gemm_tn_seg_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci, vp, vp, ci, vp, vp, cll, vp, vp, ci]),
     "iddgcn_gemm_tn_narrow_blocks": (ci, [cll]),
     "iddgcn_gemm_tn_narrow_f32": (ci, [vp, cll, ci, ci, vp, vp, vp, ci, vp, vp, ci]),
     "iddgcn_alpha_fwd_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp]),
@@ -84,7 +81,7 @@ SIGNATURES = {
     "iddgcn_combine_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_combine_planes_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_gemm_tn_planes_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
-    "iddgcn_gemm_tn_batched_f32": (ci, [vp, ci, ctypes.POINTER(TnArgs), ci, vp, cll]),
+    "iddgcn_gemm_tn_batched_f32": (ci, [vp, ci, ctypes.POINTER(TnArgs), ci, vp, cll, ci]),
     "iddgcn_distmult_bce_bf16": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp, ci]),
     "iddgcn_distmult_bce_heads_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
                                             vp, ci]),

@@ -169,12 +169,6 @@ inline int launch_status() {
     return e == hipSuccess ? 0 : (int)e;
 }
 inline bool dim_ok(int d) { return d == 32 || d == 64 || d == 128 || d == 256; }
-// test/bench hook selecting the D=256 GEMM pipelines: 0 = best (v3 row GEMM, DMA TN),
-// 1 = register-staged kernels, 2 = v2 DMA row GEMM
-static int g_rowgemm_path = 0;
-// D=256 GEMM operand precision: 0 = exact f32 MFMA (bitwise an fmaf chain), 1 = split-fp16
-// operands (hi + lo*2^-11 per value, 3 f16 MFMAs per k-step, fp32 accumulation)
-static int g_gemm_split = 0;
 
 // ---------------------------------------------------------------------------
 // CSR SpMM: one row per group of D/4 lanes, sequential sum in CSR order.
@@ -284,8 +278,8 @@ struct RowGemmP {
     const float* V; const int* v_idx;
     long long v_rel_stride, v_row_stride;
     int act; const float* aux;
-    int v_runs_max;
     int planes;           // IDDGCN_PLANES_A | _C | _AUX (D = 256 split mode, v3 kernel only)
+    int precision;        // IDDGCN_GEMM_* of this call (D = 256 v3 kernels; every other GEMM is exact f32)
     int tiles_per_block;
 };
 
@@ -367,27 +361,15 @@ __global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmBatch pb
                 const float* vb = p.V + vi * p.v_row_stride + c;
                 // every coefficient and V value of the row is loaded before the first fma (a compile-time
                 // bounded, guarded loop instead of a run-time trip count that waited on each pair in turn)
-                float cfv[MAX_R], vv[MAX_R + 1];
-                const bool comb = p.act == IDDGCN_ACT_DSIGMOID_COMBINE;
+                float cfv[MAX_R], vv[MAX_R];
 #pragma unroll
                 for (int r = 0; r < MAX_R; ++r) {
                     cfv[r] = r < p.R ? p.coef[ci * p.R + r] : 0.f;
-                    vv[r] = r < p.R + (comb ? 1 : 0) ? vb[r * p.v_rel_stride] : 0.f;
+                    vv[r] = r < p.R ? vb[r * p.v_rel_stride] : 0.f;
                 }
-                vv[MAX_R] = comb && p.R == MAX_R ? vb[MAX_R * p.v_rel_stride] : 0.f;
-                if (comb) {
-                    // x = sigmoid(V_0 + sum_r coef_r V_{r+1}): the same arithmetic as combine_kernel
-                    float xs = vv[0];
 #pragma unroll
-                    for (int r = 0; r < MAX_R; ++r)
-                        if (r < p.R) xs = fmaf(cfv[r], vv[r + 1], xs);
-                    const float x = sigmoid_fast(xs);
-                    v = v * (x * (1.0f - x));
-                } else {
-#pragma unroll
-                    for (int r = 0; r < MAX_R; ++r)
-                        if (r < p.R) v = fmaf(cfv[r], vv[r], v);
-                }
+                for (int r = 0; r < MAX_R; ++r)
+                    if (r < p.R) v = fmaf(cfv[r], vv[r], v);
             }
             if (p.act == IDDGCN_ACT_SIGMOID) {
                 v = sigmoid_fast(v);
@@ -400,29 +382,7 @@ __global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmBatch pb
     }
 }
 
-// ---------------------------------------------------------------------------
-// Row GEMM, D = 256, pipelined with LDS-DMA (global_load_lds_dwordx4).
-//   One persistent 512-thread workgroup per CU walks a contiguous range of
-//   32-row tiles.  Per tile, BEFORE the 128 MFMAs of each wave are issued:
-//     - the next tile's A rows are DMA'd into the other half of a double buffer,
-//     - this tile's epilogue operand rows (R gathered P_r[v_idx[e]] rows, or the
-//       sigma' aux rows) are DMA'd into the epilogue buffer,
-//     - this tile's per-row coefficients are loaded into registers,
-//     - the row indices of the next tile are loaded,
-//   so the memory latency hides under the MFMA phase; the epilogue then reads
-//   LDS only.  One wave-instruction moves exactly one 1 KiB row, so LDS rows can
-//   be padded to 1040 B (conflict-free ds_read_b128 of the A fragments).
-//   All LDS lives in ONE __shared__ array (separate arrays make hipcc drain vmcnt).
-// ---------------------------------------------------------------------------
-namespace r256 {
-constexpr int D = 256, NW = 8, TR = 32, LDA = D + 4;
-constexpr int ROWS_PER_WAVE = TR / NW;                     // 4
-constexpr int A_FLOATS = TR * LDA;                         // one A buffer
-constexpr int EPI_MAX = 2;                                 // epilogue operand rows per output row
-constexpr int COEF_FLOATS = TR * MAX_R;
-constexpr int LDS_FLOATS = 2 * A_FLOATS + EPI_MAX * A_FLOATS + COEF_FLOATS;
-}  // namespace r256
-
+// LDS-DMA helpers (global_load_lds: the row lands in LDS without passing through VGPRs)
 typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef __attribute__((address_space(1))) void* gbl_vptr;
 
@@ -430,163 +390,6 @@ __device__ __forceinline__ void dma_row_1k(const float* src_row, float* lds_row,
     __builtin_amdgcn_global_load_lds((gbl_vptr)(src_row + lane * 4), (lds_vptr)lds_row, 16, 0, 0);
 }
 
-__global__ __launch_bounds__(512) void rowgemm256_dma_kernel(RowGemmP p, int epi_rows) {
-    using namespace r256;
-    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
-    float* bufA = lds;                                  // [2][TR][LDA]
-    float* epi = lds + 2 * A_FLOATS;                    // [EPI_MAX][TR][LDA]
-    float* coefL = epi + EPI_MAX * A_FLOATS;            // [TR][MAX_R]
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int i = lane & 31, h = lane >> 5;
-    const int c0 = wave * 32;
-    const int R = p.R;
-    const bool gatherV = (R > 0) && (p.v_row_stride != 0);
-
-    float breg[D / 2];
-#pragma unroll
-    for (int s = 0; s < D / 2; ++s) {
-        const int kk = 8 * (s >> 2) + 4 * h + (s & 3);
-        breg[s] = p.b_trans ? p.B[(c0 + i) * D + kk] : p.B[kk * D + c0 + i];
-    }
-
-    const long long ntiles = ((long long)p.M + TR - 1) / TR;
-    const long long t_beg = (long long)blockIdx.x * p.tiles_per_block;
-    long long t_end = t_beg + p.tiles_per_block;
-    if (t_end > ntiles) t_end = ntiles;
-    if (t_beg >= t_end) return;
-    const long long Mlast = (long long)p.M - 1;
-
-    // row index of this wave's j-th row of tile t (clamped: rows past M load row M-1, never stored)
-    auto row_of = [&](long long t, int j) -> long long {
-        long long e = t * TR + wave * ROWS_PER_WAVE + j;
-        return e > Mlast ? Mlast : e;
-    };
-    // lanes 0..3 load the indices of the wave's 4 rows of tile t
-    auto load_idx = [&](const int* idx, long long t) -> int {
-        if (!idx || lane >= ROWS_PER_WAVE || t >= t_end) return 0;
-        return idx[row_of(t, lane)];
-    };
-    // wave-uniform copies (SGPRs) of the 4 row indices, made once the loads have landed
-    int sa[ROWS_PER_WAVE], sv[ROWS_PER_WAVE], sc[ROWS_PER_WAVE];
-    auto to_sgpr = [&](int v, int (&dst)[ROWS_PER_WAVE]) {
-#pragma unroll
-        for (int j = 0; j < ROWS_PER_WAVE; ++j) dst[j] = __builtin_amdgcn_readlane(v, j);
-    };
-
-    // prologue: A(t_beg) -> buffer 0; indices for A(t_beg+1) and the epilogue of t_beg
-    {
-        int ia0 = load_idx(p.a_idx, t_beg);
-        int ia1 = load_idx(p.a_idx, t_beg + 1);
-        int iv0 = load_idx(p.v_idx, t_beg);
-        int ic0 = load_idx(p.coef_idx, t_beg);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        to_sgpr(ia0, sa);
-#pragma unroll
-        for (int j = 0; j < ROWS_PER_WAVE; ++j) {
-            const long long src = p.a_idx ? (long long)sa[j] : row_of(t_beg, j);
-            dma_row_1k(p.A + src * D, bufA + (wave * ROWS_PER_WAVE + j) * LDA, lane);
-        }
-        to_sgpr(ia1, sa);
-        to_sgpr(iv0, sv);
-        to_sgpr(ic0, sc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-
-    int b = 0;
-    for (long long t = t_beg; t < t_end; ++t, b ^= 1) {
-        const long long row0 = t * TR;
-        // (1) epilogue operand rows of tile t -> epi
-        if (gatherV) {
-#pragma unroll
-            for (int j = 0; j < ROWS_PER_WAVE; ++j) {
-                const long long vi = p.v_idx ? (long long)sv[j] : row_of(t, j);
-                for (int r = 0; r < R; ++r)
-                    dma_row_1k(p.V + r * p.v_rel_stride + vi * p.v_row_stride,
-                               epi + (r * TR + wave * ROWS_PER_WAVE + j) * LDA, lane);
-            }
-        } else if (epi_rows) {      // sigma' aux rows, same rows as the output
-#pragma unroll
-            for (int j = 0; j < ROWS_PER_WAVE; ++j)
-                dma_row_1k(p.aux + row_of(t, j) * D, epi + (wave * ROWS_PER_WAVE + j) * LDA, lane);
-        }
-        // (2) per-row coefficients of tile t (lanes 0 .. 4R-1)
-        float creg = 0.f;
-        if (R > 0 && lane < ROWS_PER_WAVE * R) {
-            const int j = lane / R, r = lane % R;
-            long long ci;
-            if (p.coef_idx)
-                ci = j == 0 ? sc[0] : j == 1 ? sc[1] : j == 2 ? sc[2] : sc[3];
-            else
-                ci = row_of(t, j);
-            creg = p.coef[ci * R + r];
-        }
-        // (3) A rows of tile t+1 -> the other buffer
-        if (t + 1 < t_end) {
-#pragma unroll
-            for (int j = 0; j < ROWS_PER_WAVE; ++j) {
-                const long long src = p.a_idx ? (long long)sa[j] : row_of(t + 1, j);
-                dma_row_1k(p.A + src * D, bufA + (b ^ 1) * A_FLOATS + (wave * ROWS_PER_WAVE + j) * LDA, lane);
-            }
-        }
-        // (4) indices for the next iteration
-        const int ia_n = load_idx(p.a_idx, t + 2);
-        const int iv_n = load_idx(p.v_idx, t + 1);
-        const int ic_n = load_idx(p.coef_idx, t + 1);
-
-        // (5) MFMA over A(t)
-        f32x16 acc;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-        const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h;
-#pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            const f32x4 a4 = ld4(arow + 8 * q);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[0], breg[4 * q + 0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[1], breg[4 * q + 1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[2], breg[4 * q + 2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[3], breg[4 * q + 3], acc, 0, 0, 0);
-        }
-        // (6)-(9) everything this wave issued has landed; publish coefficients; barrier
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (R > 0 && lane < ROWS_PER_WAVE * R) {
-            const int j = lane / R, r = lane % R;
-            coefL[(wave * ROWS_PER_WAVE + j) * MAX_R + r] = creg;
-        }
-        to_sgpr(ia_n, sa);
-        to_sgpr(iv_n, sv);
-        to_sgpr(ic_n, sc);
-        __syncthreads();
-
-        // (10) epilogue from LDS (same add order as rowgemm_kernel)
-        const int c = c0 + i;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            const long long e = row0 + row;
-            if (e >= p.M) continue;
-            float v = acc[reg];
-            float* cp = p.C + e * D + c;
-            if (p.accumulate) v += *cp;
-            if (gatherV) {
-                for (int r = 0; r < R; ++r) v = fmaf(coefL[row * MAX_R + r], epi[(r * TR + row) * LDA + c], v);
-            } else if (R > 0) {        // broadcast V (v_row_stride == 0): tiny, cache-resident
-                for (int r = 0; r < R; ++r) v = fmaf(coefL[row * MAX_R + r], p.V[r * p.v_rel_stride + c], v);
-            }
-            if (p.act == IDDGCN_ACT_SIGMOID) {
-                v = sigmoid_fast(v);
-            } else if (p.act == IDDGCN_ACT_DSIGMOID) {
-                const float x = epi[row * LDA + c];
-                v = v * (x * (1.0f - x));
-            }
-            *cp = v;
-        }
-        // (11) epilogue buffers free for the next tile
-        __syncthreads();
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Row GEMM, D = 256, v3: staggered waves, wave-private epilogue slabs.
@@ -732,11 +535,6 @@ __device__ __forceinline__ float wave_max(float v) {             // max over the
     return v;
 }
 
-// REC (IDDGCN_ACT_DSIGMOID_COMBINE): the sigma' operand is not read from memory but recomputed,
-// x = sigmoid(V_0[v] + sum_r coef_r V_{r+1}[v]) from the tile's distinct V rows (NV = R + 1), so
-// the tail activation x^1 of layer 1 never has to be re-read by the backward.  The caller
-// guarantees at most REC_CAP runs of equal v_idx per 32-row tile (tail-sorted edges: 1-4).
-constexpr int REC_CAP = 8;
 // NV: gathered V tables (0 = none; 1, 2 = exactly R; 4, 8 = capacity for R <= NV, capped slabs).
 // Up to ROWGEMM_BATCH independent GEMMs of the same variant run in one launch: blockIdx.y = entry.
 // CW: broadcast V (NV = 0) with more than 2 coefficients per row (R <= 8); R <= 2 keeps the 2-slot
@@ -747,7 +545,7 @@ constexpr int REC_CAP = 8;
 // PL (split mode): the planes form (IDDGCN_PLANES_*) of the variant: AUX kernels read the sigma' operand
 // as planes rows, gathered-combine kernels (NV = 1, 2) write C as planes rows.
 // (A planes rows are a run-time flag of every X3 kernel: convert_rows just skips.)
-template <int NV, bool AUX, bool HAS_COEF, bool X3, bool REC = false, bool CW = false, bool BF = false, bool PL = false>
+template <int NV, bool AUX, bool HAS_COEF, bool X3, bool CW = false, bool BF = false, bool PL = false>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     using namespace r3;
     // A row pitch: bf16 rows (BF) need 512 B of the 1040-B fp32 row; a 528-B pitch keeps the same bank
@@ -755,22 +553,20 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     constexpr int LDA = BF ? 132 : r3::LDA;
     constexpr int A_FLOATS = TR * LDA;
     const RowGemmP p = pb.p[blockIdx.y];
-    static_assert(!PL || (X3 && !BF && !REC && !CW && ((AUX && NV == 0) || (!AUX && (NV == 1 || NV == 2)))),
+    static_assert(!PL || (X3 && !BF && !CW && ((AUX && NV == 0) || (!AUX && (NV == 1 || NV == 2)))),
                   "PL: split-mode sigma' backward or R <= 2 gathered forward");
-    static_assert(!BF || (X3 && !REC), "BF: the 16-bit A-plane pipeline, no recompute");
-    static_assert(!REC || (NV >= 2 && NV <= 3 && !AUX && HAS_COEF), "REC: V_0 + coefficient-weighted V_1.., no aux");
-    static_assert(REC || NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
-    constexpr bool WIDE = !REC && NV > 2;              // capped slabs, run-time R <= NV
+    static_assert(!BF || X3, "BF: the 16-bit A-plane pipeline");
+    static_assert(NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
+    constexpr bool WIDE = NV > 2;                      // capped slabs, run-time R <= NV
     // capped V slabs r >= 1 (rows past the cap read from L2): WIDE, and NV = 2 when V3_CAP2 > 0
-    constexpr bool CAPPED = WIDE || (V3_CAP2 > 0 && NV == 2 && !REC);
+    constexpr bool CAPPED = WIDE || (V3_CAP2 > 0 && NV == 2);
     // the sigma' slab: after the V slabs; BF keeps it out of slab 0, whose fp32 staging of the output
     // would overwrite bf16 aux rows other lanes have not read yet (different row pitches)
     constexpr int AUXS = (BF && NV == 0) ? 1 : NV;
     constexpr int NS = AUX ? AUXS + 1 : NV;
     constexpr int NSL = NS > 1 ? NS : 1;               // slabs per wave (slab 0 also stages C)
-    // Slab 0 holds 32 rows (it also stages the C tile); REC slabs r >= 1 hold REC_CAP rows, WIDE
-    // slabs r >= 1 GATHER_CAP rows.
-    constexpr int CAPV = REC ? REC_CAP : (WIDE ? GATHER_CAP : (CAPPED ? V3_CAP2 : 32));
+    // Slab 0 holds 32 rows (it also stages the C tile); WIDE slabs r >= 1 hold GATHER_CAP rows.
+    constexpr int CAPV = WIDE ? GATHER_CAP : (CAPPED ? V3_CAP2 : 32);
     constexpr int SLABC = CAPV * 32;
     constexpr int SLABS = SLAB + (NSL - 1) * SLABC;    // floats of all slabs of one wave
     // coefficient slots: 32 rows x R; up to 8 relations for WIDE and for broadcast V (NV = 0)
@@ -967,7 +763,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                     if constexpr (WIDE) {
                         if (r >= R) break;
                     }
-                    if constexpr (REC || CAPPED) {
+                    if constexpr (CAPPED) {
                         // capped slab: rows past CAPV stay unwritten (precondition broken: stay in bounds)
                         if (r > 0 && row >= CAPV) continue;
                     }
@@ -1048,7 +844,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
 #pragma unroll
                 for (int r = 0; r < CFN; ++r)
                     if (r < R) cf[r] = coefw[i * R + r];
-            } else if (REC ? R == 2 : (NV == 2 || (NV == 0 && R == 2))) {
+            } else if (NV == 2 || (NV == 0 && R == 2)) {
                 // two scalar reads (merged into one ds_read_b64): a float2-typed LDS read here made the
                 // compiler guard it with a vmcnt(0) that drained the A-tile DMA in flight
                 cf[0] = coefw[i * 2];
@@ -1077,21 +873,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                 if (p.accumulate)
                     v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (i * D + col) * 4, 0, 0));
             }
-            if constexpr (REC) {        // v *= x(1-x), x = sigmoid(V_0 + sum_r cf_r V_{r+1})
-                const int offv = vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
-                f32x4 xs = ld4(slabw + offv);
-#pragma unroll
-                for (int r = 1; r < NV; ++r) {
-                    const f32x4 s = ld4(slabw + soff(r) + offv);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) xs[q] = fmaf(cf[r - 1], s[q], xs[q]);
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float x = sigmoid_fast(xs[q]);
-                    v[q] = v[q] * (x * (1.0f - x));
-                }
-            } else if (NV > 0 && !(V3_ABL & 2)) {
+            if (NV > 0 && !(V3_ABL & 2)) {
                 const int offv = vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
 #pragma unroll
                 for (int r = 0; r < NV; ++r) {
@@ -1535,27 +1317,6 @@ constexpr int D = 256, TK = 32, LDR = D + 4, TILE = TK * LDR;
 constexpr float S_INIT = 0x1p126f;                       // pow2_scale(0): "no data yet"
 }
 
-// SEG: the tail-side segmented reduction of the same layer (tail_seg_reduce_kernel) fused into the
-// dS = x^T do pass, so do is read from HBM once instead of twice:
-//   dP_r[t] = sum_{e: t_e = t} W[e][r] do_e      (row order, fmaf chain: = tail_seg_reduce)
-//   dWedge[e][r] = <do_e, P_r[t_e]>
-// Block row ranges (row_beg) start at tail-segment starts, so every segment is summed by one block
-// and written once (no partials, no atomics; the caller zeroes dP for tails without edges).  Per
-// tile, the distinct tails' P rows (<= TNSEG_CAP, the caller's bound) are DMA'd into LDS with the
-// tile; while the fp32 do rows are still in LDS (before the in-place fp16 conversion) lane (i, h)
-// walks column 32w+i of the tile's rows for relation h: the segment sum in a register and the dot
-// partials reduced over the wave's 32 columns, then over the 8 waves (block order) by wave 0.
-struct TnSegP {
-    const int* row_beg;       // [n_blocks + 1]
-    const int* tail;          // [M] tail of each row (sorted)
-    const float* W;           // [M][R]
-    const float* P;           // [R][.][D]
-    long long p_rel_stride;
-    float* dP;                // [R][.][D], same stride as P
-    float* dWedge;            // [M][R]
-    int R;                    // 1 or 2
-};
-constexpr int TNSEG_CAP = 6;
 
 // PA: A arrives as planes rows (IDDGCN_PLANES_A, fixed scale 2^15): no A conversion; the A fragments
 // (8 consecutive rows of one column) are read straight from the row-major hi / lo planes with two
@@ -1580,12 +1341,12 @@ struct TnBatch {
     const float* B[TN_BATCH];
     float* slab[TN_BATCH];
 };
-template <bool SEG, bool PA = false>
+template <bool PA = false>
 __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long long rpb_, const float* __restrict__ A_,
                                                             const float* __restrict__ B_, float* __restrict__ slab_,
-                                                            TnSegP sp, TnBatch tb) {
+                                                            TnBatch tb) {
     using namespace tn3;
-    const bool bat = !SEG && tb.n > 0;
+    const bool bat = tb.n > 0;
     const int ent = bat ? (int)blockIdx.y : 0;
     if (bat && (int)blockIdx.x >= tb.nb[ent]) return;     // past this entry's slabs (whole workgroup)
     const long long M = bat ? tb.M[ent] : M_;
@@ -1593,19 +1354,12 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
     const float* __restrict__ A = bat ? tb.A[ent] : A_;
     const float* __restrict__ B = bat ? tb.B[ent] : B_;
     float* __restrict__ slab = bat ? tb.slab[ent] : slab_;
-    static_assert(!(SEG && PA), "planes A: unfused TN only");
     constexpr int LDRA = PA ? 272 : LDR;                 // A row pitch (floats)
     constexpr int TILE_A = TK * LDRA;
     constexpr int BUF = TILE_A + TILE;                   // one [A | B] buffer
-    // SEG region per buffer: tails[32] | run-start mask (+pad)[32] | W[32][2] | P rows [CAP][2][D];
-    // then part[8][32][2]
-    constexpr int SEG_BUF = 32 + 32 + 64 + TNSEG_CAP * 2 * D;
-    constexpr int SEG_F = SEG ? 2 * SEG_BUF + 8 * 32 * 2 : 0;
-    __shared__ __attribute__((aligned(16))) float lds[2 * BUF + 2 * 8 + SEG_F];   // [buf][A|B][TK][pitch], sB[buf][8]
-    static_assert((2 * BUF + 2 * 8 + SEG_F) * 4 <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) float lds[2 * BUF + 2 * 8];   // [buf][A|B][TK][pitch], sB[buf][8]
+    static_assert((2 * BUF + 2 * 8) * 4 <= 160 * 1024, "LDS budget");
     float* sBpub = lds + 2 * BUF;
-    float* segL = lds + 2 * BUF + 2 * 8;
-    float* partL = segL + 2 * SEG_BUF;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int i = lane & 31, h = lane >> 5;
@@ -1620,112 +1374,10 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
 #pragma unroll
     for (int cj = 0; cj < 8; ++cj) curB[cj] = S_INIT;
 
-    long long r_beg, r_end;
-    if constexpr (SEG) {
-        r_beg = sp.row_beg[blockIdx.x];
-        r_end = sp.row_beg[blockIdx.x + 1];
-    } else {
-        r_beg = (long long)blockIdx.x * rows_per_block;
-        r_end = r_beg + rows_per_block;
-        if (r_end > M) r_end = M;
-    }
+    const long long r_beg = (long long)blockIdx.x * rows_per_block;
+    long long r_end = r_beg + rows_per_block;
+    if (r_end > M) r_end = M;
     const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
-
-    // ---- SEG state and helpers ----
-    const int R = SEG ? sp.R : 0;
-    const bool sact = SEG && h < R;                  // lane (i, h) reduces relation h of column c
-    const int c = 32 * wave + i;
-    int cur_t = -1;                                  // tail of the open segment (uniform)
-    float sacc = 0.f;
-    float* const dPc = SEG ? sp.dP + (sact ? h : 0) * sp.p_rel_stride + c : nullptr;   // dP[h][.][c]
-    auto load_tails = [&](long long t) -> int {      // lane < 32: tail of row `lane` of tile t, or -1
-        const long long e = r_beg + t * TK + lane;
-        return (SEG && lane < 32 && t < nt && e < r_end) ? sp.tail[e] : -1;
-    };
-    auto seg_stage = [&](int tk, long long t, int b) {
-        float* base = segL + b * SEG_BUF;
-        int* tl = reinterpret_cast<int*>(base);
-        float* Wl = base + 64;
-        float* Pl = base + 128;
-        const int tprev = __shfl_up(tk, 1, 64);
-        const bool start = lane < 32 && tk >= 0 && (lane == 0 || tk != tprev);
-        const unsigned long long m = __ballot(start);
-        int u = __popcll(m);
-        if (u > TNSEG_CAP) u = TNSEG_CAP;            // (caller's bound broken: stay in bounds)
-        if (wave == 0 && lane < 32) tl[lane] = tk;
-        if (wave == 0 && lane == 32) tl[32] = (int)(unsigned)m;     // run starts of the tile (bit = row)
-        for (int q = wave; q < u * R; q += 8) {      // P rows of the distinct tails, one 1 KiB DMA each
-            const int sidx = R > 1 ? q / R : q, rr = q - sidx * R;
-            unsigned long long mm = m;
-            for (int z = 0; z < sidx; ++z) mm &= mm - 1;
-            const int ts = __builtin_amdgcn_readlane(tk, __builtin_ctzll(mm));
-            dma_row_1k(sp.P + rr * sp.p_rel_stride + (long long)ts * D, Pl + (sidx * 2 + rr) * D, lane);
-        }
-        if (wave == 1) {                             // the tile's W rows (32 x R floats, contiguous)
-            const long long row0 = r_beg + t * TK;
-            const long long nw = (r_end - row0 < TK ? r_end - row0 : TK) * R;
-            const float* g = lane < nw ? sp.W + row0 * R + lane : sp.W;
-            __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)Wl, 4, 0, 0);
-        }
-    };
-    // walk the fp32 do rows of tile t (before convert) for column c, relation h: 8 rows at a time,
-    // their do / W values read up front (independent LDS reads), runs from the tile's start mask
-    // (scalar branches), the P value of the run's tail re-read from LDS at each run start only
-    auto seg_scan = [&](long long t, int b) {
-        const float* base = segL + b * SEG_BUF;
-        const int* tl = reinterpret_cast<const int*>(base);
-        const float* Wl = base + 64;
-        const float* Pl = base + 128;
-        const float* Bf = lds + b * BUF + TILE_A;
-        const long long row0 = r_beg + t * TK;
-        const int nrows = (int)(r_end - row0 < TK ? r_end - row0 : TK);
-        const unsigned mstart = (unsigned)__builtin_amdgcn_readfirstlane(tl[32]);
-        const int hh = sact ? h : 0;
-        int slot = 0;
-        float pcur = 0.f;
-#pragma unroll 1
-        for (int q0 = 0; q0 < TK; q0 += 8) {
-            float d[8], w[8], pv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                d[j] = Bf[(q0 + j) * LDR + c];
-                w[j] = Wl[(q0 + j) * R + hh];
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int row = q0 + j;
-                pv[j] = 0.f;
-                if (row < nrows) {
-                    if ((mstart >> row) & 1u) {
-                        const int tr = __builtin_amdgcn_readfirstlane(tl[row]);
-                        if (tr != cur_t) {
-                            if (sact && cur_t >= 0) dPc[cur_t * D] = sacc;
-                            cur_t = tr;
-                            sacc = 0.f;
-                        }
-                        pcur = Pl[(slot * 2 + hh) * D + c];
-                        ++slot;
-                    }
-                    sacc = fmaf(w[j], d[j], sacc);
-                    pv[j] = d[j] * pcur;
-                }
-            }
-            const float tot = multi_reduce<32, 8>(pv, i);
-            if ((i & 3) == 0) partL[(wave * 32 + q0 + (i >> 2)) * 2 + h] = tot;
-        }
-    };
-    // dWedge of tile t = sum of the 8 waves' partials, in wave order; wave w writes rows 4w..4w+3
-    auto seg_dwedge = [&](long long t) {
-        const long long row0 = r_beg + t * TK;
-        const int nrows = (int)(r_end - row0 < TK ? r_end - row0 : TK);
-        const int row = 4 * wave + (lane >> 1), rr = lane & 1;
-        if (lane < 8 && row < nrows && rr < R) {
-            float sum = 0.f;
-#pragma unroll
-            for (int w = 0; w < 8; ++w) sum += partL[(w * 32 + row) * 2 + rr];
-            sp.dWedge[(row0 + row) * R + rr] = sum;
-        }
-    };
 
     auto stage = [&](long long t, int b) {
         if (TN_ABL & 4) return;
@@ -1785,24 +1437,12 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
     };
     if constexpr (PA) sA = PLANE_S;
 
-    int tnext = -1;
     if (nt > 0) {
         stage(0, 0);
-        if constexpr (SEG) {
-            seg_stage(load_tails(0), 0, 0);
-            tnext = load_tails(1);
-        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if constexpr (SEG) seg_scan(0, 0);
         convert(0);
-        if (nt > 1) {                                // tile 1 in flight while tile 0's MFMAs run
-            stage(1, 1);
-            if constexpr (SEG) {
-                seg_stage(tnext, 1, 1);
-                tnext = load_tails(2);
-            }
-        }
+        if (nt > 1) stage(1, 1);                     // tile 1 in flight while tile 0's MFMAs run
         __syncthreads();
     }
     // Tile t+2's DMA is issued as soon as every wave's MFMAs of tile t are done (the barrier after them
@@ -1812,7 +1452,6 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
     // profiles/r02/ablations/tn_abl.txt).
     int b = 0;
     for (long long t = 0; t < nt; ++t, b ^= 1) {
-        if constexpr (SEG) seg_dwedge(t);
         // B-side scales of this tile: rescale the accumulators whose block scale dropped
 #pragma unroll
         for (int cj = 0; cj < 8; ++cj) {
@@ -1850,20 +1489,12 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // tile t+1 landed (issued one tile ago)
         __syncthreads();                                         // buffer b free
-        if (t + 2 < nt) {
-            stage(t + 2, b);
-            if constexpr (SEG) {
-                seg_stage(tnext, t + 2, b);
-                tnext = load_tails(t + 3);
-            }
-        }
+        if (t + 2 < nt) stage(t + 2, b);
         if (t + 1 < nt) {
-            if constexpr (SEG) seg_scan(t + 1, b ^ 1);
             convert(b ^ 1);
             __syncthreads();
         }
     }
-    if (sact && cur_t >= 0) dPc[cur_t * D] = sacc;                 // last segment
     float* out = slab + (long long)blockIdx.x * D * D;
     const float ia = pow2_inv(sA);
 #pragma unroll
@@ -2970,42 +2601,32 @@ __global__ void step_advance_kernel(int* __restrict__ step, float* __restrict__ 
 // ---- D = 256 row-GEMM variant selection (rowgemm256_v3_kernel) ----
 struct V3Sel {
     int nv;                 // gathered V tables (template NV)
-    bool aux, hc, rec;
+    bool aux, hc;
     bool cw = false;        // broadcast V with R > 2 coefficients
     bool pl = false;        // planes C (gathered forward) / planes sigma' operand (backward)
+    bool split = false;     // IDDGCN_GEMM_SPLIT_F16 operands (template X3), else exact f32
+    bool same(const V3Sel& o) const {
+        return nv == o.nv && aux == o.aux && hc == o.hc && cw == o.cw && pl == o.pl && split == o.split;
+    }
 };
-// Which v3 instantiation computes this call, or false (the DMA-v2 / register-staged kernels then run).
-bool v3_select_(const RowGemmP& p, V3Sel& sel);
+// Which v3 instantiation computes this call, or false (the register-staged rowgemm_kernel<256> then runs:
+// a gathered V with the sigma' epilogue, or V rows that are not dense D-float rows).
 bool v3_select(const RowGemmP& p, V3Sel& sel) {
-    if (!v3_select_(p, sel)) return false;
+    const bool gatherV = p.R > 0 && p.v_row_stride != 0;
+    const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
+    if (gatherV) {
+        if (dsig || p.v_row_stride != 256) return false;
+        // R <= 2: exactly R slabs; more relations: capped slabs (rows past the cap of a tile come from L2)
+        sel = {p.R <= 2 ? p.R : (p.R <= 4 ? 4 : 8), false, true};
+    } else {
+        sel = {0, dsig, p.R > 0, p.R > 2};
+    }
+    sel.split = p.precision == IDDGCN_GEMM_SPLIT_F16;
     sel.pl = (p.planes & (IDDGCN_PLANES_C | IDDGCN_PLANES_AUX)) != 0;
     if (!sel.pl) return true;
     // the planes forms: C planes on the R <= 2 gathered forward, sigma' planes on the plain backward
-    if ((p.planes & IDDGCN_PLANES_C) && !(sel.nv >= 1 && sel.nv <= 2 && !sel.rec && !sel.aux)) return false;
+    if ((p.planes & IDDGCN_PLANES_C) && !(sel.nv >= 1 && sel.nv <= 2 && !sel.aux)) return false;
     if ((p.planes & IDDGCN_PLANES_AUX) && !(sel.aux && sel.nv == 0 && !sel.hc)) return false;
-    return true;
-}
-bool v3_select_(const RowGemmP& p, V3Sel& sel) {
-    if (!(g_rowgemm_path == 0 || g_gemm_split)) return false;
-    const bool gatherV = p.R > 0 && p.v_row_stride != 0;
-    const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
-    if (p.act == IDDGCN_ACT_DSIGMOID_COMBINE) {
-        // x^1 recompute: R <= 2, dense V rows, the caller's bound on V runs per 32-row tile
-        if (!(p.R <= 2 && p.v_row_stride == 256 && p.v_runs_max >= 1 && p.v_runs_max <= REC_CAP)) return false;
-        sel = {p.R + 1, false, true, true, false};
-        return true;
-    }
-    if (gatherV) {
-        if (dsig || p.v_row_stride != 256) return false;
-        if (p.R <= 2) {
-            sel = {p.R, false, true, false, false};
-            return true;
-        }
-        // more relations: capped slabs (rows past the cap of a tile come from L2)
-        sel = {p.R <= 4 ? 4 : 8, false, true, false, false};
-        return true;
-    }
-    sel = {0, dsig, p.R > 0, false, p.R > 2};
     return true;
 }
 
@@ -3015,7 +2636,7 @@ RowGemmP to_p(const iddgcn_rowgemm_t& a) {
     p.M = a.M; p.A = a.A; p.a_idx = a.a_idx; p.B = a.B; p.b_trans = a.b_trans;
     p.C = a.C; p.accumulate = a.accumulate; p.R = a.R; p.coef = a.coef; p.coef_idx = a.coef_idx;
     p.V = a.V; p.v_idx = a.v_idx; p.v_rel_stride = a.v_rel_stride; p.v_row_stride = a.v_row_stride;
-    p.act = a.act; p.aux = a.aux; p.v_runs_max = a.v_runs_max; p.planes = a.planes;
+    p.act = a.act; p.aux = a.aux; p.planes = a.planes; p.precision = a.precision;
     p.tiles_per_block = 1;
     return p;
 }
@@ -3024,16 +2645,15 @@ RowGemmP to_p(const iddgcn_rowgemm_t& a) {
 int check_rowgemm(const iddgcn_rowgemm_t& a) {
     if (!dim_ok(a.D)) return IDDGCN_E_BAD_DIM;
     if (a.R < 0 || a.R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (a.precision != IDDGCN_GEMM_EXACT_F32 && a.precision != IDDGCN_GEMM_SPLIT_F16) return IDDGCN_E_BAD_ARG;
     if (a.M == 0) return 0;
     if (a.M < 0 || !a.A || !a.B || !a.C) return IDDGCN_E_BAD_ARG;
     if (a.R > 0 && (!a.coef || !a.V)) return IDDGCN_E_BAD_ARG;
     if (a.act == IDDGCN_ACT_DSIGMOID && !a.aux) return IDDGCN_E_BAD_ARG;
-    if (a.act == IDDGCN_ACT_DSIGMOID_COMBINE && (a.R < 1 || a.R + 1 > MAX_R || a.v_row_stride == 0))
-        return IDDGCN_E_BAD_ARG;
-    if (a.act < IDDGCN_ACT_NONE || a.act > IDDGCN_ACT_DSIGMOID_COMBINE) return IDDGCN_E_BAD_ARG;
+    if (a.act < IDDGCN_ACT_NONE || a.act > IDDGCN_ACT_DSIGMOID) return IDDGCN_E_BAD_ARG;
     if (a.planes) {
         if (a.planes & ~(IDDGCN_PLANES_A | IDDGCN_PLANES_C | IDDGCN_PLANES_AUX)) return IDDGCN_E_BAD_ARG;
-        if (a.D != 256 || !g_gemm_split || a.a_idx) return IDDGCN_E_BAD_ARG;
+        if (a.D != 256 || a.precision != IDDGCN_GEMM_SPLIT_F16 || a.a_idx) return IDDGCN_E_BAD_ARG;
         if ((a.planes & IDDGCN_PLANES_C) && (a.act != IDDGCN_ACT_SIGMOID || a.accumulate)) return IDDGCN_E_BAD_ARG;
         if ((a.planes & IDDGCN_PLANES_AUX) && a.act != IDDGCN_ACT_DSIGMOID) return IDDGCN_E_BAD_ARG;
         V3Sel sel;
@@ -3062,7 +2682,7 @@ void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel, bool b
     if (nbmax == 0) return;
     const dim3 g((unsigned)nbmax, (unsigned)n), blk(512);
     if (bf) {      // bf16 edge tables: gathered-combine forward, sigma' backward, plain
-#define V3B(NV, AUX, HC) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, false, false, true>), g, blk, 0, st, pb)
+#define V3B(NV, AUX, HC) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, false, true>), g, blk, 0, st, pb)
         if (sel.nv == 1) V3B(1, false, true);
         else if (sel.nv == 2) V3B(2, false, true);
         else if (sel.nv == 4) V3B(4, false, true);
@@ -3072,35 +2692,32 @@ void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel, bool b
 #undef V3B
         return;
     }
-    const bool x3 = g_gemm_split != 0;
-#define V3L(NV, AUX, HC, REC)                                                                        \
-    {                                                                                                \
-        if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, REC>), g, blk, 0, st, pb); \
-        else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, false, REC>), g, blk, 0, st, pb);   \
+    const bool x3 = sel.split;
+#define V3L(NV, AUX, HC)                                                                        \
+    {                                                                                           \
+        if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true>), g, blk, 0, st, pb); \
+        else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, false>), g, blk, 0, st, pb);   \
     }
-#define V3W(AUX)                                                                                            \
-    {                                                                                                       \
-        if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, true, false, true>), g, blk, 0, st, pb); \
-        else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, false, false, true>), g, blk, 0, st, pb);   \
+#define V3W(AUX)                                                                                     \
+    {                                                                                                \
+        if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, true, true>), g, blk, 0, st, pb); \
+        else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, false, true>), g, blk, 0, st, pb);   \
     }
     if (sel.pl) {           // check_rowgemm: split mode
-        if (sel.nv == 1) hipLaunchKernelGGL((rowgemm256_v3_kernel<1, false, true, true, false, false, false, true>), g, blk, 0, st, pb);
-        else if (sel.nv == 2) hipLaunchKernelGGL((rowgemm256_v3_kernel<2, false, true, true, false, false, false, true>), g, blk, 0, st, pb);
-        else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, true, false, true, false, false, false, true>), g, blk, 0, st, pb);
-    } else if (sel.rec) {
-        if (sel.nv == 2) V3L(2, false, true, true)
-        else V3L(3, false, true, true)
-    } else if (sel.nv == 1) V3L(1, false, true, false)
-    else if (sel.nv == 2) V3L(2, false, true, false)
-    else if (sel.nv == 4) V3L(4, false, true, false)
-    else if (sel.nv == 8) V3L(8, false, true, false)
+        if (sel.nv == 1) hipLaunchKernelGGL((rowgemm256_v3_kernel<1, false, true, true, false, false, true>), g, blk, 0, st, pb);
+        else if (sel.nv == 2) hipLaunchKernelGGL((rowgemm256_v3_kernel<2, false, true, true, false, false, true>), g, blk, 0, st, pb);
+        else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, true, false, true, false, false, true>), g, blk, 0, st, pb);
+    } else if (sel.nv == 1) V3L(1, false, true)
+    else if (sel.nv == 2) V3L(2, false, true)
+    else if (sel.nv == 4) V3L(4, false, true)
+    else if (sel.nv == 8) V3L(8, false, true)
     else if (sel.hc && sel.cw) {
         if (sel.aux) V3W(true)
         else V3W(false)
-    } else if (sel.hc && sel.aux) V3L(0, true, true, false)
-    else if (sel.hc) V3L(0, false, true, false)
-    else if (sel.aux) V3L(0, true, false, false)
-    else V3L(0, false, false, false)
+    } else if (sel.hc && sel.aux) V3L(0, true, true)
+    else if (sel.hc) V3L(0, false, true)
+    else if (sel.aux) V3L(0, true, false)
+    else V3L(0, false, false)
 #undef V3L
 #undef V3W
 }
@@ -3148,18 +2765,6 @@ extern "C" {
 
 int iddgcn_abi_version(void) { return IDDGCN_ABI_VERSION; }
 
-int iddgcn_set_rowgemm_path(int path) {
-    const int old = g_rowgemm_path;
-    g_rowgemm_path = (path < 0 || path > 2) ? 0 : path;
-    return old;
-}
-
-int iddgcn_set_gemm_precision(int mode) {
-    const int old = g_gemm_split;
-    g_gemm_split = mode == IDDGCN_GEMM_SPLIT_F16 ? 1 : 0;
-    return old;
-}
-
 int iddgcn_spmm_csr_f32(void* stream, int n_seg, int n_rows, int d, const int* row_ptr, const int* col,
                         const float* vals, const float* X, float* Y, int accumulate) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
@@ -3204,6 +2809,14 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     if (a->M == 0) return 0;                 // nothing to do (an empty C may have a null pointer)
     RowGemmP p = to_p(*a);
     hipStream_t st = (hipStream_t)stream;
+    V3Sel sel;
+    if (a->D == 256 && v3_select(p, sel)) {
+        RowGemmBatch pb;
+        pb.p[0] = p;
+        launch_v3(st, pb, 1, sel);
+        return launch_status();
+    }
+    // D < 256, and the D = 256 forms the v3 kernel does not take: the register-staged kernel (exact f32)
 #define RGEMM(DD, MAXB)                                                                         \
     {                                                                                           \
         const long long nt = ((long long)p.M + RG<DD>::TR - 1) / RG<DD>::TR;                    \
@@ -3213,35 +2826,6 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
         RowGemmBatch pb;                                                                        \
         pb.p[0] = p;                                                                            \
         hipLaunchKernelGGL(rowgemm_kernel<DD>, dim3((unsigned)nb), dim3(RG<DD>::NW * 64), 0, st, pb); \
-    }
-    const bool gatherV = p.R > 0 && p.v_row_stride != 0;
-    const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
-    V3Sel sel;
-    if (a->D == 256 && v3_select(p, sel)) {
-        RowGemmBatch pb;
-        pb.p[0] = p;
-        launch_v3(st, pb, 1, sel);
-        return launch_status();
-    }
-    if (p.act == IDDGCN_ACT_DSIGMOID_COMBINE) {
-        switch (a->D) {      // any v_idx order: the register-staged kernel
-            case 32: RGEMM(32, 2048); break;
-            case 64: RGEMM(64, 2048); break;
-            case 128: RGEMM(128, 1024); break;
-            default: RGEMM(256, 256); break;
-        }
-        return launch_status();
-    }
-    const int epi_rows = gatherV ? p.R : (dsig ? 1 : 0);
-    const bool dma_ok = a->D == 256 && epi_rows <= r256::EPI_MAX && !(gatherV && dsig) &&
-                        (!gatherV || p.v_row_stride == 256) && g_rowgemm_path != 1;
-    if (dma_ok) {
-        const long long nt = ((long long)p.M + r256::TR - 1) / r256::TR;
-        long long nb = nt < 256 ? nt : 256;
-        p.tiles_per_block = (int)((nt + nb - 1) / nb);
-        nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
-        hipLaunchKernelGGL(rowgemm256_dma_kernel, dim3((unsigned)nb), dim3(512), 0, st, p, epi_rows);
-        return launch_status();
     }
     switch (a->D) {
         case 32: RGEMM(32, 2048); break;
@@ -3258,14 +2842,8 @@ int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* a) {
     const RowGemmP p = to_p(*a);
     V3Sel sel;
     if (a->D == 256 && v3_select(p, sel))
-        return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.rec ? 4 : 0) + (sel.cw ? 8 : 0) +
+        return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.cw ? 8 : 0) + (sel.split ? 2000 : 0) +
                (sel.pl ? 1000 : 0);
-    const bool gatherV = p.R > 0 && p.v_row_stride != 0;
-    const bool dsig = p.act == IDDGCN_ACT_DSIGMOID;
-    const int epi_rows = gatherV ? p.R : (dsig ? 1 : 0);
-    if (p.act != IDDGCN_ACT_DSIGMOID_COMBINE && a->D == 256 && epi_rows <= r256::EPI_MAX && !(gatherV && dsig) &&
-        (!gatherV || p.v_row_stride == 256) && g_rowgemm_path != 1)
-        return 200;
     return 100;
 }
 
@@ -3288,8 +2866,7 @@ int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
             p = to_p(a[k]);
             if (!v3_select(p, sel)) same = false;
             else if (m == 0) sel0 = sel;
-            else same = sel.nv == sel0.nv && sel.aux == sel0.aux && sel.hc == sel0.hc && sel.rec == sel0.rec &&
-                        sel.cw == sel0.cw && sel.pl == sel0.pl;
+            else same = sel.same(sel0);
             ++m;
         }
         if (same) {
@@ -3335,24 +2912,23 @@ int iddgcn_gemm_tn_blocks(long long M, int d) {
 }
 
 int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const float* B, float* slab, int n_blocks,
-                       float* C, int accumulate) {
+                       float* C, int accumulate, int precision) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (M < 0 || n_blocks < 1 || !A || !B || !slab || !C) return IDDGCN_E_BAD_ARG;
+    if (precision != IDDGCN_GEMM_EXACT_F32 && precision != IDDGCN_GEMM_SPLIT_F16) return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;
     long long rpb = (M + n_blocks - 1) / n_blocks;
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
-    if (d == 256 && g_gemm_split) {
-        hipLaunchKernelGGL(gemm_tn256_x3_kernel<false>, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab,
-                           TnSegP{}, TnBatch{});
-    } else if (d == 256 && g_rowgemm_path != 1) {
+    if (d == 256 && precision == IDDGCN_GEMM_SPLIT_F16) {
+        hipLaunchKernelGGL(gemm_tn256_x3_kernel<>, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab, TnBatch{});
+    } else if (d == 256) {
         hipLaunchKernelGGL(gemm_tn256_dma_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
     } else switch (d) {
         case 32: TNK(32); break;
         case 64: TNK(64); break;
-        case 128: TNK(128); break;
-        default: TNK(256); break;
+        default: TNK(128); break;
     }
 #undef TNK
     int rc = launch_status();
@@ -3362,14 +2938,16 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     return launch_status();
 }
 
-int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n, float* slab, long long slab_floats) {
+int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n, float* slab, long long slab_floats,
+                               int precision) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (n < 0 || n > IDDGCN_TN_BATCH || (n > 0 && (!e || !slab))) return IDDGCN_E_BAD_ARG;
+    if (precision != IDDGCN_GEMM_EXACT_F32 && precision != IDDGCN_GEMM_SPLIT_F16) return IDDGCN_E_BAD_ARG;
     for (int k = 0; k < n; ++k)
         if (e[k].M < 0 || (e[k].M > 0 && (!e[k].A || !e[k].B)) || !e[k].C) return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;
     const long long dd = (long long)d * d;
-    if (!(d == 256 && g_gemm_split)) {
+    if (!(d == 256 && precision == IDDGCN_GEMM_SPLIT_F16)) {
         // other widths and the exact mode: the single-call kernels one after another (slab reused in order)
         for (int k = 0; k < n; ++k) {
             if (e[k].M == 0) {                     // no rows: C = 0, or C unchanged when accumulating
@@ -3380,7 +2958,8 @@ int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n,
             long long nb = iddgcn_gemm_tn_blocks(e[k].M, d);
             if (nb * dd > slab_floats) nb = slab_floats / dd;           // fewer partials, longer row ranges
             if (nb < 1) return IDDGCN_E_BAD_ARG;
-            const int rc = iddgcn_gemm_tn_f32(stream, e[k].M, d, e[k].A, e[k].B, slab, (int)nb, e[k].C, e[k].accumulate);
+            const int rc = iddgcn_gemm_tn_f32(stream, e[k].M, d, e[k].A, e[k].B, slab, (int)nb, e[k].C, e[k].accumulate,
+                                              precision);
             if (rc) return rc;
         }
         return 0;
@@ -3410,8 +2989,8 @@ int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n,
     }
     if (off > slab_floats) return IDDGCN_E_BAD_ARG;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(gemm_tn256_x3_kernel<false>, dim3(nbmax, (unsigned)n), dim3(512), 0, st, 0LL, 0LL, nullptr,
-                       nullptr, nullptr, TnSegP{}, tb);
+    hipLaunchKernelGGL(gemm_tn256_x3_kernel<>, dim3(nbmax, (unsigned)n), dim3(512), 0, st, 0LL, 0LL, nullptr, nullptr,
+                       nullptr, tb);
     int rc = launch_status();
     if (rc) return rc;
     for (int k = 0; k < n; ++k) launch_reduce_slabs(st, nbk[k], dd, tb.slab[k], e[k].C, e[k].accumulate, 1.0f);
@@ -3420,33 +2999,14 @@ int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n,
 
 int iddgcn_gemm_tn_planes_f32(void* stream, long long M, int d, const void* A, const float* B, float* slab,
                               int n_blocks, float* C, int accumulate) {
-    if (d != 256 || !g_gemm_split) return IDDGCN_E_BAD_DIM;
+    if (d != 256) return IDDGCN_E_BAD_DIM;
     if (M < 0 || n_blocks < 1 || !A || !B || !slab || !C) return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;
     long long rpb = (M + n_blocks - 1) / n_blocks;
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
-    hipLaunchKernelGGL((gemm_tn256_x3_kernel<false, true>), dim3(n_blocks), dim3(512), 0, st, M, rpb,
-                       (const float*)A, B, slab, TnSegP{}, TnBatch{});
-    int rc = launch_status();
-    if (rc) return rc;
-    const long long n = (long long)d * d;
-    launch_reduce_slabs(st, n_blocks, n, slab, C, accumulate, 1.0f);
-    return launch_status();
-}
-
-int iddgcn_gemm_tn_seg_f32(void* stream, long long M, int d, const float* A, const float* B, float* slab,
-                           int n_blocks, float* C, int accumulate, const int* row_beg, const int* tail, int R,
-                           const float* W, const float* P, long long p_rel_stride, float* dP, float* dWedge,
-                           int max_tile_runs) {
-    if (d != 256 || !g_gemm_split) return IDDGCN_E_BAD_DIM;
-    if (R < 1 || R > 2) return IDDGCN_E_BAD_REL;
-    if (M < 0 || n_blocks < 1 || !A || !B || !slab || !C || !row_beg || !tail || !W || !P || !dP || !dWedge ||
-        max_tile_runs < 1 || max_tile_runs > TNSEG_CAP)
-        return IDDGCN_E_BAD_ARG;
-    hipStream_t st = (hipStream_t)stream;
-    const TnSegP sp{row_beg, tail, W, P, p_rel_stride, dP, dWedge, R};
-    hipLaunchKernelGGL(gemm_tn256_x3_kernel<true>, dim3(n_blocks), dim3(512), 0, st, M, 0LL, A, B, slab, sp, TnBatch{});
+    hipLaunchKernelGGL((gemm_tn256_x3_kernel<true>), dim3(n_blocks), dim3(512), 0, st, M, rpb, (const float*)A, B, slab,
+                       TnBatch{});
     int rc = launch_status();
     if (rc) return rc;
     const long long n = (long long)d * d;
@@ -3747,7 +3307,6 @@ int iddgcn_rowgemm_bf16(void* stream, const iddgcn_rowgemm_t* a) {
     sel.nv = a->R == 0 ? 0 : a->R == 1 ? 1 : a->R == 2 ? 2 : a->R <= 4 ? 4 : 8;
     sel.aux = dsig;
     sel.hc = a->R > 0;
-    sel.rec = false;
     RowGemmBatch pb;
     pb.p[0] = p;
     launch_v3((hipStream_t)stream, pb, 1, sel, true);

@@ -136,9 +136,8 @@ class GraphedTrainStep:
 
         def body():
             eng._t_global = t_global
-            with eng._precision():
-                eng.forward(params, adj, ed, ws, True)
-                eng.backward(params, grads, adj, ed, ws)
+            eng.forward(params, adj, ed, ws, True)
+            eng.backward(params, grads, adj, ed, ws)
             opt.apply_table(params, grads, self.alpha, self.step)
             ops.step_advance(self.step, self.losses, grads.loss)
 
@@ -170,12 +169,8 @@ class Workspace:
         f = dict(dtype=torch.float32, device=device)
         e = lambda *s: torch.empty(*s, **f)  # noqa: E731
         self.AE = e(R, N, D)
-        # [ES1 | P^1_0 .. P^1_{R-1} | P^2 .. | P^3 ..]: ES1 sits right before layer 1's P_r so that
-        # EP1 = (ES1, P^1_0, ...) is one (R+1)-table operand (x^1 recompute in the backward)
-        EP = e(1 + NUM_LAYERS * R, N, D)
-        self.ES1 = EP[0]
-        self.P = EP[1:].view(NUM_LAYERS, R, N, D)
-        self.EP1 = EP[:1 + R]
+        self.ES1 = e(N, D)                      # E·S^1 (layer-1 x·S at node level)
+        self.P = e(NUM_LAYERS, R, N, D)         # P_r^l = AE_r·K_r^l
         self.X = e(NUM_LAYERS, N, D)            # head chain X^1..X^3
         self.Ssm = e(NUM_LAYERS, N, R)
         self.W = e(NUM_LAYERS, N, R)
@@ -210,21 +205,22 @@ GEMM_MODES = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16}
 class Engine:
     """Runs forward / backward / Adam for one (graph, scored-edge batch).
 
-    ``gemm`` selects the operand precision of the D=256 MFMA GEMMs (include/iddgcn.h,
-    iddgcn_set_gemm_precision): "split" (default) splits every fp32 operand into two fp16
-    halves with power-of-two row/column scales and accumulates in fp32 (fp32-class error, 3 f16
-    MFMAs per k-step); "exact" runs v_mfma_f32_32x32x2_f32, bitwise an fmaf chain.  Other widths
-    and all non-GEMM kernels are exact f32 in both modes.
+    ``gemm`` selects the operand precision of the D=256 MFMA GEMMs, passed with every GEMM call
+    (include/iddgcn.h IDDGCN_GEMM_*, ABI 6: no process-global state, so engines in different modes may
+    run side by side on different streams or threads): "exact" (default) runs v_mfma_f32_32x32x2_f32,
+    bitwise an fmaf chain — the reference's fp32 arithmetic; "split" splits every fp32 operand into two
+    fp16 halves with power-of-two row/column scales and accumulates in fp32 (within one fp32 ulp per
+    operand, 3 f16 MFMAs per k-step), an opt-in faster mode.  Other widths and all non-GEMM kernels are
+    exact f32 in both modes.
     """
 
-    def __init__(self, num_entities, num_relations, dim, device=None, gemm="split", recompute_x1=False,
-                 fuse_tail_seg=False, features="f32", planes=True):
+    def __init__(self, num_entities, num_relations, dim, device=None, gemm="exact", features="f32", planes=True):
         if dim not in (32, 64, 128, 256):
             raise L.IddgcnError("embedding dim must be one of 32, 64, 128, 256")
         if features not in ("f32", "bf16"):
             raise L.IddgcnError("features must be 'f32' or 'bf16'")
-        if features == "bf16" and (dim != 256 or recompute_x1 or fuse_tail_seg):
-            raise L.IddgcnError("the bf16-feature mode is D=256 only, without recompute_x1 / fuse_tail_seg")
+        if features == "bf16" and dim != 256:
+            raise L.IddgcnError("the bf16-feature mode is D=256 only")
         # bf16-feature mode (BASELINE config 5, perf only): the edge tables x^l / do^l stored as bf16 and
         # the edge GEMMs on bf16 MFMA; node tables, weights, accumulation and epilogues stay fp32
         self.features = features
@@ -235,13 +231,6 @@ class Engine:
             raise L.IddgcnError(f"gemm must be one of {sorted(GEMM_MODES)}")
         self.N, self.R, self.D = num_entities, num_relations, dim
         self.gemm = gemm
-        # layer-2 backward: rebuild sigma'(x^1) from node tables instead of re-reading x^1 (4.1 GB
-        # less HBM traffic per step at config 3, but ~6% slower per launch: off by default)
-        self.recompute_x1 = recompute_x1
-        # layers 2-3 backward: tail segmented reduction fused into the dS pass (do read once; 8.2 GB
-        # less HBM traffic per step at config 3, but the per-tile scan is serial with the TN pipeline:
-        # 3.9 ms vs 2.0 + 0.9 ms unfused, so off by default)
-        self.fuse_tail_seg = fuse_tail_seg
         # pre-split tail tables x^1, x^2 (include/iddgcn.h IDDGCN_PLANES_*): their producers (layer-1
         # combine, layer-2 forward GEMM) write [hi | lo] fp16 rows once, so the forward GEMMs of layers 2-3,
         # the dS TN GEMMs and the sigma' backward skip their per-tile conversion (see use_planes)
@@ -254,19 +243,20 @@ class Engine:
         self.probe = None      # {name: [(start_event, end_event), ...]} when timing kernels
 
     @property
+    def gemm(self):
+        return self._gemm
+
+    @gemm.setter
+    def gemm(self, mode):
+        if mode not in GEMM_MODES:
+            raise L.IddgcnError(f"gemm must be one of {sorted(GEMM_MODES)}")
+        self._gemm = mode
+
+    @property
     def use_planes(self):
         """x^1, x^2 are stored pre-split: split GEMM mode at D = 256 with fp32 features, R <= 2 (the
-        gathered forward's planes form), not with the fused tail segmented reduction."""
-        return (self.planes and self.gemm == "split" and self.D == 256 and self.features == "f32" and self.R <= 2
-                and not self.fuse_tail_seg)
-
-    @contextlib.contextmanager
-    def _precision(self):
-        old = L.lib().iddgcn_set_gemm_precision(GEMM_MODES[self.gemm])
-        try:
-            yield
-        finally:
-            L.lib().iddgcn_set_gemm_precision(old)
+        gathered forward's planes form)."""
+        return self.planes and self.gemm == "split" and self.D == 256 and self.features == "f32" and self.R <= 2
 
     @contextlib.contextmanager
     def _mark(self, name):
@@ -290,6 +280,11 @@ class Engine:
         """Scored-edge layout, built on the GPU (iddgcn_build_scored_edges)."""
         return ScoredEdges.from_triples(triples, labels, self.N, self.R, self.device)
 
+    def release(self):
+        """Drop the cached workspaces (their device memory goes back to torch's caching allocator): a
+        predict workspace and a training workspace of a 40M-edge batch do not fit one GPU together."""
+        self._ws = {}
+
     def workspace(self, T, train):
         key = (T, train)
         if key not in self._ws:
@@ -306,6 +301,7 @@ class Engine:
     def forward(self, P, adj, ed, ws, train):
         N, R, D, T = self.N, self.R, self.D, ed.T
         E = P["E"]
+        pk = dict(precision=self.gemm)          # every GEMM call carries this engine's operand precision
         sh = self.node_shard
         if sh is None and self.spmm_shard is not None:
             # row-partitioned A_r·E (every rank holds E): this rank's (relation, row) pieces, then all-gather
@@ -314,21 +310,21 @@ class Engine:
                 ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + n0:r * (N + 1) + n1 + 1], adj.fwd_col, adj.fwd_val, E,
                              ws.AE[r][n0:n1].view(1, n1 - n0, D), 1, n1 - n0)
             ss.all_gather(ws.AE.view(R * N, D))
-            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], {}) for l in range(NUM_LAYERS) for r in range(R)]
+            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], pk) for l in range(NUM_LAYERS) for r in range(R)]
         elif sh is None:
             # AE_r = A_r·E, all relations in one launch (IDDGCN.py:69-70)
             ops.spmm_csr(adj.fwd_ptr, adj.fwd_col, adj.fwd_val, E, ws.AE, R, N)
             # P_r^l = AE_r·K_r^l (node-level form of IDDGCN.py:71-72,76-77) and, layer 1, x·S1 at node
             # level for both sides (inputs E[h], E[t]): independent GEMMs, batched (one launch below D=256)
-            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], {}) for l in range(NUM_LAYERS) for r in range(R)]
+            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], pk) for l in range(NUM_LAYERS) for r in range(R)]
         else:
             # relation-sharded: this rank's (relation, node-row) pieces of AE_r and P_r^l, then all-gather P
             proj = []
             for r, n0, n1 in sh.pieces():
                 ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + n0:r * (N + 1) + n1 + 1], adj.fwd_col, adj.fwd_val, E,
                              ws.AE[r][n0:n1].view(1, n1 - n0, D), 1, n1 - n0)
-                proj += [(ws.AE[r][n0:n1], P[f"K{l + 1}"][r], ws.P[l, r][n0:n1], {}) for l in range(NUM_LAYERS)]
-        proj.append((E, P["S1"], ws.ES1, {}))
+                proj += [(ws.AE[r][n0:n1], P[f"K{l + 1}"][r], ws.P[l, r][n0:n1], pk) for l in range(NUM_LAYERS)]
+        proj.append((E, P["S1"], ws.ES1, pk))
         for i in range(0, len(proj), 16):
             ops.rowgemm_batched(proj[i:i + 16])
         if sh is not None:
@@ -345,11 +341,11 @@ class Engine:
             ops.alpha_fwd(ws.X[l - 1], P[f"Wa{l + 1}"], P[f"ba{l + 1}"], ws.Ssm[l], ws.W[l])
             ops.gather_rows(ws.W[l], ed.h, ws.Wedge[l])
             ops.rowgemm(ws.X[l - 1], S, ws.X[l], coef=ws.W[l], V=ws.P[l], v_rel_stride=N * D,
-                        act=L.ACT_SIGMOID)
+                        act=L.ACT_SIGMOID, **pk)
             with self._mark("tail_fwd_gemm"):
                 ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID,
-                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0)
+                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, **pk)
         # DistMult (+ BCE and backward seed when training)
         if train:
             # one pass over head segments: p / loss / drel partials, the tail seed do^3 (per edge)
@@ -376,6 +372,7 @@ class Engine:
         small gradients + the loss after the layer loop, then row chunks of dE as the transposed SpMM
         produces them, so the all-reduce of the large dE overlaps the SpMM of the next chunk."""
         N, R, D = self.N, self.R, self.D
+        pk = dict(precision=self.gemm)
         dOn, dOn_next = ws.dOn_a, ws.dOn_b      # head seed dO^3, written by distmult_bce_heads
         if self.node_shard is not None:
             ws.dAE.zero_()                      # rows other ranks own stay 0 in the dE SpMM below
@@ -383,30 +380,16 @@ class Engine:
         for l in (2, 1, 0):                     # layer index l -> reference layer l+1
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
             do = ws.xt[l]                       # do^{l+1}, written over x^{l+1}
-            # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part; for layers 2-3 the
-            # fused kernel does it inside the dS pass (do read once)
-            seg = self._tn_seg(ed) if l > 0 else None
-            if seg is None:
-                ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
-                                    dsum=ws.dES if l == 0 else None)
+            # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part
+            ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
+                                dsum=ws.dES if l == 0 else None)
             if l > 0:
                 # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x), written over x^{l}
                 with self._mark("tail_dS_tn"):
-                    if seg is not None:
-                        ops.gemm_tn_seg(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, seg[0], ed.t, ws.Wedge[l], Pl,
-                                        ws.dP, ws.dWedge, seg[1])
-                    else:
-                        ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl)
-                rec = l == 1 and self._recompute_ok(ed)
-                with self._mark("tail_bwd_rec_gemm" if rec else "tail_bwd_gemm"):
-                    if rec:
-                        # x^1 = sigmoid(ES1[t] + sum_r W^1[h,r] P^1_r[t]) rebuilt on chip (forward, above)
-                        ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID_COMBINE,
-                                    coef=ws.Wedge[0], V=ws.EP1, v_idx=ed.t, v_rel_stride=N * D,
-                                    v_runs_max=ed.tail_runs32)
-                    else:
-                        ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
-                                    planes=L.PLANES_AUX if pl else 0)
+                    ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)
+                with self._mark("tail_bwd_gemm"):
+                    ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
+                                planes=L.PLANES_AUX if pl else 0, **pk)
             # head side (node level)
             ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
                               dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)
@@ -421,17 +404,17 @@ class Engine:
             if sh is None:
                 tn += [(ws.AE[r], ws.dP[r], dK[r], False) for r in range(R)]
             for i in range(0, len(tn), L.TN_BATCH):
-                ops.gemm_tn_batched(tn[i:i + L.TN_BATCH], ws.tn_slab)
+                ops.gemm_tn_batched(tn[i:i + L.TN_BATCH], ws.tn_slab, **pk)
             if l > 0:
                 ops.rowgemm(dOn, Sl, dOn_next, b_trans=True, coef=ws.dz, V=ws.WaT, v_rel_stride=D,
-                            v_row_stride=0, act=L.ACT_DSIGMOID, aux=Xin)
+                            v_row_stride=0, act=L.ACT_DSIGMOID, aux=Xin, **pk)
             else:
                 # dE (head input of layer 1 + x·S1 inputs of both sides)
                 ops.rowgemm(ws.dES, Sl, G["E"], b_trans=True, coef=ws.dz, V=ws.WaT, v_rel_stride=D,
-                            v_row_stride=0)
+                            v_row_stride=0, **pk)
             # relation kernels: dK_r = AE_r^T dP_r (above) ; dAE_r += dP_r K_r^T
             if sh is None:
-                ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2)))
+                ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2), **pk))
                                      for r in range(R)])
             else:
                 # relation-sharded: the owners sum the edge partials of dP, then form their rows of dK_r (a
@@ -439,9 +422,9 @@ class Engine:
                 sh.reduce_scatter(ws.dP.view(R * N, D))
                 dK.zero_()
                 for r, n0, n1 in sh.pieces():
-                    ops.gemm_tn(ws.AE[r][n0:n1], ws.dP[r][n0:n1], dK[r], ws.tn_slab, accumulate=True)
-                ops.rowgemm_batched([(ws.dP[r][n0:n1], K[r], ws.dAE[r][n0:n1], dict(b_trans=True, accumulate=True))
-                                     for r, n0, n1 in sh.pieces()])
+                    ops.gemm_tn(ws.AE[r][n0:n1], ws.dP[r][n0:n1], dK[r], ws.tn_slab, accumulate=True, **pk)
+                ops.rowgemm_batched([(ws.dP[r][n0:n1], K[r], ws.dAE[r][n0:n1],
+                                      dict(b_trans=True, accumulate=True, **pk)) for r, n0, n1 in sh.pieces()])
             dOn, dOn_next = dOn_next, dOn
         # DistMult rel grad and the loss: every gradient past E is final now
         ops.reduce_slabs(ws.drel_slab, ws.nb_dm, G["rel"])
@@ -463,19 +446,6 @@ class Engine:
             if comm is not None:
                 comm.ready(G["E"][n0:n1].reshape(-1))
 
-    def _tn_seg(self, ed):
-        """(row_beg, max tile runs) when the fused dS + tail segmented reduction applies: D=256 in the
-        split-fp16 GEMM mode, R <= 2, at most ops.TN_SEG_CAP distinct tails per tile; else None."""
-        if not (self.fuse_tail_seg and self.D == 256 and self.gemm == "split" and self.R <= 2 and ed.T > 0):
-            return None
-        rb, runs = ed.tn_seg_layout(ops.tn_blocks(ed.T, self.D))
-        return (rb, runs) if 1 <= runs <= ops.TN_SEG_CAP else None
-
-    def _recompute_ok(self, ed):
-        """The x^1-recompute GEMM runs when it takes the D=256 on-chip path (<= 8 tail runs per
-        32-edge block); other shapes re-read x^1 (the generic kernel would be slower)."""
-        return self.recompute_x1 and self.D == 256 and 1 <= ed.tail_runs32 <= 8
-
     # -- public steps ---------------------------------------------------------
     def train_step(self, params, grads, opt, adj, ed, t_global=None, comm=None):
         """One full-batch step (IDDGCN.py:123-178).  Returns the device scalar (grads.loss) holding the
@@ -483,9 +453,8 @@ class Engine:
         all-reduce (parallel.BucketedAllReduce), overlapped with the end of the backward."""
         ws = self.workspace(ed.T, True)
         self._t_global = t_global
-        with self._precision():
-            self.forward(params, adj, ed, ws, True)
-            self.backward(params, grads, adj, ed, ws, comm)
+        self.forward(params, adj, ed, ws, True)
+        self.backward(params, grads, adj, ed, ws, comm)
         if comm is not None:
             comm.finish()
         opt.apply(params, grads)
@@ -495,8 +464,7 @@ class Engine:
         """Probabilities p = sigmoid(s) of the scored edges (caller's order); with ``logits=True``
         also the pre-sigmoid DistMult scores s (IDDGCN.py:108)."""
         ws = self.workspace(ed.T, False)
-        with self._precision():
-            self.forward(params, adj, ed, ws, False)
+        self.forward(params, adj, ed, ws, False)
         return (ed.unsort(ws.p), ed.unsort(ws.s)) if logits else ed.unsort(ws.p)
 
     def layer_outputs(self, ed, rows=None):
@@ -518,12 +486,10 @@ class Engine:
         self._t_global = t_global
         self._want_p = True
         try:
-            with self._precision():
-                self.forward(params, adj, ed, ws, True)
+            self.forward(params, adj, ed, ws, True)
         finally:
             self._want_p = False
-        with self._precision():
-            self.backward(params, grads, adj, ed, ws)
+        self.backward(params, grads, adj, ed, ws)
         if logits:
             return grads.loss, ed.unsort(ws.p), ed.unsort(ws.s)
         return grads.loss, ed.unsort(ws.p)
@@ -546,11 +512,14 @@ class Engine:
             if getattr(self, "_scratch_grads", None) is None:
                 self._scratch_grads = FlatParams(N, R, D, self.device)
             grads = self._scratch_grads
+        if self.node_shard is not None or self.spmm_shard is not None:
+            # a sharded backward leaves only this rank's rows of dAE (or its reduce-scattered range): the
+            # SDDMM below needs the full per-rank dAE
+            raise L.IddgcnError("value_grads: not available on an Engine with node_shard / spmm_shard set")
         self._pred_seed, self._want_p = float(scale), True
         try:
-            with self._precision():
-                self.forward(params, adj, ed, ws, True)
-                self.backward(params, grads, adj, ed, ws)
+            self.forward(params, adj, ed, ws, True)
+            self.backward(params, grads, adj, ed, ws)
         finally:
             self._pred_seed, self._want_p = None, False
         dv = torch.empty(adj.total_nnz, dtype=torch.float32, device=self.device)

@@ -91,8 +91,6 @@ class _SingleEdge:
     """A one-triple ScoredEdges whose device arrays are rewritten in place from a device (3,) int64
     triple (so a captured graph can be replayed for any triple)."""
 
-    tail_runs32 = 1            # one edge: one tail run
-
     def __init__(self, eng, triple_buf):
         self.T, self.y = 1, None
         dev = eng.device

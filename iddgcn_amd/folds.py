@@ -117,7 +117,9 @@ def make_fold(data_dir, fold, mode=0, seed=89, num_splits=5):
     tr_pos, te_pos = split_pos_triple_into_folds(resp, mu, dr, num_splits, seed, mode)[fold]
     tr_neg, te_neg = split_neg_triple_into_folds(neg, num_splits, seed, mode)[fold]
     te_neg_f = te_neg[te_neg["rel"].isin([0, 1])]
-    te_pos = te_pos[~te_pos["rel"].isin([2, 3])]
+    # IDDGCN.py:344 drops the rel 2/3 test rows BY INDEX LABEL: in the cold-start modes the test frame keeps
+    # the repeated labels of concat([dc, dd, cc]), so response rows sharing a label with one go too
+    te_pos = te_pos.drop(te_pos[te_pos["rel"].isin([2, 3])].index)
     X_train = pd.concat([tr_pos, reverse_triples(tr_pos)], axis=0).astype(np.int64)
     X_test = pd.concat([te_pos, reverse_triples(te_pos)], axis=0).astype(np.int64)
     X_train_neg = pd.concat([tr_neg, reverse_triples(tr_neg)], axis=0)

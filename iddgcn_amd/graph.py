@@ -298,55 +298,6 @@ class ScoredEdges:
         self.order = None
         return self
 
-    _runs32 = None
-
-    @property
-    def tail_runs32(self):
-        """Most runs of equal tail in any aligned 32-edge block (0 for no edges).  The D=256 row
-        GEMM that recomputes the layer-1 tail activation keeps at most 8 distinct tail rows of a
-        block on chip (include/iddgcn.h, IDDGCN_ACT_DSIGMOID_COMBINE)."""
-        if self._runs32 is None:
-            T = self.T
-            if T == 0:
-                self._runs32 = 0
-            else:
-                t = self.t
-                start = torch.zeros((T + 31) // 32 * 32, dtype=torch.int32, device=t.device)
-                start[:T] = 1
-                start[1:T] = (t[1:] != t[:-1]).int()
-                start[0:T:32] = 1
-                self._runs32 = int(start.view(-1, 32).sum(1).max().item())
-        return self._runs32
-
-    _tn_seg = None
-
-    def tn_seg_layout(self, n_blocks):
-        """Row ranges of n_blocks TN blocks that start at tail-segment starts (each tail's edges in
-        one block) and the most distinct tails in any 32-row tile of those ranges, for the fused
-        dS + tail segmented reduction (ops.gemm_tn_seg).  Cached per n_blocks."""
-        if self._tn_seg is None or self._tn_seg[0] != n_blocks:
-            T, t = self.T, self.t
-            dev = t.device
-            k = torch.arange(n_blocks + 1, device=dev, dtype=torch.int64) * T // n_blocks
-            if T > 0:
-                kc = k.clamp(max=T - 1)
-                inner = (k > 0) & (k < T)
-                same = inner & (t[kc] == t[(k - 1).clamp(min=0)])
-                k = torch.where(same, self.tptr[t[kc].long() + 1].long(), k)
-            row_beg = k.to(torch.int32).contiguous()
-            runs = 0
-            if T > 0:
-                e = torch.arange(T, device=dev, dtype=torch.int64)
-                blk = torch.bucketize(e, k, right=True) - 1
-                local = e - k[blk]
-                first = (local % 32) == 0
-                start = first.clone()
-                start[1:] |= t[1:] != t[:-1]
-                tile = torch.cumsum(first.long(), 0) - 1
-                runs = int(torch.bincount(tile, weights=start.double()).max().item())
-            self._tn_seg = (n_blocks, row_beg, runs)
-        return self._tn_seg[1], self._tn_seg[2]
-
     def unsort(self, x):
         """Sorted-order per-edge tensor -> caller's order."""
         return x[self.inv]

@@ -24,6 +24,17 @@ def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+_PRECISION = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16,
+              L.GEMM_EXACT_F32: L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16: L.GEMM_SPLIT_F16}
+
+
+def _prec(precision):
+    """GEMM operand precision of one call (include/iddgcn.h IDDGCN_GEMM_*): "exact" / "split" or the constant."""
+    if precision not in _PRECISION:
+        raise L.IddgcnError(f"precision must be 'exact' or 'split', got {precision!r}")
+    return _PRECISION[precision]
+
+
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -93,8 +104,8 @@ def rowgemm(A, B, C, **kw):
 
 
 def rowgemm_kernel_id(A, B, C, **kw):
-    """Which kernel rowgemm(A, B, C, **kw) runs (iddgcn_rowgemm_kernel_id): 300 + 10*NV + ... for the D=256
-    v3 pipeline, 200 the v2 LDS-DMA kernel, 100 the register-staged one."""
+    """Which kernel rowgemm(A, B, C, **kw) runs (iddgcn_rowgemm_kernel_id): 300 + 10*NV + ... (+2000 split
+    operands) for the D=256 v3 pipeline, 100 the register-staged one."""
     args = _rowgemm_args(A, B, C, **kw)
     return int(L.lib().iddgcn_rowgemm_kernel_id(ctypes.byref(args)))
 
@@ -109,13 +120,12 @@ def rowgemm_batched(calls):
 
 
 def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, coef_idx=None, V=None,
-                  v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None, v_runs_max=0,
-                  planes=0):
-    """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32).  act=ACT_DSIGMOID_COMBINE
-    multiplies by x(1-x) with x = sigmoid(V_0[v_idx] + sum_r coef_r V_{r+1}[v_idx]) (V: R+1 tables);
-    v_runs_max bounds the runs of equal v_idx per aligned 32-row block (0 = unknown).  planes: L.PLANES_*
-    flags, which of A / C / aux are pre-split planes tables (fp32-shaped tensors holding [hi | lo] fp16
-    rows; D = 256, split GEMM mode)."""
+                  v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None, planes=0,
+                  precision="exact"):
+    """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32).  planes: L.PLANES_* flags,
+    which of A / C / aux are pre-split planes tables (fp32-shaped tensors holding [hi | lo] fp16 rows;
+    D = 256, split GEMM mode).  precision: "exact" (v_mfma_f32_32x32x2_f32) or "split" (split-fp16
+    operands), per call (D = 256; other widths are exact f32)."""
     D = B.shape[0]
     M = C.shape[0] if M is None else M
     R = 0 if coef is None else coef.shape[-1]
@@ -137,24 +147,22 @@ def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=
         _idx_ok(v_idx, M, vrows, "v_idx")
     if act == L.ACT_DSIGMOID:
         _req(aux, et, (M, D), "aux")
-    if act == L.ACT_DSIGMOID_COMBINE:
-        if not R or V is None or V.numel() < (R + 1) * int(v_rel_stride):
-            raise L.IddgcnError("ACT_DSIGMOID_COMBINE needs coef (R columns) and R+1 V tables")
     return L.RowGemmArgs(
         M=M, D=D, A=_ptr(A), a_idx=_ptr(a_idx), B=_ptr(B), b_trans=int(b_trans), C=_ptr(C),
         accumulate=int(accumulate), R=R, coef=_ptr(coef), coef_idx=_ptr(coef_idx), V=_ptr(V),
         v_idx=_ptr(v_idx), v_rel_stride=int(v_rel_stride),
         v_row_stride=int(D if v_row_stride is None else v_row_stride), act=int(act), aux=_ptr(aux),
-        v_runs_max=int(v_runs_max), planes=int(planes))
+        planes=int(planes), precision=_prec(precision))
 
 
 def tn_blocks(M, D):
     return int(L.lib().iddgcn_gemm_tn_blocks(int(M), int(D)))
 
 
-def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False):
+def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False, precision="exact"):
     """C (+)= A^T B; bf16 A and B (the bf16-feature mode) select iddgcn_gemm_tn_bf16; a_planes: A is a
-    pre-split planes table (iddgcn_gemm_tn_planes_f32, D = 256, split GEMM mode)."""
+    pre-split planes table (iddgcn_gemm_tn_planes_f32, D = 256, split GEMM mode); precision: the fp32 form's
+    operand precision ("exact" / "split", D = 256)."""
     M, D = A.shape
     et = _BF16 if A.dtype == _BF16 else _F32
     _req(A, et, (M, D), "A")
@@ -163,48 +171,22 @@ def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False):
     nb = tn_blocks(M, D)
     if slab.numel() < nb * D * D:
         raise L.IddgcnError("gemm_tn slab too small")
+    args = (_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C), int(accumulate))
     if a_planes:
-        if et != _F32:
-            raise L.IddgcnError("gemm_tn: planes A takes an fp32-shaped table")
-        fn = L.lib().iddgcn_gemm_tn_planes_f32
+        if et != _F32 or _prec(precision) != L.GEMM_SPLIT_F16:
+            raise L.IddgcnError("gemm_tn: planes A takes an fp32-shaped table in the split mode")
+        rc = L.lib().iddgcn_gemm_tn_planes_f32(*args)
+    elif et == _BF16:
+        rc = L.lib().iddgcn_gemm_tn_bf16(*args)
     else:
-        fn = L.lib().iddgcn_gemm_tn_bf16 if et == _BF16 else L.lib().iddgcn_gemm_tn_f32
-    L.check(fn(_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C), int(accumulate)), "gemm_tn")
+        rc = L.lib().iddgcn_gemm_tn_f32(*args, _prec(precision))
+    L.check(rc, "gemm_tn")
 
 
-TN_SEG_CAP = 6   # distinct tails per 32-row tile the fused kernel stages on chip (include/iddgcn.h)
-
-
-def gemm_tn_seg(A, B, C, slab, row_beg, tail, W, P, dP, dWedge, max_tile_runs, accumulate=False):
-    """C = A^T B fused with the tail-side segmented reduction of B (iddgcn_gemm_tn_seg_f32):
-    dP[r][t] = sum_{tail[e]=t} W[e,r] B[e], dWedge[e,r] = <B[e], P[r][tail[e]]>.  row_beg: block row
-    ranges aligned to tail-segment starts (graph.ScoredEdges.tn_seg_layout); dP zeroed here."""
-    M, D = A.shape
-    R = W.shape[1]
-    _req(A, _F32, (M, D), "A")
-    _req(B, _F32, (M, D), "B")
-    _req(C, _F32, (D, D), "C")
-    _req(row_beg, _I32, None, "row_beg")
-    _req(tail, _I32, (M,), "tail")
-    _req(W, _F32, (M, R), "W")
-    _req(P, _F32, None, "P")
-    _req(dP, _F32, tuple(P.shape), "dP")
-    _req(dWedge, _F32, (M, R), "dWedge")
-    nb = row_beg.shape[0] - 1
-    if P.dim() != 3 or P.shape[0] != R or P.shape[2] != D:
-        raise L.IddgcnError("gemm_tn_seg: P must be (R, N, D)")
-    if slab.numel() < nb * D * D:
-        raise L.IddgcnError("gemm_tn_seg slab too small")
-    dP.zero_()
-    L.check(L.lib().iddgcn_gemm_tn_seg_f32(_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C),
-                                           int(accumulate), _ptr(row_beg), _ptr(tail), R, _ptr(W), _ptr(P),
-                                           P.shape[1] * D, _ptr(dP), _ptr(dWedge), int(max_tile_runs)),
-            "gemm_tn_seg")
-
-
-def gemm_tn_batched(entries, slab):
+def gemm_tn_batched(entries, slab, precision="exact"):
     """Up to L.TN_BATCH independent C (+)= A^T B, entries = [(A, B, C, accumulate), ...] (fp32, same D), in one
-    launch (iddgcn_gemm_tn_batched_f32, ABI 5); slab holds the partials of all entries."""
+    launch (iddgcn_gemm_tn_batched_f32, ABI 5; one launch at D = 256 in the split mode); slab holds the
+    partials of all entries."""
     if not entries:
         return
     if len(entries) > L.TN_BATCH:
@@ -218,8 +200,8 @@ def gemm_tn_batched(entries, slab):
         _req(C, _F32, (D, D), "C")
         arr[k] = L.TnArgs(M, _ptr(A), _ptr(B), _ptr(C), int(bool(acc)))
     _req(slab, _F32, None, "slab")
-    L.check(L.lib().iddgcn_gemm_tn_batched_f32(_stream(), D, arr, len(entries), _ptr(slab), slab.numel()),
-            "gemm_tn_batched")
+    L.check(L.lib().iddgcn_gemm_tn_batched_f32(_stream(), D, arr, len(entries), _ptr(slab), slab.numel(),
+                                               _prec(precision)), "gemm_tn_batched")
 
 
 def tn_narrow_blocks(M):

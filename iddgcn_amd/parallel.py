@@ -40,16 +40,19 @@ class BucketedAllReduce:
     already queued on the current stream, so it overlaps whatever is queued next; ``finish()`` makes
     the current stream wait for all of them.  ``row_chunks(N)`` is how the engine splits dE (N rows)
     into buckets: each at least ``min_bucket_rows`` rows, at most ``max_chunks`` of them (RCCL over
-    xGMI runs per-link bound rings; a handful of large buckets keeps every ring busy)."""
+    xGMI runs per-link bound rings; a handful of large buckets keeps every ring busy).
 
-    def __init__(self, group=None, max_chunks=4, min_bucket_rows=4096):
+    ``host_staged``: None (default) stages GPU buckets through host memory, synchronously, on a gloo group
+    (several ranks sharing one GPU in tests) and reduces them in place on the device on RCCL ("nccl");
+    False forces the device branch on any backend (gloo's all_reduce takes GPU tensors too, so the tests
+    run the asynchronous in-place path the RCCL ranks take); True forces host staging."""
+
+    def __init__(self, group=None, max_chunks=4, min_bucket_rows=4096, host_staged=None):
         self.group = group
         self.max_chunks = max_chunks
         self.min_bucket_rows = min_bucket_rows
         self._works = []
-        # a gloo group (CPU collectives, e.g. several ranks sharing one GPU in a test) gets GPU buckets
-        # staged through host memory, synchronously; RCCL ("nccl") reduces them in place on the device
-        self._host_staged = None
+        self._host_staged = host_staged
 
     def row_chunks(self, n_rows):
         k = max(1, min(self.max_chunks, n_rows // max(1, self.min_bucket_rows)))

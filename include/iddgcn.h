@@ -16,7 +16,10 @@
  *   - `stream` is a hipStream_t passed as void*; NULL = default stream;
  *   - return 0 on success, a positive hipError_t on a launch error, or a
  *     negative IDDGCN_E* code on invalid arguments (nothing is launched then);
- *   - feature width D must be one of 32, 64, 128, 256; relations R <= 8.
+ *   - feature width D must be one of 32, 64, 128, 256; relations R <= 8;
+ *   - re-entrant: no process-global state.  Every option (the GEMM operand
+ *     precision included) travels with its call, so calls on different streams,
+ *     devices or host threads do not interact (ABI 6).
  */
 #ifndef IDDGCN_H_
 #define IDDGCN_H_
@@ -25,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 5
+#define IDDGCN_ABI_VERSION 6
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -35,12 +38,18 @@ extern "C" {
 #define IDDGCN_ACT_NONE     0
 #define IDDGCN_ACT_SIGMOID  1
 #define IDDGCN_ACT_DSIGMOID 2     /* v *= aux * (1 - aux)   (sigmoid backward) */
-/* v *= x * (1 - x) with x = sigmoid(V_0[v_idx] + sum_{r<R} coef[r] * V_{r+1}[v_idx]) recomputed
- * from node tables (the layer-1 tail activation, IDDGCN.py:62-79, without re-reading it):
- * V holds R + 1 tables of v_rel_stride floats, aux is unused.  v_runs_max > 0 asserts that no
- * aligned 32-row block of v_idx holds more runs of equal values than that; the D = 256 kernel
- * needs <= 8 (tail-sorted edges), any other input takes the generic kernel. */
-#define IDDGCN_ACT_DSIGMOID_COMBINE 3
+
+/* Operand precision of the D = 256 MFMA GEMMs (iddgcn_rowgemm_t.precision, the TN entries' `precision`):
+ *   IDDGCN_GEMM_EXACT_F32 (0, the default of a zero-initialised struct): v_mfma_f32_32x32x2_f32, bitwise an
+ *     fmaf chain (the reference's fp32 arithmetic);
+ *   IDDGCN_GEMM_SPLIT_F16: each operand row (A) / column (B) is scaled by a power of two so its max lies in
+ *     [2^14, 2^15), every value is split as hi + lo (two fp16, 22-23 significant bits: within one fp32 ulp
+ *     of the value), and hi*hi + hi*lo + lo*hi runs on v_mfma_f32_32x32x16_f16 with fp32 accumulation; the
+ *     power-of-two scales are undone exactly in the epilogue.  An opt-in faster mode: results are
+ *     deterministic but not bitwise equal to the exact mode.
+ * Row GEMMs for D < 256 and every other kernel always compute in exact f32. */
+#define IDDGCN_GEMM_EXACT_F32 0
+#define IDDGCN_GEMM_SPLIT_F16 1
 
 /* Pre-split edge tables ("planes", ABI 4; D = 256, split-fp16 GEMM mode only).  A row of values in
  * [0, 1] (sigmoid outputs) stored as 8 column blocks of 128 B, block b = [hi f16 of columns 32b..32b+31 |
@@ -81,6 +90,7 @@ int iddgcn_sddmm_csr_f32(void* stream, int n_seg, int n_rows, int d,
  *                  * V[r*v_rel_stride + (v_idx ? v_idx[e] : e)*v_row_stride + c]
  *   C[e][c] = act(v)   (NONE | SIGMOID | DSIGMOID with aux[e][c]; C may alias aux: the backward
  *                       writes do^{l-1} over its sigma' operand x^{l-1})
+ * at the operand precision `precision` (IDDGCN_GEMM_*; D = 256 only, other widths are exact f32)
  * Replaces IDDGCN.py:62-63 + 71-79 (x·S, + sigmoid(alpha_r)·(AE_r[idx]·K_r), sigmoid)
  * with P_r = AE_r·K_r precomputed at node level, and the matching backward GEMMs. */
 typedef struct {
@@ -93,46 +103,29 @@ typedef struct {
     const float* V; const int* v_idx;
     long long v_rel_stride, v_row_stride;
     int act; const float* aux;
-    int v_runs_max;       /* bound on runs of equal v_idx per aligned 32-row block, 0 = unknown (the
-                             D = 256 x^1 recompute, IDDGCN_ACT_DSIGMOID_COMBINE, needs it) */
     int planes;           /* IDDGCN_PLANES_* flags (ABI 4; 0 = every table fp32).  Nonzero needs D = 256,
                              the split-fp16 mode and no a_idx; invalid combinations return IDDGCN_E_BAD_ARG */
+    int precision;        /* IDDGCN_GEMM_EXACT_F32 (0) or IDDGCN_GEMM_SPLIT_F16 (ABI 6: per call) */
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 
 /* Which kernel iddgcn_rowgemm_f32 would run for these arguments (a test / benchmark hook; nothing is
- * launched): 300 + 10*NV + aux + 2*coef + 4*recompute + 8*(broadcast V with R > 2 coefficients)
- * + 1000 for the planes form (C or aux planes) for the D = 256 v3 pipeline (NV = gathered V
+ * launched): 300 + 10*NV + aux + 2*coef + 8*(broadcast V with R > 2 coefficients) + 1000 for the planes
+ * form (C or aux planes) + 2000 for split-fp16 operands, for the D = 256 v3 pipeline (NV = gathered V
  * tables: 1, 2, or capacity 4 / 8 for R <= 8, whose LDS slabs keep 7 distinct V rows per 32-row tile
- * and read further ones from L2), 200 for the v2 LDS-DMA row GEMM, 100 for the register-staged kernel
- * (any D, any V order), -1 for an invalid D. */
+ * and read further ones from L2); 100 for the register-staged kernel (D < 256, and D = 256 forms the v3
+ * kernel does not take: a gathered V with the sigma' epilogue, V rows that are not dense); -1 for an
+ * invalid D. */
 int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* args);
-
-/* Select the D=256 GEMM pipelines (host-side switch for A/B tests and benchmarks;
- * all paths are bitwise identical): 0 (default) = staggered v3 row GEMM + LDS-DMA TN GEMM,
- * 1 = register-staged kernels, 2 = v2 LDS-DMA row GEMM.  Returns the previous setting. */
-int iddgcn_set_rowgemm_path(int path);
-
-/* Operand precision of the D=256 row GEMMs (process-wide; returns the previous mode):
- *   IDDGCN_GEMM_EXACT_F32 (default): v_mfma_f32_32x32x2_f32, bitwise an fmaf chain;
- *   IDDGCN_GEMM_SPLIT_F16: each operand row (A) / column (B) is scaled by a power of two so its
- *     max lies in [2^14, 2^15), every value is split as hi + lo*2^-11 (two fp16, 22 significant
- *     bits), and hi*hi + 2^-11 (hi*lo + lo*hi) runs on v_mfma_f32_32x32x16_f16 with fp32
- *     accumulation; the power-of-two scales are undone exactly in the epilogue.  Accuracy is
- *     fp32-class (operand error <= 2^-22 relative, below the K=256 fp32 summation error);
- *     results are deterministic but not bitwise equal to the exact mode.
- * Row GEMMs for D < 256 and every other kernel always compute in exact f32. */
-#define IDDGCN_GEMM_EXACT_F32 0
-#define IDDGCN_GEMM_SPLIT_F16 1
-int iddgcn_set_gemm_precision(int mode);
 
 /* C[D][D] (+)= A^T · B over M rows (A, B are M x D).  Two stages: each of n_blocks
  * workgroups writes a D x D partial into `slab` (n_blocks*D*D floats), then the
  * partials are summed in block order (deterministic).  n_blocks from
- * iddgcn_gemm_tn_blocks().  Weight gradients dS, dK_r (tape.gradient, IDDGCN.py:172). */
+ * iddgcn_gemm_tn_blocks().  precision: IDDGCN_GEMM_* (D = 256; other widths exact f32).
+ * Weight gradients dS, dK_r (tape.gradient, IDDGCN.py:172). */
 int iddgcn_gemm_tn_blocks(long long M, int d);
 int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const float* B,
-                       float* slab, int n_blocks, float* C, int accumulate);
+                       float* slab, int n_blocks, float* C, int accumulate, int precision);
 /* Up to IDDGCN_TN_BATCH independent C_k (+)= A_k^T B_k (fp32, same D) in one launch (ABI 5): at D = 256 in the
  * split-fp16 mode one launch of ~256 workgroups shared out over the entries (blockIdx.y = entry), then each
  * entry's partials summed in block order; otherwise the single-call kernels in turn.  slab: slab_floats floats,
@@ -147,23 +140,12 @@ typedef struct {
     float* C;
     int accumulate;
 } iddgcn_tn_t;
-int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n, float* slab, long long slab_floats);
+int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n, float* slab, long long slab_floats,
+                               int precision);
 /* iddgcn_gemm_tn_f32 with A a planes table (IDDGCN_PLANES_A; D = 256, split-fp16 mode): dS = x^T do
  * with x^{l} pre-split by its producer (IDDGCN.py:62-63 autodiff). */
 int iddgcn_gemm_tn_planes_f32(void* stream, long long M, int d, const void* A, const float* B, float* slab,
                               int n_blocks, float* C, int accumulate);
-
-/* dS = A^T B (as iddgcn_gemm_tn_f32, split-fp16 mode, D = 256) fused with the tail-side segmented
- * reduction of the same layer (iddgcn_tail_seg_reduce_f32 without dsum), reading B (= do) once:
- * dP[r][t] = sum_{e: tail[e] = t} W[e][r] B[e] and dWedge[e][r] = <B[e], P[r][tail[e]]>.
- * Replaces the autodiff of IDDGCN.py:62-63 (x_t·S) and :71-77 (gather of A_r·E·K_r, sigma(alpha)
- * scale) on the tail side.  row_beg[n_blocks + 1]: block row ranges that start at tail-segment
- * starts; max_tile_runs: the caller's bound (<= 6) on distinct tails in any 32-row tile of those
- * ranges; dP must be zeroed by the caller (tails without edges); R in {1, 2}. */
-int iddgcn_gemm_tn_seg_f32(void* stream, long long M, int d, const float* A, const float* B, float* slab,
-                           int n_blocks, float* C, int accumulate, const int* row_beg, const int* tail, int R,
-                           const float* W, const float* P, long long p_rel_stride, float* dP, float* dWedge,
-                           int max_tile_runs);
 
 /* out[D][R] (+)= A^T·dz and out_b[R] (+)= colsum(dz) over M rows (dW_alpha, db_alpha).
  * slab holds (n_blocks+1)*(D+1)*R floats; n_blocks from iddgcn_gemm_tn_narrow_blocks(). */

@@ -78,9 +78,13 @@ def layer_call(E, head_idx, head_e, tail_idx, tail_e, adj, K, S, Wa, ba, ae_cach
     return torch.sigmoid(head_output), torch.sigmoid(tail_output)  # :79
 
 
-def model_forward(P, heads, rels, tails, adj, return_layers=False, return_logits=False, ae_cache=None):
+def model_forward(P, heads, rels, tails, adj, return_layers=False, return_logits=False, ae_cache=None,
+                  tail_round=None):
     """get_IDDGCN_Model wiring (IDDGCN.py:226-275) + DistMult (:103-109).  Returns the probabilities
-    [, the per-layer (x_h, x_t) outputs] [, the pre-sigmoid DistMult logits (:108, inside the sigmoid)]."""
+    [, the per-layer (x_h, x_t) outputs] [, the pre-sigmoid DistMult logits (:108, inside the sigmoid)].
+    ``tail_round`` (test hook, default None = the reference): applied to each layer's tail output x_t^l, to
+    replay a storage rounding of the tail activations (the build's bf16-feature mode stores x^1..x^3 as
+    bf16) so its kernels can be compared with float64 arithmetic on the same rounded tables."""
     E = P["E"]
     h = torch.as_tensor(heads, dtype=torch.int64)
     r = torch.as_tensor(rels, dtype=torch.int64)
@@ -89,6 +93,8 @@ def model_forward(P, heads, rels, tails, adj, return_layers=False, return_logits
     layers = []
     for l in (1, 2, 3):                                          # :238-274 (all_e = E feeds every layer)
         xh, xt = layer_call(E, h, xh, t, xt, adj, P[f"K{l}"], P[f"S{l}"], P[f"Wa{l}"], P[f"ba{l}"], ae_cache)
+        if tail_round is not None:
+            xt = tail_round(xt)
         layers.append((xh, xt))
     rel_e = P["rel"][r]                                          # :106
     logit = torch.sum(xh * rel_e * xt, dim=-1)                   # :108 (argument of the sigmoid)
@@ -192,16 +198,18 @@ def predict(params, triples, adj_coo, num_entities, dtype=torch.float64, logits=
         return model_forward(P, tr[:, 0], tr[:, 1], tr[:, 2], adj).numpy()
 
 
-def forward_detail(params, triples, adj_coo, num_entities, dtype=torch.float64):
+def forward_detail(params, triples, adj_coo, num_entities, dtype=torch.float64, tail_round=None):
     """The forward of IDDGCN.py:226-275 on `triples` with everything a parity test compares: the
     probabilities, the pre-sigmoid DistMult logits and the per-layer outputs [(x_h^l, x_t^l)], l=1..3,
-    as numpy arrays.  Cost O(len(triples)) plus one SpMM per relation per layer."""
+    as numpy arrays.  Cost O(len(triples)) plus one SpMM per relation per layer.  ``adj_coo`` may hold
+    only the adjacency rows of the entities the triples touch (A_r·E is only gathered at h and t), which
+    keeps the oracle cheap on million-node graphs.  ``tail_round``: see model_forward."""
     P = to_torch_params(params, dtype, requires_grad=False)
     adj = adj_to_torch(adj_coo, num_entities, dtype)
     tr = np.asarray(triples).astype(np.int64)
     with torch.no_grad():
         p, layers, s = model_forward(P, tr[:, 0], tr[:, 1], tr[:, 2], adj, return_layers=True, return_logits=True,
-                                     ae_cache={})
+                                     ae_cache={}, tail_round=tail_round)
     return p.numpy(), s.numpy(), [(a.numpy(), b.numpy()) for a, b in layers]
 
 

@@ -129,12 +129,16 @@ def split_neg_triple_into_folds(dc, num_folds, seed, mode=0):
     return out
 
 
-def make_fold_files(data_dir, fold, seed=89, num_splits=5):
+def make_fold_files(data_dir, fold, seed=89, num_splits=5, mode=0):
     """IDDGCN.py:312-373 — rebuild one fold's X_train / X_test / neg files.
 
     Returns dict of numpy arrays equal to the bundled
     ``mode0_fold{k}_X_train.csv``, ``_X_test.csv``, ``_neg_X_test.csv`` and
-    ``_X_train_neg.npy`` (the survey verified bit-for-bit reproduction).
+    ``_X_train_neg.npy`` (the survey verified bit-for-bit reproduction).  ``mode`` 1-3 runs the same
+    script body on the cold-start splits (IDDGCN.py:327 loops mode over range(0, 1) only); the test-side
+    drop of rel 2/3 rows is the script's label-based DataFrame.drop (:344), which in these modes also
+    removes response rows sharing a label with a dropped row (the cold-start test frames keep the
+    repeated labels of concat([dc, dd, cc])).
     """
     from sklearn.utils import shuffle
     resp = pd.read_csv(f"{data_dir}/triplets_dc.csv", header=0)
@@ -144,8 +148,8 @@ def make_fold_files(data_dir, fold, seed=89, num_splits=5):
     neg = pd.read_csv(f"{data_dir}/negative_dc_28_1754.csv", header=0)
     for df in (resp, mu, dr):
         df.columns = ['obj', 'rel', 'sbj']
-    pos_splits = split_pos_triple_into_folds(resp, mu, dr, num_splits, seed)
-    neg_splits = split_neg_triple_into_folds(neg, num_splits, seed)
+    pos_splits = split_pos_triple_into_folds(resp, mu, dr, num_splits, seed, mode)
+    neg_splits = split_neg_triple_into_folds(neg, num_splits, seed, mode)
     X_train_t, X_test_t = pos_splits[fold]
     neg_train, neg_test = neg_splits[fold]
     neg_test_f = neg_test[neg_test['rel'].isin([0, 1])]

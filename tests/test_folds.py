@@ -62,3 +62,16 @@ def test_make_fold_reproduces_bundled_files(k, golden):
     for name in ("X_train", "X_test", "neg_X_test"):
         assert np.array_equal(ours[name].astype(np.int64), f[name].astype(np.int64)), name
     assert np.array_equal(ours["X_train_neg"][0].astype(np.int64), f["X_train_neg"].astype(np.int64))
+
+
+@pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="reference datasets not present")
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_make_fold_cold_start_modes_follow_the_script(mode):
+    """Modes 1-3 (IDDGCN.py:312-363 with mode != 0): the product's make_fold equals the oracle's restatement
+    of the script body, including the label-based drop of the rel 2/3 test rows (:344) that also removes
+    response rows whose label repeats one of theirs."""
+    for k in range(5):
+        ours = folds.make_fold(REFERENCE, k, mode=mode)
+        ref = ref_utils.make_fold_files(REFERENCE, k, mode=mode)
+        for name in ("X_train", "X_test", "neg_X_test", "X_train_neg"):
+            assert np.array_equal(ours[name].astype(np.int64), ref[name].astype(np.int64)), (mode, k, name)

@@ -1,0 +1,104 @@
+"""BASELINE config 5 at FULL size on one GPU (1M nodes, 8 relations, 40M adjacency edges + 10M negatives,
+D=256, the bf16-feature mode: edge tables x^1..x^3 stored as bf16, edge GEMMs on bf16 MFMA).
+
+  * The negatives are drawn on the device with the reference's recipe (utils1.py:646-655: one uniform
+    corruption of the head or the tail per triple, numpy's legacy MT19937 stream) from every 4th positive,
+    as bench.py does: bit for bit equal to oracle/ref_utils.generate_negative_samples_np.
+  * The forward (IDDGCN.py:60-109 with the R = 8 relation loop :68-77: capped-slab gathered forward GEMMs,
+    bf16 tail tables) on a 10k scored-edge sample against the float64 oracle run on the SAME bf16-rounded
+    tail tables (oracle model_forward's tail_round hook rounds x_t^l to bf16 where the engine stores it):
+    what remains is fp32-vs-fp64 arithmetic, the weights' bf16 hi+lo split (16 significant bits) and the
+    rare element whose bf16 rounding lands the other way; bars logits 5e-3 + 1e-3 |s|, probabilities 2e-3
+    (each such flip moves one element by one bf16 ulp, 2^-9 relative).
+  * A full training step is finite and bitwise deterministic run to run.
+"""
+import numpy as np
+import pytest
+import torch
+
+from iddgcn_amd.engine import Engine, FlatParams
+from iddgcn_amd.graph import get_adj_mats
+from iddgcn_amd.sampling import negative_samples
+from iddgcn_amd.utils import synthetic_graph
+from oracle.ref_model import forward_detail
+from oracle.ref_utils import generate_negative_samples_np, get_adj_coo
+
+pytestmark = pytest.mark.gpu
+N, R, M, D, NEG_EVERY = 1_000_000, 8, 40_000_000, 256, 4
+
+
+def mild_params(seed=1):
+    rng = np.random.default_rng(seed)
+    p = {"E": rng.standard_normal((N, D), dtype=np.float32) / np.float32(np.sqrt(D))}
+    for l in (1, 2, 3):
+        p[f"K{l}"] = rng.standard_normal((R, D, D)) / D
+        p[f"S{l}"] = rng.standard_normal((D, D)) / np.sqrt(D)
+        p[f"relw{l}"] = rng.uniform(-.05, .05, R)
+        p[f"Wa{l}"] = rng.standard_normal((D, R)) / np.sqrt(D)
+        p[f"ba{l}"] = rng.standard_normal(R) * 0.1
+    p["rel"] = rng.standard_normal((R, D))
+    return {k: v.astype(np.float32) for k, v in p.items()}
+
+
+@pytest.fixture(scope="module")
+def cfg5(cuda):
+    pos, _ = synthetic_graph(N, R, M, seed=0)                   # bench.py's config-5 graph
+    src = pos[::NEG_EVERY]
+    neg = negative_samples(src, N, 89, device=cuda)             # as bench.py: on the device
+    tri = np.concatenate([pos, neg])
+    lab = np.concatenate([np.ones(len(pos), np.float32), np.zeros(len(neg), np.float32)])
+    eng = Engine(N, R, D, cuda, features="bf16")
+    adj = get_adj_mats(pos, N, R, device=cuda)
+    ed = eng.edges(tri, lab)
+    sample = np.sort(np.random.default_rng(0).choice(len(tri), 10_000, replace=False))
+    need = np.unique(np.concatenate([tri[sample, 0], tri[sample, 2]]))
+    coo = get_adj_coo(pos[np.isin(pos[:, 0], need)], N, R)
+    yield {"eng": eng, "adj": adj, "ed": ed, "tri": tri[sample], "sample": sample, "coo": coo, "src": src,
+           "neg": neg}
+    eng.release()
+    del eng, adj, ed
+    torch.cuda.empty_cache()
+
+
+def test_config5_device_negatives_bit_exact(cfg5):
+    src, neg = cfg5["src"], cfg5["neg"]
+    assert neg.shape == (M // NEG_EVERY, 3)
+    rh, rr, rt = generate_negative_samples_np(src[:, 0], src[:, 1], src[:, 2], N, 89)
+    assert np.array_equal(neg[:, 0], rh) and np.array_equal(neg[:, 1], rr) and np.array_equal(neg[:, 2], rt)
+
+
+def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, cuda):
+    params = mild_params()
+    eng, ed, sample = cfg5["eng"], cfg5["ed"], cfg5["sample"]
+    P = FlatParams(N, R, D, cuda)
+    P.load(params)
+    p, s = eng.predict(P, cfg5["adj"], ed, logits=True)
+    ps, ss = p.cpu().numpy()[sample].astype(np.float64), s.cpu().numpy()[sample].astype(np.float64)
+    bf = lambda x: x.to(torch.bfloat16).to(x.dtype)  # noqa: E731   the engine's bf16 storage of x_t^l
+    p64, s64, _ = forward_detail(params, cfg5["tri"], cfg5["coo"], N, dtype=torch.float64, tail_round=bf)
+    err = np.abs(ss - s64)
+    assert np.all(err <= 5e-3 + 1e-3 * np.abs(s64)), f"logits: max err {err.max():.2e} (max|s| {np.abs(s64).max():.2f})"
+    assert np.abs(ps - p64).max() <= 2e-3
+    # and the bf16 storage is what the engine's tables hold: its layer-3 tail rows are bf16 values
+    _, xt3 = eng.layer_outputs(ed, rows=sample[:64])[2]
+    assert torch.equal(xt3, xt3.to(torch.bfloat16).float())
+    del P
+    eng.release()
+
+
+def test_config5_step_finite_and_deterministic(cfg5, cuda):
+    eng, ed, adj = cfg5["eng"], cfg5["ed"], cfg5["adj"]
+    eng.release()
+    P = FlatParams(N, R, D, cuda)
+    P.load(mild_params(2))
+    out = []
+    for _ in range(2):
+        G = FlatParams(N, R, D, cuda)
+        loss, p = eng.loss_and_grads(P, G, adj, ed)
+        out.append((float(loss.item()), p.cpu().numpy(), G.buf.clone()))
+        del G, p
+    eng.release()
+    (la, pa, ga), (lb, pb, gb) = out
+    assert np.isfinite(la) and la > 0
+    assert la == lb and np.array_equal(pa, pb) and torch.equal(ga, gb)
+    assert bool(torch.isfinite(ga).all())

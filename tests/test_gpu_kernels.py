@@ -417,59 +417,39 @@ def _run_structured_idx(M, N, gen):
     return idx
 
 
-@pytest.mark.parametrize("mode", ["plain", "combine", "combine_r1", "combine_runs", "dsig", "rank_bcast",
-                                  "rank_bcast_nodsig", "accumulate", "gatherA", "small_M"])
-def test_rowgemm_dma_path_bitwise_equals_register_path(mode, cuda):
-    """D=256 LDS-DMA pipelined kernel == register-staged kernel, bit for bit (same MFMA chain,
-    same epilogue order), including a ragged last tile and multi-tile persistent blocks."""
+@pytest.mark.parametrize("mode", ["zero_coef", "combine", "combine_r1", "combine_runs", "accumulate", "gatherA",
+                                  "small_M"])
+def test_rowgemm_v3_exact_bitwise_equals_register_kernel(mode, cuda):
+    """D=256 exact mode: the pipelined v3 kernel == the register-staged kernel, bit for bit (the same k-ordered
+    MFMA fmaf chain, the same epilogue order), including a ragged last tile and multi-tile persistent blocks.
+    The register-staged kernel is reached by storing the V rows with a padded row stride (the v3 kernel takes
+    dense rows only); "zero_coef" (coefficients 0: the plain GEMM) compares the MFMA chains alone."""
     g = torch.Generator().manual_seed(43)
     D, N, M, R = 256, 700, (77 if mode == "small_M" else 40_000 + 17), (1 if mode == "combine_r1" else 2)
     A = torch.randn(M, D, generator=g).to(cuda)
     S = (torch.randn(D, D, generator=g) / 16).to(cuda)
-    kw = {}
-    if mode in ("combine", "combine_r1"):
-        kw = dict(coef=torch.rand(N, R, generator=g).to(cuda), coef_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
-                  V=torch.randn(R, N, D, generator=g).to(cuda), v_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
-                  v_rel_stride=N * D, act=L.ACT_SIGMOID)
-    elif mode == "combine_runs":
-        kw = dict(coef=torch.rand(N, R, generator=g).to(cuda), coef_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda),
-                  V=torch.randn(R, N, D, generator=g).to(cuda), v_idx=_run_structured_idx(M, N, g).int().to(cuda),
-                  v_rel_stride=N * D, act=L.ACT_SIGMOID)
-    elif mode == "dsig":
-        kw = dict(b_trans=True, act=L.ACT_DSIGMOID, aux=torch.rand(M, D, generator=g).to(cuda))
-    elif mode == "rank_bcast":
-        kw = dict(b_trans=True, coef=torch.randn(M, R, generator=g).to(cuda), V=torch.randn(R, D, generator=g).to(cuda),
-                  v_rel_stride=D, v_row_stride=0, act=L.ACT_DSIGMOID, aux=torch.rand(M, D, generator=g).to(cuda))
-    elif mode == "rank_bcast_nodsig":
-        kw = dict(b_trans=True, coef=torch.randn(M, R, generator=g).to(cuda), V=torch.randn(R, D, generator=g).to(cuda),
-                  v_rel_stride=D, v_row_stride=0)
-    elif mode == "accumulate":
-        kw = dict(accumulate=True, b_trans=True)
+    coef = torch.rand(N, R, generator=g).to(cuda)
+    if mode == "zero_coef":
+        coef.zero_()
+    v_idx = _run_structured_idx(M, N, g) if mode == "combine_runs" else torch.randint(0, N, (M,), generator=g)
+    kw = dict(coef=coef, coef_idx=torch.randint(0, N, (M,), generator=g).int().to(cuda), v_idx=v_idx.int().to(cuda),
+              act=L.ACT_SIGMOID)
+    if mode == "accumulate":
+        kw.update(accumulate=True, b_trans=True, act=L.ACT_NONE)
     elif mode == "gatherA":
-        kw = dict(a_idx=torch.randint(0, M, (M,), generator=g).int().to(cuda))
+        kw.update(a_idx=torch.randint(0, M, (M,), generator=g).int().to(cuda))
+    V = torch.randn(R, N, D, generator=g).to(cuda)
+    Vpad = torch.zeros(R, N, 2 * D, device=cuda)
+    Vpad[:, :, :D] = V
     C0 = torch.randn(M, D, generator=g).to(cuda)
     out = []
-    for force in (0, 1, 2):
-        old = L.lib().iddgcn_set_rowgemm_path(force)
-        try:
-            C = C0.clone()
-            ops.rowgemm(A, S, C, **kw)
-            out.append(C)
-        finally:
-            L.lib().iddgcn_set_rowgemm_path(old)
+    for Vt, vrs, kid in ((V, D, 300 + 10 * R + 2), (Vpad, 2 * D, 100)):
+        kv = dict(kw, V=Vt, v_row_stride=vrs, v_rel_stride=N * vrs)
+        assert ops.rowgemm_kernel_id(A, S, C0, **kv) == kid
+        C = C0.clone()
+        ops.rowgemm(A, S, C, **kv)
+        out.append(C)
     assert torch.equal(out[0], out[1])
-    assert torch.equal(out[0], out[2])
-
-
-class _gemm_mode:
-    def __init__(self, mode):
-        self.mode = mode
-
-    def __enter__(self):
-        self.old = L.lib().iddgcn_set_gemm_precision(self.mode)
-
-    def __exit__(self, *a):
-        L.lib().iddgcn_set_gemm_precision(self.old)
 
 
 def _maxrel(got, ref):
@@ -504,116 +484,6 @@ def test_rowgemm_batched_equals_single_calls(D, cuda):
     ops.rowgemm_batched([(A, B, C, dict(kw, M=C.shape[0])) for (A, B, _, kw), C in zip(calls, outs)])
     for a, b in zip(single, outs):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("R", [1, 2])
-@pytest.mark.parametrize("case", ["uniform", "hub", "ragged", "tiny"])
-def test_gemm_tn_seg_fused(R, case, cuda):
-    """dS = x^T do fused with the tail-side segmented reduction (iddgcn_gemm_tn_seg_f32, split mode,
-    D=256): dS within the split TN bar of fp64, dP bitwise equal to tail_seg_reduce_kernel (same
-    row-order fmaf chain; zero for tails without edges), dWedge within 1e-6 of fp64; block ranges
-    start at tail-segment starts, including a hub tail longer than a block (that block then
-    accumulates dS over far more rows: bar 4e-6) and empty blocks."""
-    from iddgcn_amd.graph import ScoredEdges
-    g = torch.Generator().manual_seed(7 + R + len(case))
-    D, N = 256, 500
-    M = {"uniform": 20_000, "hub": 20_000, "ragged": 20_011, "tiny": 40}[case]
-    t = torch.randint(0, 6 if case == "tiny" else N, (M,), generator=g)
-    if case == "hub":
-        t[: M // 3] = 17                       # one tail with a third of the edges
-    t[t == 3] = 4                              # a tail without edges
-    h = torch.randint(0, N, (M,), generator=g)
-    r = torch.randint(0, R, (M,), generator=g)
-    ed = ScoredEdges.from_triples(torch.stack([h, r, t], 1), None, N, R, cuda)
-    x = torch.rand(M, D, generator=g, dtype=torch.float64)
-    do = torch.randn(M, D, generator=g, dtype=torch.float64) * 1e-4
-    W = torch.rand(M, R, generator=g, dtype=torch.float64)
-    P = torch.randn(R, N, D, generator=g, dtype=torch.float64)
-    xf, dof, Wf, Pf = (a.float().to(cuda).contiguous() for a in (x, do, W, P))
-    nb = ops.tn_blocks(M, D)
-    rb, runs = ed.tn_seg_layout(nb)
-    assert 1 <= runs <= ops.TN_SEG_CAP
-    rbc = rb.cpu().long()
-    ts = ed.t.cpu().long()
-    assert rbc[0] == 0 and rbc[-1] == M and bool((rbc[1:] >= rbc[:-1]).all())
-    inner = rbc[(rbc > 0) & (rbc < M)]
-    assert bool((ts[inner] != ts[inner - 1]).all())          # every block starts a tail segment
-    slab = torch.empty(nb * D * D, device=cuda)
-    dS, dP, dWe = torch.empty(D, D, device=cuda), torch.full((R, N, D), 5.0, device=cuda), torch.empty(M, R, device=cuda)
-    dS2, dP2, dWe2 = torch.empty(D, D, device=cuda), torch.empty(R, N, D, device=cuda), torch.empty(M, R, device=cuda)
-    with _gemm_mode(L.GEMM_SPLIT_F16):
-        ops.gemm_tn_seg(xf, dof, dS, slab, rb, ed.t, Wf, Pf, dP, dWe, runs)
-        ops.tail_seg_reduce(ed.tptr, None, Wf, dof, Pf, dP2, dWe2)
-        ops.gemm_tn(xf, dof, dS2, slab)
-        again = torch.empty_like(dWe)
-        ops.gemm_tn_seg(xf, dof, torch.empty_like(dS), slab, rb, ed.t, Wf, Pf, torch.empty_like(dP), again, runs)
-    assert torch.equal(again, dWe)                             # deterministic
-    assert torch.equal(dP, dP2)
-    assert torch.equal(dP[:, 3], torch.zeros_like(dP[:, 3]))
-    ref_dS = x.t() @ do
-    # the hub tail puts a third of the rows into one block: one fp32 accumulation chain of ~6.7k rows
-    # (sqrt(6.7k) * 2^-24 ~ 5e-6) instead of ~80 rows per block
-    bar = 4e-6 if case == "hub" else max(2 * _maxrel(dS2, ref_dS.to(cuda)), 1e-6)
-    assert _maxrel(dS, ref_dS.to(cuda)) <= bar
-    tl = ed.t.cpu().long()
-    ref_dw = torch.stack([(do * P[rr][tl]).sum(1) for rr in range(R)], 1)
-    assert _maxrel(dWe, ref_dw.to(cuda)) <= 1e-6
-
-
-def _runs32(t):
-    """Most runs of equal values in any aligned 32-row block (graph.ScoredEdges.tail_runs32)."""
-    s = torch.ones(len(t), dtype=torch.int64)
-    s[1:] = (t[1:] != t[:-1]).long()
-    s[::32] = 1
-    s = torch.cat([s, s.new_zeros(-len(t) % 32)])
-    return int(s.view(-1, 32).sum(1).max())
-
-
-@pytest.mark.parametrize("D", DIMS)
-@pytest.mark.parametrize("R", [1, 2])
-def test_rowgemm_dsigmoid_combine(D, R, cuda):
-    """(dO·S^T) * x(1-x) with x = sigmoid(V_0[t] + sum_r W[e,r] V_{r+1}[t]) rebuilt from node tables
-    (IDDGCN_ACT_DSIGMOID_COMBINE, the layer-2 tail backward without re-reading x^1): the generic
-    kernel (any t) and, at D=256 with <= 8 runs per 32 rows, the on-chip kernel, in both GEMM modes,
-    against fp64 (split <= 2x the exact error, floor 1e-6); the on-chip kernel bitwise equal to the
-    generic one in exact mode; equal to ACT_DSIGMOID on the materialised x."""
-    g = torch.Generator().manual_seed(101 + D + R)
-    M, N = 4099, 300
-    dO = torch.randn(M, D, generator=g, dtype=torch.float64) * 1e-3
-    S = torch.randn(D, D, generator=g, dtype=torch.float64) / D ** 0.5
-    W = torch.rand(M, R, generator=g, dtype=torch.float64)
-    V = torch.randn(R + 1, N, D, generator=g, dtype=torch.float64)
-    t = torch.randint(0, N, (M,), generator=g).sort().values
-    runs = _runs32(t)
-    assert 1 <= runs <= 8
-    xs = V[0][t] + sum(W[:, r:r + 1] * V[r + 1][t] for r in range(R))
-    x = torch.sigmoid(xs)
-    ref = ((dO @ S.t()) * x * (1 - x)).to(cuda)
-    dOf, Sf, Wf, Vf, ti = (a.float().contiguous().to(cuda) for a in (dO, S, W, V, t))
-    ti = ti.int()
-
-    def run(v_runs_max, act=L.ACT_DSIGMOID_COMBINE, aux=None):
-        C = torch.full((M, D), 3.0, device=cuda)
-        if act == L.ACT_DSIGMOID_COMBINE:
-            ops.rowgemm(dOf, Sf, C, b_trans=True, act=act, coef=Wf, V=Vf, v_idx=ti, v_rel_stride=N * D,
-                        v_runs_max=v_runs_max)
-        else:
-            ops.rowgemm(dOf, Sf, C, b_trans=True, act=act, aux=aux)
-        return C
-
-    errs = {}
-    for gm in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16):
-        with _gemm_mode(gm):
-            generic, fast = run(0), run(runs)
-            errs[gm] = _maxrel(fast, ref)
-            assert _maxrel(generic, ref) <= 2e-5
-            if gm == L.GEMM_EXACT_F32:
-                assert torch.equal(fast, generic)
-                xm = torch.empty(M, D, device=cuda)             # the materialised x^1 (combine_kernel)
-                ops.combine(Vf[0], Wf, Vf[1:].contiguous(), xm, y_idx=ti, v_idx=ti, v_rel_stride=N * D)
-                assert _maxrel(run(0, L.ACT_DSIGMOID, xm), ref) <= 2e-5
-    assert errs[L.GEMM_EXACT_F32] <= 2e-5
-    assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
 
 
 @pytest.mark.parametrize("mode", ["plain", "trans", "combine", "combine_r1", "combine_runs", "dsig", "rank_bcast",
@@ -671,13 +541,12 @@ def test_rowgemm_split_f16_vs_fp64(mode, cuda):
         ref = A @ S
     errs, outs = {}, {}
     for gm in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16):
-        with _gemm_mode(gm):
-            C = C0.float().clone() if C0 is not None else torch.full((M, D), 7.0, device=cuda)
-            ops.rowgemm(Af, Sf, C, **kw)
-            if gm == L.GEMM_SPLIT_F16:
-                C2 = C0.float().clone() if C0 is not None else torch.empty(M, D, device=cuda)
-                ops.rowgemm(Af, Sf, C2, **kw)
-                assert torch.equal(C, C2)
+        C = C0.float().clone() if C0 is not None else torch.full((M, D), 7.0, device=cuda)
+        ops.rowgemm(Af, Sf, C, precision=gm, **kw)
+        if gm == L.GEMM_SPLIT_F16:
+            C2 = C0.float().clone() if C0 is not None else torch.empty(M, D, device=cuda)
+            ops.rowgemm(Af, Sf, C2, precision=gm, **kw)
+            assert torch.equal(C, C2)
         outs[gm], errs[gm] = C, _maxrel(C, ref)
     split = outs[L.GEMM_SPLIT_F16]
     if mode == "zero_rows":
@@ -711,52 +580,20 @@ def test_gemm_tn_split_f16_vs_fp64(M, kind, cuda):
     slab = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
     errs = {}
     for gm in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16):
-        with _gemm_mode(gm):
-            C = torch.empty(D, D, device=cuda)
-            ops.gemm_tn(A.float(), B.float(), C, slab)
-            errs[gm] = _maxrel(C, ref)
-            if gm == L.GEMM_SPLIT_F16:
-                C2 = torch.empty(D, D, device=cuda)
-                ops.gemm_tn(A.float(), B.float(), C2, slab)
-                assert torch.equal(C, C2)
+        C = torch.empty(D, D, device=cuda)
+        ops.gemm_tn(A.float(), B.float(), C, slab, precision=gm)
+        errs[gm] = _maxrel(C, ref)
+        if gm == L.GEMM_SPLIT_F16:
+            C2 = torch.empty(D, D, device=cuda)
+            ops.gemm_tn(A.float(), B.float(), C2, slab, precision=gm)
+            assert torch.equal(C, C2)
     assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
-
-
-@pytest.mark.parametrize("M", [31, 5003, 300_017])
-def test_gemm_tn_dma_path_bitwise_equals_register_path(M, cuda):
-    """D=256 LDS-DMA TN kernel == register-staged TN kernel, bit for bit (same MFMA order,
-    zero-filled partial tiles)."""
-    g = torch.Generator().manual_seed(M)
-    D = 256
-    A, B = torch.randn(M, D, generator=g).to(cuda), torch.randn(M, D, generator=g).to(cuda)
-    slab = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
-    out = []
-    for force in (0, 1):
-        old = L.lib().iddgcn_set_rowgemm_path(force)
-        try:
-            C = torch.empty(D, D, device=cuda)
-            ops.gemm_tn(A, B, C, slab)
-            out.append(C)
-        finally:
-            L.lib().iddgcn_set_rowgemm_path(old)
-    assert torch.equal(out[0], out[1])
-    close(out[0], A.double().t() @ B.double(), 2e-6 * np.sqrt(M))
 
 
 def _tail_runs(lengths, M):
     """Sorted row indices built from consecutive runs of the given lengths (tail-sorted edges)."""
     idx = torch.repeat_interleave(torch.arange(len(lengths)), torch.as_tensor(lengths))[:M]
     return idx
-
-
-def _runs32(idx):
-    M = idx.numel()
-    start = torch.ones(M, dtype=torch.int64)
-    start[1:] = (idx[1:] != idx[:-1]).long()
-    start[0::32] = 1
-    pad = torch.zeros((M + 31) // 32 * 32, dtype=torch.int64)
-    pad[:M] = start
-    return int(pad.view(-1, 32).sum(1).max())
 
 
 @pytest.mark.parametrize("R", [3, 4, 5, 8])
@@ -789,10 +626,10 @@ def test_rowgemm256_many_relations_gather(R, gm, order, cuda):
               act=L.ACT_SIGMOID)
     errs = {}
     for mode in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16) if gm == "split" else (L.GEMM_EXACT_F32,):
-        with _gemm_mode(mode):
-            C = torch.empty(M, D, device=cuda)
-            assert ops.rowgemm_kernel_id(A.float(), S.float(), C, **kw) == 300 + 10 * (4 if R <= 4 else 8) + 2
-            ops.rowgemm(A.float(), S.float(), C, **kw)
+        C = torch.empty(M, D, device=cuda)
+        assert ops.rowgemm_kernel_id(A.float(), S.float(), C, precision=mode, **kw) == \
+            300 + 10 * (4 if R <= 4 else 8) + 2 + (2000 if mode == L.GEMM_SPLIT_F16 else 0)
+        ops.rowgemm(A.float(), S.float(), C, precision=mode, **kw)
         errs[mode] = _maxrel(C, ref)
     assert errs[L.GEMM_EXACT_F32] <= 2e-5, errs
     if gm == "split":
@@ -812,11 +649,10 @@ def test_rowgemm256_rank_update_many_relations(R, gm, cuda):
     C0 = rnd(M, D, dev=cuda, gen=g)
     ref = (C0 + dO @ S.t() + dz @ Wa.t()) * X * (1 - X)
     kw = dict(b_trans=True, accumulate=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D,
-              v_row_stride=0, act=L.ACT_DSIGMOID, aux=X.float())
-    with _gemm_mode(L.GEMM_SPLIT_F16 if gm == "split" else L.GEMM_EXACT_F32):
-        C = C0.float().clone()
-        assert ops.rowgemm_kernel_id(dO.float(), S.float(), C, **kw) == 300 + 2 + 1 + 8
-        ops.rowgemm(dO.float(), S.float(), C, **kw)
+              v_row_stride=0, act=L.ACT_DSIGMOID, aux=X.float(), precision=gm)
+    C = C0.float().clone()
+    assert ops.rowgemm_kernel_id(dO.float(), S.float(), C, **kw) == 300 + 2 + 1 + 8 + (2000 if gm == "split" else 0)
+    ops.rowgemm(dO.float(), S.float(), C, **kw)
     assert _maxrel(C, ref) <= 2e-5
 
 
@@ -833,14 +669,14 @@ def test_rowgemm256_batched_one_launch_bitwise(gm, cuda):
             A = torch.randn(max(M, 1), D, generator=g).to(cuda)
             B = (torch.randn(D, D, generator=g) / 16).to(cuda)
             calls.append((A, B, torch.randn(M, D, generator=g).to(cuda)))
-        with _gemm_mode(L.GEMM_SPLIT_F16 if gm == "split" else L.GEMM_EXACT_F32):
-            single = []
-            for A, B, C0 in calls:
-                C = C0.clone()
-                ops.rowgemm(A, B, C, M=C.shape[0], **kw)
-                single.append(C)
-            outs = [C0.clone() for _, _, C0 in calls]
-            ops.rowgemm_batched([(A, B, C, dict(kw, M=C.shape[0])) for (A, B, _), C in zip(calls, outs)])
+        kw = dict(kw, precision=gm)
+        single = []
+        for A, B, C0 in calls:
+            C = C0.clone()
+            ops.rowgemm(A, B, C, M=C.shape[0], **kw)
+            single.append(C)
+        outs = [C0.clone() for _, _, C0 in calls]
+        ops.rowgemm_batched([(A, B, C, dict(kw, M=C.shape[0])) for (A, B, _), C in zip(calls, outs)])
         for a, b in zip(single, outs):
             assert torch.equal(a, b)
 
@@ -897,26 +733,25 @@ def test_gemm_tn_batched(D, mode, cuda):
     g = torch.Generator().manual_seed(D + len(mode))
     Ms = [30_001, 4_100, 0, 777]
     ents, refs, singles = [], [], []
-    with _gemm_mode(L.GEMM_SPLIT_F16 if mode == "split" else L.GEMM_EXACT_F32):
-        for k, M in enumerate(Ms):
-            A = torch.randn(M, D, generator=g, dtype=torch.float64)
-            B = torch.randn(M, D, generator=g, dtype=torch.float64) * 10 ** (-3 * k)
-            C0 = torch.randn(D, D, generator=g, dtype=torch.float64)
-            acc = k % 2 == 1
-            Af, Bf = A.float().to(cuda), B.float().to(cuda)
-            C = C0.float().to(cuda)
-            ents.append((Af, Bf, C, acc))
-            refs.append(A.t() @ B + (C0.float().double() if acc else 0))
-            Cs = C0.float().to(cuda)
-            if M:                                  # (the single-call entry takes no empty operands)
-                slab1 = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
-                ops.gemm_tn(Af, Bf, Cs, slab1, accumulate=acc)
-            singles.append(Cs)
-        Cinit = [c.clone() for _, _, c, _ in ents]
-        slab = torch.empty(256 * D * D, device=cuda)
-        ops.gemm_tn_batched(ents, slab)
-        again = [c.clone() for c in Cinit]
-        ops.gemm_tn_batched([(a, b, c2, acc) for (a, b, _, acc), c2 in zip(ents, again)], slab)
+    for k, M in enumerate(Ms):
+        A = torch.randn(M, D, generator=g, dtype=torch.float64)
+        B = torch.randn(M, D, generator=g, dtype=torch.float64) * 10 ** (-3 * k)
+        C0 = torch.randn(D, D, generator=g, dtype=torch.float64)
+        acc = k % 2 == 1
+        Af, Bf = A.float().to(cuda), B.float().to(cuda)
+        C = C0.float().to(cuda)
+        ents.append((Af, Bf, C, acc))
+        refs.append(A.t() @ B + (C0.float().double() if acc else 0))
+        Cs = C0.float().to(cuda)
+        if M:                                  # (the single-call entry takes no empty operands)
+            slab1 = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
+            ops.gemm_tn(Af, Bf, Cs, slab1, accumulate=acc, precision=mode)
+        singles.append(Cs)
+    Cinit = [c.clone() for _, _, c, _ in ents]
+    slab = torch.empty(256 * D * D, device=cuda)
+    ops.gemm_tn_batched(ents, slab, precision=mode)
+    again = [c.clone() for c in Cinit]
+    ops.gemm_tn_batched([(a, b, c2, acc) for (a, b, _, acc), c2 in zip(ents, again)], slab, precision=mode)
     for (_, _, C, _), C2, ref, Cs, M in zip(ents, again, refs, singles, Ms):
         assert torch.equal(C, C2)
         ref = ref.to(cuda)

@@ -122,7 +122,9 @@ def test_fit_world2_gloo_one_gpu_equals_single_process(cuda):
 
 def _step_worker(rank, world, port, q, mode, N, R, D):
     """One data-parallel step (forward + backward + bucketed all-reduce, no Adam) on this rank's shard of
-    the scored edges, edge-partitioned or with relation-sharded node tables."""
+    the scored edges, edge-partitioned or with relation-sharded node tables.  "edge_device": the
+    bucketed all-reduce on its device branch (asynchronous, in place on the GPU buckets, ordered after
+    the chunked dE SpMM on the stream: what the RCCL ranks run), not host-staged."""
     import torch.distributed as dist
     from iddgcn_amd.parallel import BucketedAllReduce, RelationShard
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -143,12 +145,11 @@ def _step_worker(rank, world, port, q, mode, N, R, D):
         P.load(_mild(N, R, D, 9))
         adj = eng.adjacency(get_adj_mats(pos, N, R))
         ed = eng.edges(tri[lo:hi], lab[lo:hi])
-        comm = BucketedAllReduce(min_bucket_rows=64)
+        comm = BucketedAllReduce(min_bucket_rows=64, host_staged=False if mode == "edge_device" else None)
         ws = eng.workspace(ed.T, True)
         eng._t_global = len(tri)
-        with eng._precision():
-            eng.forward(P, adj, ed, ws, True)
-            eng.backward(P, G, adj, ed, ws, comm)
+        eng.forward(P, adj, ed, ws, True)
+        eng.backward(P, G, adj, ed, ws, comm)
         comm.finish()
         torch.cuda.synchronize()
         q.put((rank, float(G.loss.item()), G.to_numpy()))
@@ -176,7 +177,7 @@ def test_relation_sharded_step_equals_full_batch(N, R, D, cuda):
     full, full_loss = G.to_numpy(), float(loss.item())
     del eng, P, G
     res = {}
-    for mode in ("edge", "relation", "spmm"):
+    for mode in ("edge", "edge_device", "relation", "spmm"):
         port = _free_port()
         procs = [ctx.Process(target=_step_worker, args=(r, 2, port, q, mode, N, R, D)) for r in range(2)]
         for p in procs:

@@ -22,12 +22,7 @@ pytestmark = pytest.mark.gpu
 D = 256
 
 
-class split_mode:
-    def __enter__(self):
-        self.old = L.lib().iddgcn_set_gemm_precision(L.GEMM_SPLIT_F16)
-
-    def __exit__(self, *a):
-        L.lib().iddgcn_set_gemm_precision(self.old)
+SPLIT = dict(precision="split")      # the planes forms exist in the split-fp16 GEMM mode only
 
 
 def to_planes(x):
@@ -89,13 +84,12 @@ def test_rowgemm_planes_a_and_c(M, cuda):
     xp = to_planes(x)
     xd = ops.planes_to_f32(xp)
     S, W, P, t = _fwd_inputs(M, N, R, g, cuda)
-    kw = dict(coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)
+    kw = dict(coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID, **SPLIT)
     c32, cpa, cpl = (torch.empty(M, D, device=cuda) for _ in range(3))
-    with split_mode():
-        ops.rowgemm(xd, S, c32, **kw)
-        ops.rowgemm(xp, S, cpa, planes=L.PLANES_A, **kw)
-        ops.rowgemm(xp, S, cpl, planes=L.PLANES_A | L.PLANES_C, **kw)
-        assert ops.rowgemm_kernel_id(xp, S, cpl, planes=L.PLANES_A | L.PLANES_C, **kw) == 1322
+    ops.rowgemm(xd, S, c32, **kw)
+    ops.rowgemm(xp, S, cpa, planes=L.PLANES_A, **kw)
+    ops.rowgemm(xp, S, cpl, planes=L.PLANES_A | L.PLANES_C, **kw)
+    assert ops.rowgemm_kernel_id(xp, S, cpl, planes=L.PLANES_A | L.PLANES_C, **kw) == 3322
     # A planes vs the per-row split of the same values: the same hi / lo except at re-split ties
     assert (cpa - c32).abs().max().item() <= 1e-6
     # C planes: the planes encoding of the same fp32 epilogue values
@@ -117,10 +111,9 @@ def test_rowgemm_planes_aux(inplace, cuda):
     S = (torch.randn(D, D, generator=g) / 16).to(cuda)
     c32 = torch.empty(M, D, device=cuda)
     cpl = xp.clone() if inplace else torch.empty(M, D, device=cuda)
-    with split_mode():
-        ops.rowgemm(do, S, c32, b_trans=True, act=L.ACT_DSIGMOID, aux=xd)
-        ops.rowgemm(do, S, cpl, b_trans=True, act=L.ACT_DSIGMOID, aux=xp.clone() if not inplace else cpl,
-                    planes=L.PLANES_AUX)
+    ops.rowgemm(do, S, c32, b_trans=True, act=L.ACT_DSIGMOID, aux=xd, **SPLIT)
+    ops.rowgemm(do, S, cpl, b_trans=True, act=L.ACT_DSIGMOID, aux=xp.clone() if not inplace else cpl,
+                planes=L.PLANES_AUX, **SPLIT)
     assert torch.equal(cpl, c32)          # sigma' from the same fp32 values, same GEMM
 
 
@@ -134,9 +127,8 @@ def test_gemm_tn_planes_a(M, cuda):
     do = (torch.randn(M, D, generator=g) * 1e-3).to(cuda)
     slab = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
     c32, cpl = torch.empty(D, D, device=cuda), torch.empty(D, D, device=cuda)
-    with split_mode():
-        ops.gemm_tn(xd, do, c32, slab)
-        ops.gemm_tn(xp, do, cpl, slab, a_planes=True)
+    ops.gemm_tn(xd, do, c32, slab, **SPLIT)
+    ops.gemm_tn(xp, do, cpl, slab, a_planes=True, **SPLIT)
     ref = xd.double().t() @ do.double()
     scale = ref.abs().max().item()
     assert (cpl.double() - c32.double()).abs().max().item() <= 1e-6 * scale
@@ -149,19 +141,17 @@ def test_planes_flag_checks(cuda):
     x = unit_rows(M, g, cuda)
     S, W, P, t = _fwd_inputs(M, N, R, g, cuda)
     C = torch.empty(M, D, device=cuda)
-    with split_mode():
-        with pytest.raises(L.IddgcnError):         # planes C needs the sigmoid epilogue
-            ops.rowgemm(x, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, planes=L.PLANES_C)
-        with pytest.raises(L.IddgcnError):         # planes aux needs DSIGMOID
-            ops.rowgemm(x, S, C, planes=L.PLANES_AUX)
-        with pytest.raises(L.IddgcnError):         # unknown bit
-            ops.rowgemm(x, S, C, planes=8)
-    old = L.lib().iddgcn_set_gemm_precision(L.GEMM_EXACT_F32)
-    try:
-        with pytest.raises(L.IddgcnError):         # exact mode has no planes form
-            ops.rowgemm(x, S, C, planes=L.PLANES_A)
-    finally:
-        L.lib().iddgcn_set_gemm_precision(old)
+    with pytest.raises(L.IddgcnError):         # planes C needs the sigmoid epilogue
+        ops.rowgemm(x, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, planes=L.PLANES_C, **SPLIT)
+    with pytest.raises(L.IddgcnError):         # planes aux needs DSIGMOID
+        ops.rowgemm(x, S, C, planes=L.PLANES_AUX, **SPLIT)
+    with pytest.raises(L.IddgcnError):         # unknown bit
+        ops.rowgemm(x, S, C, planes=8, **SPLIT)
+    with pytest.raises(L.IddgcnError):         # exact mode has no planes form
+        ops.rowgemm(x, S, C, planes=L.PLANES_A, precision="exact")
+    with pytest.raises(L.IddgcnError):         # nor has the exact TN
+        ops.gemm_tn(x, x, torch.empty(D, D, device=cuda), torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda),
+                    a_planes=True, precision="exact")
 
 
 def test_engine_step_planes_on_off(cuda):
@@ -179,7 +169,7 @@ def test_engine_step_planes_on_off(cuda):
     lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
     out = []
     for planes in (True, False):
-        eng = Engine(N, R, D, cuda, planes=planes)
+        eng = Engine(N, R, D, cuda, gemm="split", planes=planes)
         assert eng.use_planes == planes
         P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
         P.load(params)

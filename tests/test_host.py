@@ -204,3 +204,17 @@ def test_graph_build_workspace_queries_are_pure_host():
     assert lib.iddgcn_radix_sort_pairs(None, 10, 4, 40, None, None, None, None, None, 0) == -3
     assert lib.iddgcn_build_adjacency(None, 10, 0, 4, None, None, None, None, None, None, None, None, None,
                                       None, 0) == -3
+
+
+def test_rowgemm_precision_is_a_per_call_argument():
+    """ABI 6: the GEMM operand precision travels with each call (iddgcn_rowgemm_t.precision, the TN entries'
+    `precision`); there is no process-global switch left to race on, and an unknown mode is refused before
+    anything is launched."""
+    lib = _lib.lib()
+    assert not hasattr(lib, "iddgcn_set_gemm_precision") or "iddgcn_set_gemm_precision" not in header_symbols()
+    assert "iddgcn_set_gemm_precision" not in _lib.SIGNATURES and "iddgcn_set_rowgemm_path" not in _lib.SIGNATURES
+    args = _lib.RowGemmArgs(M=0, D=256, precision=7)
+    assert lib.iddgcn_rowgemm_f32(None, args) == -3
+    args.precision = _lib.GEMM_SPLIT_F16
+    assert lib.iddgcn_rowgemm_f32(None, args) == 0          # M = 0: valid, nothing to do
+    assert lib.iddgcn_gemm_tn_f32(None, 32, 256, None, None, None, 1, None, 0, 0) == -3

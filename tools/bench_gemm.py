@@ -47,40 +47,36 @@ def run1(T, N, D, R, reps, check, modes):
         "bwd_dsig": (dO[:n].double() @ Sd.t()) * aux[:n].double() * (1 - aux[:n].double()),
         "plain": Ad @ Sd,
     }
-    cases = {
-        "fwd_combine": lambda: ops.rowgemm(A, S, C, coef=W, coef_idx=h, V=P, v_idx=t, v_rel_stride=N * D,
-                                           act=L.ACT_SIGMOID),
-        "bwd_dsig": lambda: ops.rowgemm(dO, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux),
-        "plain": lambda: ops.rowgemm(A, S, C),
-        "tn": lambda: ops.gemm_tn(A, dO, dS, slab),
-    }
     tn_ref = A.double().t() @ dO.double()
-    for mode, mname in ((L.GEMM_EXACT_F32, "exact"), (L.GEMM_SPLIT_F16, "split")):
+    for mname in ("exact", "split"):
         if mname not in modes:
             continue
-        old = L.lib().iddgcn_set_gemm_precision(mode)
-        try:
-            for name, fn in cases.items():
+        cases = {
+            "fwd_combine": lambda: ops.rowgemm(A, S, C, coef=W, coef_idx=h, V=P, v_idx=t, v_rel_stride=N * D,
+                                               act=L.ACT_SIGMOID, precision=mname),
+            "bwd_dsig": lambda: ops.rowgemm(dO, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux, precision=mname),
+            "plain": lambda: ops.rowgemm(A, S, C, precision=mname),
+            "tn": lambda: ops.gemm_tn(A, dO, dS, slab, precision=mname),
+        }
+        for name, fn in cases.items():
+            fn()
+            torch.cuda.synchronize()
+            err = ""
+            if name in refs:
+                ref = refs[name]
+                e = ((C[:n].double() - ref).abs().max() / ref.abs().max()).item()
+                err = f" relerr={e:.2e}"
+            elif name == "tn":
+                e = ((dS.double() - tn_ref).abs().max() / tn_ref.abs().max()).item()
+                err = f" relerr={e:.2e}"
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
                 fn()
-                torch.cuda.synchronize()
-                err = ""
-                if name in refs:
-                    ref = refs[name]
-                    e = ((C[:n].double() - ref).abs().max() / ref.abs().max()).item()
-                    err = f" relerr={e:.2e}"
-                elif name == "tn":
-                    e = ((dS.double() - tn_ref).abs().max() / tn_ref.abs().max()).item()
-                    err = f" relerr={e:.2e}"
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(reps):
-                    fn()
-                e1.record()
-                torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / reps
-                print(f"{mname:5s} {name:12s} {ms:7.3f} ms  {2.0 * D * D * T / ms / 1e9:6.1f} TF{err}", flush=True)
-        finally:
-            L.lib().iddgcn_set_gemm_precision(old)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            print(f"{mname:5s} {name:12s} {ms:7.3f} ms  {2.0 * D * D * T / ms / 1e9:6.1f} TF{err}", flush=True)
 
 
 if __name__ == "__main__":

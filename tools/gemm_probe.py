@@ -20,29 +20,28 @@ def main(case, mode, reps=3, T=4_000_000, N=100_000, D=256, R=2):
     A = torch.rand(T, D, device=dev, generator=g)
     S = torch.randn(D, D, device=dev, generator=g)
     C = torch.empty(T, D, device=dev)
-    L.lib().iddgcn_set_gemm_precision(L.GEMM_SPLIT_F16 if mode == "split" else L.GEMM_EXACT_F32)
     if case == "fwd8":
         A = A.bfloat16()
         C = C.bfloat16()
         W = torch.rand(T, R, device=dev, generator=g)
         P = torch.randn(R, N, D, device=dev, generator=g)
         t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
-        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)  # noqa
+        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID, precision=mode)  # noqa
     elif case == "fwd":
         W = torch.rand(T, R, device=dev, generator=g)
         P = torch.randn(R, N, D, device=dev, generator=g)
         t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
-        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)  # noqa
+        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID, precision=mode)  # noqa
     elif case == "bwd":
         aux = torch.rand(T, D, device=dev, generator=g)
-        fn = lambda: ops.rowgemm(A, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux)  # noqa
+        fn = lambda: ops.rowgemm(A, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux, precision=mode)  # noqa
     elif case == "plain":
-        fn = lambda: ops.rowgemm(A, S, C)  # noqa
+        fn = lambda: ops.rowgemm(A, S, C, precision=mode)  # noqa
     else:
         B = torch.randn(T, D, device=dev, generator=g)
         slab = torch.empty(ops.tn_blocks(T, D) * D * D, device=dev)
         dS = torch.empty(D, D, device=dev)
-        fn = lambda: ops.gemm_tn(A, B, dS, slab)  # noqa
+        fn = lambda: ops.gemm_tn(A, B, dS, slab, precision=mode)  # noqa
     for _ in range(reps):
         fn()
     torch.cuda.synchronize()
