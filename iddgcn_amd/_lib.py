@@ -15,7 +15,7 @@ if os.environ.get("IDDGCN_LIB"):
 ABI_VERSION = 6
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
-GEMM_EXACT_F32, GEMM_SPLIT_F16 = 0, 1
+GEMM_EXACT_F32, GEMM_SPLIT_F16, GEMM_F32_4CHAIN = 0, 1, 2
 PLANES_A, PLANES_C, PLANES_AUX = 1, 2, 4          # iddgcn_rowgemm_t.planes (pre-split edge tables, ABI 4)
 
 vp = ctypes.c_void_p

@@ -333,17 +333,33 @@ __global__ __launch_bounds__(RG<D>::NW * 64) void rowgemm_kernel(RowGemmBatch pb
         }
         __syncthreads();
 
-        f32x16 acc;
+        // IDDGCN_GEMM_F32_4CHAIN: k-step q (8 k-values) goes into chain q % 4, (c0 + c1) + (c2 + c3) at the end
+        const bool c4 = p.precision == IDDGCN_GEMM_F32_4CHAIN;
+        f32x16 acc, acc1, acc2, acc3;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+        for (int j = 0; j < 16; ++j) acc[j] = acc1[j] = acc2[j] = acc3[j] = 0.f;
         const float* arow = As + (rg * 32 + i) * C::LDA + 4 * h;
+        if (c4) {
 #pragma unroll
-        for (int q = 0; q < D / 8; ++q) {
-            const f32x4 a4 = ld4(arow + 8 * q);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[0], breg[4 * q + 0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[1], breg[4 * q + 1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[2], breg[4 * q + 2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[3], breg[4 * q + 3], acc, 0, 0, 0);
+            for (int q = 0; q < D / 8; ++q) {
+                const f32x4 a4 = ld4(arow + 8 * q);
+                f32x16& ac = (q & 3) == 0 ? acc : (q & 3) == 1 ? acc1 : (q & 3) == 2 ? acc2 : acc3;
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[0], breg[4 * q + 0], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[1], breg[4 * q + 1], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[2], breg[4 * q + 2], ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[3], breg[4 * q + 3], ac, 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[j] = (acc[j] + acc1[j]) + (acc2[j] + acc3[j]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < D / 8; ++q) {
+                const f32x4 a4 = ld4(arow + 8 * q);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[0], breg[4 * q + 0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[1], breg[4 * q + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[2], breg[4 * q + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[3], breg[4 * q + 3], acc, 0, 0, 0);
+            }
         }
 
         const int c = c0 + i;
@@ -535,6 +551,12 @@ __device__ __forceinline__ float wave_max(float v) {             // max over the
     return v;
 }
 
+// C4 (IDDGCN_GEMM_F32_4CHAIN, f32 MFMA, plain form: the node-level projections P_r^l = AE_r K_r^l, E S^1):
+// k-step q (8 k-values) accumulates into chain q % 4, the four chains summed pairwise at the end; the same
+// f32 MFMA products, 64-long instead of 256-long accumulation chains (~2x less accumulation error).  The rows
+// of AE_r sum ~20 entity rows, so P reaches |1e3|, and the 256-long fp32 chain was the largest error source
+// of the logits at the reference's init (tools/logit_error_probe.py).  No accumulator is read mid-chain
+// (a mid-chain fp64 or f32 partial-sum dump made hipcc spill the weight registers of this kernel).
 // NV: gathered V tables (0 = none; 1, 2 = exactly R; 4, 8 = capacity for R <= NV, capped slabs).
 // Up to ROWGEMM_BATCH independent GEMMs of the same variant run in one launch: blockIdx.y = entry.
 // CW: broadcast V (NV = 0) with more than 2 coefficients per row (R <= 8); R <= 2 keeps the 2-slot
@@ -545,7 +567,7 @@ __device__ __forceinline__ float wave_max(float v) {             // max over the
 // PL (split mode): the planes form (IDDGCN_PLANES_*) of the variant: AUX kernels read the sigma' operand
 // as planes rows, gathered-combine kernels (NV = 1, 2) write C as planes rows.
 // (A planes rows are a run-time flag of every X3 kernel: convert_rows just skips.)
-template <int NV, bool AUX, bool HAS_COEF, bool X3, bool CW = false, bool BF = false, bool PL = false>
+template <int NV, bool AUX, bool HAS_COEF, bool X3, bool CW = false, bool BF = false, bool PL = false, bool C4 = false>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     using namespace r3;
     // A row pitch: bf16 rows (BF) need 512 B of the 1040-B fp32 row; a 528-B pitch keeps the same bank
@@ -556,6 +578,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     static_assert(!PL || (X3 && !BF && !CW && ((AUX && NV == 0) || (!AUX && (NV == 1 || NV == 2)))),
                   "PL: split-mode sigma' backward or R <= 2 gathered forward");
     static_assert(!BF || X3, "BF: the 16-bit A-plane pipeline");
+    static_assert(!C4 || (!X3 && NV == 0 && !AUX && !HAS_COEF), "C4: the f32 plain form (node projections)");
     static_assert(NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
     constexpr bool WIDE = NV > 2;                      // capped slabs, run-time R <= NV
     // capped V slabs r >= 1 (rows past the cap read from L2): WIDE, and NV = 2 when V3_CAP2 > 0
@@ -1005,18 +1028,28 @@ _Pragma("unroll") \
             if constexpr (!X3) { \
 _Pragma("unroll") \
                 for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
+                /* C4: four interleaved f32 chains (k-step q into chain q % 4, 64 k-values each), summed pairwise */ \
+                /* at the end: no accumulator is read mid-chain, the chains are 4x shorter */ \
+                f32x16 acc1, acc2, acc3; \
+_Pragma("unroll") \
+                for (int j = 0; j < 16; ++j) acc1[j] = acc2[j] = acc3[j] = 0.f; \
                 const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
                 f32x4 a_cur = ld4(arow); \
 _Pragma("unroll") \
                 for (int q = 0; q < D / 8; ++q) { \
                     f32x4 a_nxt = a_cur; \
                     if (q + 1 < D / 8) a_nxt = ld4(arow + 8 * (q + 1)); \
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 0], a_cur[0], acc, 0, 0, 0); \
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 1], a_cur[1], acc, 0, 0, 0); \
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 2], a_cur[2], acc, 0, 0, 0); \
-                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 3], a_cur[3], acc, 0, 0, 0); \
+                    f32x16& ac = !C4 ? acc : ((q & 3) == 0 ? acc : (q & 3) == 1 ? acc1 : (q & 3) == 2 ? acc2 : acc3); \
+                    ac = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 0], a_cur[0], ac, 0, 0, 0); \
+                    ac = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 1], a_cur[1], ac, 0, 0, 0); \
+                    ac = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 2], a_cur[2], ac, 0, 0, 0); \
+                    ac = __builtin_amdgcn_mfma_f32_32x32x2f32(breg[4 * q + 3], a_cur[3], ac, 0, 0, 0); \
                     __builtin_amdgcn_sched_barrier(0); \
                     a_cur = a_nxt; \
+                } \
+                if constexpr (C4) { \
+_Pragma("unroll") \
+                    for (int j = 0; j < 16; ++j) acc[j] = (acc[j] + acc1[j]) + (acc2[j] + acc3[j]); \
                 } \
             } else if constexpr (BF) { \
                 /* bf16 A fragments straight from the row; W hi and lo, one accumulator */ \
@@ -2605,8 +2638,10 @@ struct V3Sel {
     bool cw = false;        // broadcast V with R > 2 coefficients
     bool pl = false;        // planes C (gathered forward) / planes sigma' operand (backward)
     bool split = false;     // IDDGCN_GEMM_SPLIT_F16 operands (template X3), else exact f32
+    bool c4 = false;        // IDDGCN_GEMM_F32_4CHAIN (template C4)
     bool same(const V3Sel& o) const {
-        return nv == o.nv && aux == o.aux && hc == o.hc && cw == o.cw && pl == o.pl && split == o.split;
+        return nv == o.nv && aux == o.aux && hc == o.hc && cw == o.cw && pl == o.pl && split == o.split &&
+               c4 == o.c4;
     }
 };
 // Which v3 instantiation computes this call, or false (the register-staged rowgemm_kernel<256> then runs:
@@ -2622,6 +2657,8 @@ bool v3_select(const RowGemmP& p, V3Sel& sel) {
         sel = {0, dsig, p.R > 0, p.R > 2};
     }
     sel.split = p.precision == IDDGCN_GEMM_SPLIT_F16;
+    sel.c4 = p.precision == IDDGCN_GEMM_F32_4CHAIN;
+    if (sel.c4 && (sel.nv || sel.aux || sel.hc)) return false;      // C4 at D = 256: plain form only
     sel.pl = (p.planes & (IDDGCN_PLANES_C | IDDGCN_PLANES_AUX)) != 0;
     if (!sel.pl) return true;
     // the planes forms: C planes on the R <= 2 gathered forward, sigma' planes on the plain backward
@@ -2645,7 +2682,12 @@ RowGemmP to_p(const iddgcn_rowgemm_t& a) {
 int check_rowgemm(const iddgcn_rowgemm_t& a) {
     if (!dim_ok(a.D)) return IDDGCN_E_BAD_DIM;
     if (a.R < 0 || a.R > MAX_R) return IDDGCN_E_BAD_REL;
-    if (a.precision != IDDGCN_GEMM_EXACT_F32 && a.precision != IDDGCN_GEMM_SPLIT_F16) return IDDGCN_E_BAD_ARG;
+    if (a.precision != IDDGCN_GEMM_EXACT_F32 && a.precision != IDDGCN_GEMM_SPLIT_F16 &&
+        a.precision != IDDGCN_GEMM_F32_4CHAIN)
+        return IDDGCN_E_BAD_ARG;
+    // F32_4CHAIN at D = 256: the plain form (no coefficients, no sigma' operand, no planes)
+    if (a.precision == IDDGCN_GEMM_F32_4CHAIN && a.D == 256 && (a.R > 0 || a.act == IDDGCN_ACT_DSIGMOID || a.planes))
+        return IDDGCN_E_BAD_ARG;
     if (a.M == 0) return 0;
     if (a.M < 0 || !a.A || !a.B || !a.C) return IDDGCN_E_BAD_ARG;
     if (a.R > 0 && (!a.coef || !a.V)) return IDDGCN_E_BAD_ARG;
@@ -2703,7 +2745,9 @@ void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel, bool b
         if (x3) hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, true, true>), g, blk, 0, st, pb); \
         else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, AUX, true, false, true>), g, blk, 0, st, pb);   \
     }
-    if (sel.pl) {           // check_rowgemm: split mode
+    if (sel.c4) {           // check_rowgemm / v3_select: the plain f32 form
+        hipLaunchKernelGGL((rowgemm256_v3_kernel<0, false, false, false, false, false, false, true>), g, blk, 0, st, pb);
+    } else if (sel.pl) {    // check_rowgemm: split mode
         if (sel.nv == 1) hipLaunchKernelGGL((rowgemm256_v3_kernel<1, false, true, true, false, false, true>), g, blk, 0, st, pb);
         else if (sel.nv == 2) hipLaunchKernelGGL((rowgemm256_v3_kernel<2, false, true, true, false, false, true>), g, blk, 0, st, pb);
         else hipLaunchKernelGGL((rowgemm256_v3_kernel<0, true, false, true, false, false, true>), g, blk, 0, st, pb);
@@ -2843,7 +2887,7 @@ int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* a) {
     V3Sel sel;
     if (a->D == 256 && v3_select(p, sel))
         return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.cw ? 8 : 0) + (sel.split ? 2000 : 0) +
-               (sel.pl ? 1000 : 0);
+               (sel.c4 ? 4000 : 0) + (sel.pl ? 1000 : 0);
     return 100;
 }
 

@@ -200,6 +200,7 @@ class Workspace:
 
 
 GEMM_MODES = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16}
+PROJ_MODES = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16, "exact4": L.GEMM_F32_4CHAIN}
 
 
 class Engine:
@@ -252,6 +253,33 @@ class Engine:
             raise L.IddgcnError(f"gemm must be one of {sorted(GEMM_MODES)}")
         self._gemm = mode
 
+    _proj_gemm = None
+
+    @property
+    def proj_gemm(self):
+        """Precision of the node-level projections (plain row GEMMs over N rows: P_r^l = AE_r K_r^l, E S^1 and
+        the backward's dAE_r = dP_r K_r^T).  Default: "exact4" (f32 MFMA, four interleaved accumulation
+        chains) in the exact mode — AE_r sums ~20 entity rows, P reaches |1e3| at the reference's init, and a
+        256-long fp32 chain there was the largest error of the logits (tools/logit_error_probe.py) — else
+        the engine's ``gemm``."""
+        if self._proj_gemm is not None:
+            return self._proj_gemm
+        return "exact4" if self._gemm == "exact" else self._gemm
+
+    @property
+    def row_gemm(self):
+        """Precision of the other row GEMMs (the tail / head chains and their backward): the engine's ``gemm``,
+        except at D < 256 in the exact mode, where the register-staged kernel takes "exact4" for every form (the
+        four-chain accumulation costs nothing there and keeps the trained-weight logits of the reference's
+        64-wide model further inside the 1e-4 bar)."""
+        return "exact4" if (self._gemm == "exact" and self.D < 256) else self._gemm
+
+    @proj_gemm.setter
+    def proj_gemm(self, mode):
+        if mode is not None and mode not in PROJ_MODES:
+            raise L.IddgcnError(f"proj_gemm must be None or one of {sorted(PROJ_MODES)}")
+        self._proj_gemm = mode
+
     @property
     def use_planes(self):
         """x^1, x^2 are stored pre-split: split GEMM mode at D = 256 with fp32 features, R <= 2 (the
@@ -302,6 +330,8 @@ class Engine:
         N, R, D, T = self.N, self.R, self.D, ed.T
         E = P["E"]
         pk = dict(precision=self.gemm)          # every GEMM call carries this engine's operand precision
+        pn = dict(precision=self.proj_gemm)     # (the plain node-level projections)
+        pr = dict(precision=self.row_gemm)      # (the other row GEMMs)
         sh = self.node_shard
         if sh is None and self.spmm_shard is not None:
             # row-partitioned A_r·E (every rank holds E): this rank's (relation, row) pieces, then all-gather
@@ -310,21 +340,21 @@ class Engine:
                 ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + n0:r * (N + 1) + n1 + 1], adj.fwd_col, adj.fwd_val, E,
                              ws.AE[r][n0:n1].view(1, n1 - n0, D), 1, n1 - n0)
             ss.all_gather(ws.AE.view(R * N, D))
-            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], pk) for l in range(NUM_LAYERS) for r in range(R)]
+            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], pn) for l in range(NUM_LAYERS) for r in range(R)]
         elif sh is None:
             # AE_r = A_r·E, all relations in one launch (IDDGCN.py:69-70)
             ops.spmm_csr(adj.fwd_ptr, adj.fwd_col, adj.fwd_val, E, ws.AE, R, N)
             # P_r^l = AE_r·K_r^l (node-level form of IDDGCN.py:71-72,76-77) and, layer 1, x·S1 at node
             # level for both sides (inputs E[h], E[t]): independent GEMMs, batched (one launch below D=256)
-            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], pk) for l in range(NUM_LAYERS) for r in range(R)]
+            proj = [(ws.AE[r], P[f"K{l + 1}"][r], ws.P[l, r], pn) for l in range(NUM_LAYERS) for r in range(R)]
         else:
             # relation-sharded: this rank's (relation, node-row) pieces of AE_r and P_r^l, then all-gather P
             proj = []
             for r, n0, n1 in sh.pieces():
                 ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + n0:r * (N + 1) + n1 + 1], adj.fwd_col, adj.fwd_val, E,
                              ws.AE[r][n0:n1].view(1, n1 - n0, D), 1, n1 - n0)
-                proj += [(ws.AE[r][n0:n1], P[f"K{l + 1}"][r], ws.P[l, r][n0:n1], pk) for l in range(NUM_LAYERS)]
-        proj.append((E, P["S1"], ws.ES1, pk))
+                proj += [(ws.AE[r][n0:n1], P[f"K{l + 1}"][r], ws.P[l, r][n0:n1], pn) for l in range(NUM_LAYERS)]
+        proj.append((E, P["S1"], ws.ES1, pn))
         for i in range(0, len(proj), 16):
             ops.rowgemm_batched(proj[i:i + 16])
         if sh is not None:
@@ -341,11 +371,11 @@ class Engine:
             ops.alpha_fwd(ws.X[l - 1], P[f"Wa{l + 1}"], P[f"ba{l + 1}"], ws.Ssm[l], ws.W[l])
             ops.gather_rows(ws.W[l], ed.h, ws.Wedge[l])
             ops.rowgemm(ws.X[l - 1], S, ws.X[l], coef=ws.W[l], V=ws.P[l], v_rel_stride=N * D,
-                        act=L.ACT_SIGMOID, **pk)
+                        act=L.ACT_SIGMOID, **pr)
             with self._mark("tail_fwd_gemm"):
                 ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID,
-                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, **pk)
+                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, **pr)
         # DistMult (+ BCE and backward seed when training)
         if train:
             # one pass over head segments: p / loss / drel partials, the tail seed do^3 (per edge)
@@ -372,7 +402,7 @@ class Engine:
         small gradients + the loss after the layer loop, then row chunks of dE as the transposed SpMM
         produces them, so the all-reduce of the large dE overlaps the SpMM of the next chunk."""
         N, R, D = self.N, self.R, self.D
-        pk = dict(precision=self.gemm)
+        pk, pn, pr = dict(precision=self.gemm), dict(precision=self.proj_gemm), dict(precision=self.row_gemm)
         dOn, dOn_next = ws.dOn_a, ws.dOn_b      # head seed dO^3, written by distmult_bce_heads
         if self.node_shard is not None:
             ws.dAE.zero_()                      # rows other ranks own stay 0 in the dE SpMM below
@@ -389,7 +419,7 @@ class Engine:
                     ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)
                 with self._mark("tail_bwd_gemm"):
                     ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
-                                planes=L.PLANES_AUX if pl else 0, **pk)
+                                planes=L.PLANES_AUX if pl else 0, **pr)
             # head side (node level)
             ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
                               dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)
@@ -407,14 +437,14 @@ class Engine:
                 ops.gemm_tn_batched(tn[i:i + L.TN_BATCH], ws.tn_slab, **pk)
             if l > 0:
                 ops.rowgemm(dOn, Sl, dOn_next, b_trans=True, coef=ws.dz, V=ws.WaT, v_rel_stride=D,
-                            v_row_stride=0, act=L.ACT_DSIGMOID, aux=Xin, **pk)
+                            v_row_stride=0, act=L.ACT_DSIGMOID, aux=Xin, **pr)
             else:
                 # dE (head input of layer 1 + x·S1 inputs of both sides)
                 ops.rowgemm(ws.dES, Sl, G["E"], b_trans=True, coef=ws.dz, V=ws.WaT, v_rel_stride=D,
-                            v_row_stride=0, **pk)
+                            v_row_stride=0, **pr)
             # relation kernels: dK_r = AE_r^T dP_r (above) ; dAE_r += dP_r K_r^T
             if sh is None:
-                ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2), **pk))
+                ops.rowgemm_batched([(ws.dP[r], K[r], ws.dAE[r], dict(b_trans=True, accumulate=(l != 2), **pn))
                                      for r in range(R)])
             else:
                 # relation-sharded: the owners sum the edge partials of dP, then form their rows of dK_r (a
@@ -424,7 +454,7 @@ class Engine:
                 for r, n0, n1 in sh.pieces():
                     ops.gemm_tn(ws.AE[r][n0:n1], ws.dP[r][n0:n1], dK[r], ws.tn_slab, accumulate=True, **pk)
                 ops.rowgemm_batched([(ws.dP[r][n0:n1], K[r], ws.dAE[r][n0:n1],
-                                      dict(b_trans=True, accumulate=True, **pk)) for r, n0, n1 in sh.pieces()])
+                                      dict(b_trans=True, accumulate=True, **pn)) for r, n0, n1 in sh.pieces()])
             dOn, dOn_next = dOn_next, dOn
         # DistMult rel grad and the loss: every gradient past E is final now
         ops.reduce_slabs(ws.drel_slab, ws.nb_dm, G["rel"])

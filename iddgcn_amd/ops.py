@@ -24,14 +24,16 @@ def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
-_PRECISION = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16,
-              L.GEMM_EXACT_F32: L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16: L.GEMM_SPLIT_F16}
+_PRECISION = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16, "exact4": L.GEMM_F32_4CHAIN,
+              L.GEMM_EXACT_F32: L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16: L.GEMM_SPLIT_F16,
+              L.GEMM_F32_4CHAIN: L.GEMM_F32_4CHAIN}
 
 
 def _prec(precision):
-    """GEMM operand precision of one call (include/iddgcn.h IDDGCN_GEMM_*): "exact" / "split" or the constant."""
+    """GEMM operand precision of one call (include/iddgcn.h IDDGCN_GEMM_*): "exact" / "split" / "exact4" (f32
+    MFMA with four interleaved accumulation chains: row GEMMs, plain form at D = 256) or the constant."""
     if precision not in _PRECISION:
-        raise L.IddgcnError(f"precision must be 'exact' or 'split', got {precision!r}")
+        raise L.IddgcnError(f"precision must be 'exact', 'split' or 'exact4', got {precision!r}")
     return _PRECISION[precision]
 
 

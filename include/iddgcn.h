@@ -47,9 +47,15 @@ extern "C" {
  *     of the value), and hi*hi + hi*lo + lo*hi runs on v_mfma_f32_32x32x16_f16 with fp32 accumulation; the
  *     power-of-two scales are undone exactly in the epilogue.  An opt-in faster mode: results are
  *     deterministic but not bitwise equal to the exact mode.
- * Row GEMMs for D < 256 and every other kernel always compute in exact f32. */
+ *   IDDGCN_GEMM_F32_4CHAIN (row GEMMs: any D; at D = 256 the plain form only — no coefficients, no sigma'
+ *     operand, no planes): the exact mode's f32 MFMA arithmetic with the accumulation over k split into
+ *     four interleaved fp32 chains (k-block q of 8 values into chain q mod 4), summed pairwise at the end:
+ *     4x shorter rounding chains, ~2x less accumulation error at K = 256; deterministic.  The node-level
+ *     projections P_r^l = AE_r K_r^l (|P| up to ~1e3: AE_r sums ~20 entity rows) use it in the exact mode.
+ * Row GEMMs for D < 256 and every other kernel compute in exact f32 (or F32_4CHAIN where asked). */
 #define IDDGCN_GEMM_EXACT_F32 0
 #define IDDGCN_GEMM_SPLIT_F16 1
+#define IDDGCN_GEMM_F32_4CHAIN 2
 
 /* Pre-split edge tables ("planes", ABI 4; D = 256, split-fp16 GEMM mode only).  A row of values in
  * [0, 1] (sigmoid outputs) stored as 8 column blocks of 128 B, block b = [hi f16 of columns 32b..32b+31 |
@@ -105,13 +111,13 @@ typedef struct {
     int act; const float* aux;
     int planes;           /* IDDGCN_PLANES_* flags (ABI 4; 0 = every table fp32).  Nonzero needs D = 256,
                              the split-fp16 mode and no a_idx; invalid combinations return IDDGCN_E_BAD_ARG */
-    int precision;        /* IDDGCN_GEMM_EXACT_F32 (0) or IDDGCN_GEMM_SPLIT_F16 (ABI 6: per call) */
+    int precision;        /* IDDGCN_GEMM_EXACT_F32 (0), _SPLIT_F16 or _F32_4CHAIN (ABI 6: per call) */
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 
 /* Which kernel iddgcn_rowgemm_f32 would run for these arguments (a test / benchmark hook; nothing is
  * launched): 300 + 10*NV + aux + 2*coef + 8*(broadcast V with R > 2 coefficients) + 1000 for the planes
- * form (C or aux planes) + 2000 for split-fp16 operands, for the D = 256 v3 pipeline (NV = gathered V
+ * form (C or aux planes) + 2000 for split-fp16 operands + 4000 for F32_4CHAIN, for the D = 256 v3 pipeline (NV = gathered V
  * tables: 1, 2, or capacity 4 / 8 for R <= 8, whose LDS slabs keep 7 distinct V rows per 32-row tile
  * and read further ones from L2); 100 for the register-staged kernel (D < 256, and D = 256 forms the v3
  * kernel does not take: a gathered V with the sigma' epilogue, V rows that are not dense); -1 for an

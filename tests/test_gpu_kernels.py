@@ -760,3 +760,35 @@ def test_gemm_tn_batched(D, mode, cuda):
             continue
         bar = max(2 * _maxrel(Cs, ref), 2e-6)
         assert _maxrel(C, ref) <= bar
+
+
+@pytest.mark.parametrize("D", DIMS)
+def test_rowgemm_f32_4chain_accumulation(D, cuda):
+    """IDDGCN_GEMM_F32_4CHAIN ("exact4", the node-level projections P_r^l = AE_r K_r^l in the exact mode): the
+    f32 MFMA products with the k-accumulation in four interleaved fp32 chains summed pairwise.  On
+    projection-shaped operands (rows like AE_r = sums of ~20 U[0,1) entity rows, weights N(0, 1): |C| up
+    to ~1e3) its error against fp64 is below the single 256-long chain's, the result is deterministic, the
+    plain / transposed / accumulate forms all take it, and the D = 256 forms it does not cover are refused."""
+    g = torch.Generator().manual_seed(5 * D)
+    M = 20_011
+    A = (torch.rand(M, D, generator=g, dtype=torch.float64) * 20 + torch.rand(M, 1, generator=g, dtype=torch.float64)).to(cuda)
+    B = torch.randn(D, D, generator=g, dtype=torch.float64).to(cuda)
+    C0 = torch.randn(M, D, generator=g, dtype=torch.float64).to(cuda) * 100
+    for kw, ref in ((dict(), A @ B), (dict(b_trans=True), A @ B.t()), (dict(accumulate=True), C0 + A @ B)):
+        errs = {}
+        for prec in ("exact", "exact4"):
+            C = C0.float().clone() if kw.get("accumulate") else torch.empty(M, D, device=cuda)
+            ops.rowgemm(A.float(), B.float(), C, precision=prec, **kw)
+            errs[prec] = (C.double() - ref).abs().max().item()
+            if prec == "exact4":
+                C2 = C0.float().clone() if kw.get("accumulate") else torch.empty(M, D, device=cuda)
+                ops.rowgemm(A.float(), B.float(), C2, precision=prec, **kw)
+                assert torch.equal(C, C2)
+                if D == 256:
+                    assert ops.rowgemm_kernel_id(A.float(), B.float(), C, precision=prec, **kw) == 4300
+        assert errs["exact4"] <= errs["exact"], (kw, errs)
+        assert errs["exact4"] <= 2e-6 * ref.abs().max().item() * np.sqrt(D / 64), (kw, errs)
+    if D == 256:       # coefficients / sigma' epilogues keep the single chain at D = 256
+        with pytest.raises(L.IddgcnError):
+            ops.rowgemm(A.float(), B.float(), torch.empty(M, D, device=cuda), precision="exact4", act=L.ACT_DSIGMOID,
+                        aux=torch.rand(M, D, device=cuda))

@@ -19,19 +19,19 @@ import sys
 
 import pandas as pd
 
+# rowgemm256_v3_kernel<NV, AUX, HAS_COEF, X3, CW, BF, PL, C4> (ABI 6 template order)
 SYMBOLS = {
-    "split": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, true, false, false, false",
-              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, false, false",
-              "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, true, true, false, false",
-              "tail_dS_tn": "gemm_tn256_x3_kernel<false"},
-    "exact": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, false, false, false, false>",
-              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, false, false, false, false>",
-              "tail_bwd_rec_gemm": "rowgemm256_v3_kernel<3, false, true, false, true, false, false>",
+    # split mode: the layer-2 forward writes planes C (PL true), layer 3 does not; the backward reads planes
+    "split": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, true, false, false,",
+              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, false,",
+              "tail_dS_tn": "gemm_tn256_x3_kernel<"},
+    "exact": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, false, false, false, false, false>",
+              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, false, false, false, false, false>",
               "tail_dS_tn": "gemm_tn256_dma_kernel"},
     # the bf16-feature mode (config 5: R = 8 gathered relations, bf16 edge tables); recorded under the
-    # bench's gemm key ("split") with `python tools/pmc_traffic.py ... split synthetic-5 1 profiles/r02 bf16`
-    "bf16": {"tail_fwd_gemm": "rowgemm256_v3_kernel<8, false, true, true, false, false, true, false>",
-             "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, false, true, false>",
+    # bench's gemm key with `python tools/pmc_traffic.py ... exact synthetic-5 1 profiles/r03 bf16`
+    "bf16": {"tail_fwd_gemm": "rowgemm256_v3_kernel<8, false, true, true, false, true, false, false>",
+             "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, true, false, false>",
              "tail_dS_tn": "gemm_tn256_bf16_kernel"},
 }
 

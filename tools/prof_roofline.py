@@ -14,7 +14,7 @@ import sys
 import pandas as pd
 
 
-def main(trace, bench, name="rowgemm256_v3_kernel<2, false, true, true, false, false, false>", frac=0.5):
+def main(trace, bench, name="rowgemm256_v3_kernel<2, false, true, false, false, false, false, false>", frac=0.5):
     t = pd.read_csv(trace)
     k = t[t["Kernel_Name"].str.contains(name, regex=False)].copy()
     k["ms"] = (k["End_Timestamp"] - k["Start_Timestamp"]) / 1e6
