@@ -47,7 +47,8 @@ GEMM_NOTE = {
 # the arithmetic the path computes in, per GEMM mode (the bench line's "dtype")
 DTYPE = {"split": "f32 (D=256 GEMMs on split-fp16x2 operands, fp32 accumulate)", "exact": "f32"}
 DTYPE_BF16 = ("bf16 edge tables (x^l, do^l) with bf16 MFMA for the edge GEMMs (weights as bf16 hi+lo), fp32 node "
-              "tables, accumulation and epilogues (perf-only mode, BASELINE config 5)")
+              "tables, accumulation and epilogues, node-level GEMMs on split-fp16 operands (perf-only mode, BASELINE "
+              "config 5)")
 
 CONFIGS = {
     2: dict(name="synthetic-fold0-shape", N=845, R=4, M=37_510, D=64, scaling="weak"),
@@ -55,7 +56,7 @@ CONFIGS = {
     4: dict(name="synthetic-4", N=1_000_000, R=2, M=20_000_000, D=256, scaling="strong"),
     # 40M positives, 10M negatives (one per 4 positives), generated on the device
     5: dict(name="synthetic-5", N=1_000_000, R=8, M=40_000_000, D=256, scaling="strong", neg_every=4,
-            features="bf16"),
+            features="bf16", gemm="split"),
 }
 
 
@@ -246,6 +247,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
 
     cfg = CONFIGS[cid]
     N, R, D = cfg["N"], cfg["R"], cfg["D"]
+    # config 5 is the bf16-feature throughput mode: its node-level GEMMs take split-fp16 operands too
+    gemm = cfg.get("gemm", gemm) if (args.features or cfg.get("features", "f32")) == "bf16" else gemm
     shard = args.shard if shard is None else shard
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
@@ -265,6 +268,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
                           np.zeros(max(0, hi - max(lo, npos)), np.float32)])
     feat = args.features or cfg.get("features", "f32")
     eng = Engine(N, R, D, dev, gemm=gemm, features=feat, planes=not args.no_planes)
+    eng.overlap = args.overlap
     adj = get_adj_mats(pos, N, R, device=dev)            # device graph build (bit-identical to the host's)
     ed = eng.edges(tri, lab)
     del pos, neg, tri, lab
@@ -371,6 +375,8 @@ def main():
                     help="operand precision of the D=256 MFMA GEMMs: exact f32 (the reference's arithmetic, the "
                          "headline) or the opt-in split-fp16 operands (timed too, under other_gemm_mode)")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")
+    ap.add_argument("--overlap", action="store_true",
+                    help="backward: layer-2/3 tail reductions on a side stream beside the dS TN (A/B)")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")

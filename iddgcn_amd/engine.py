@@ -321,6 +321,16 @@ class Engine:
         return self._ws[key]
 
     # -- forward ------------------------------------------------------------
+    # backward: the layer-2/3 tail reductions (HBM-bound) on a side stream beside the exact-mode dS TN (MFMA-bound,
+    # 151 VGPRs: room for two more waves per SIMD)
+    overlap = False
+    _side = None
+
+    def _side_stream(self):
+        if self._side is None or self._side.device != torch.cuda.current_stream().device:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
     node_shard = None      # parallel.RelationShard: per-relation node tables split over the ranks
     # parallel.RelationShard used for the two SpMMs only (node GEMMs replicated): A_r·E row-partitioned and
     # all-gathered, dAE reduce-scattered to the row owners before a transposed SpMM over their columns
@@ -410,9 +420,19 @@ class Engine:
         for l in (2, 1, 0):                     # layer index l -> reference layer l+1
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
             do = ws.xt[l]                       # do^{l+1}, written over x^{l+1}
-            # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part
-            ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
-                                dsum=ws.dES if l == 0 else None)
+            # tail side: dP (tail part), dWedge, and for layer 1 the dES tail part.  With `overlap` (layers
+            # 2-3) the HBM-bound reduction runs on a side stream beside the MFMA-bound dS TN and sigma'
+            # GEMM (it reads do, P, Wedge and writes dP, dWedge: nothing those two touch); the side stream
+            # first waits for everything queued so far (the previous layer's readers of dP), and the
+            # main stream waits for it before the head-side work that reads dP, dWedge
+            side = self._side_stream() if (self.overlap and l > 0) else None
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge)
+            else:
+                ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
+                                    dsum=ws.dES if l == 0 else None)
             if l > 0:
                 # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x), written over x^{l}
                 with self._mark("tail_dS_tn"):
@@ -420,6 +440,8 @@ class Engine:
                 with self._mark("tail_bwd_gemm"):
                     ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
                                 planes=L.PLANES_AUX if pl else 0, **pr)
+            if side is not None:
+                torch.cuda.current_stream().wait_stream(side)
             # head side (node level)
             ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
                               dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)

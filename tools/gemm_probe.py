@@ -42,9 +42,16 @@ def main(case, mode, reps=3, T=4_000_000, N=100_000, D=256, R=2):
         slab = torch.empty(ops.tn_blocks(T, D) * D * D, device=dev)
         dS = torch.empty(D, D, device=dev)
         fn = lambda: ops.gemm_tn(A, B, dS, slab, precision=mode)  # noqa
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     for _ in range(reps):
         fn()
+    e1.record()
     torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    print(f"{case} {mode}: {ms:.3f} ms per launch, {2.0 * D * D * T / ms / 1e9:.1f} TFLOP/s algorithmic", flush=True)
 
 
 if __name__ == "__main__":
