@@ -43,9 +43,13 @@ GEMM_NOTE = {
              "scales), 3 f16 MFMAs per k-step, fp32 accumulation; every other kernel exact f32 "
              "(include/iddgcn.h IDDGCN_GEMM_SPLIT_F16, per call)",
     "exact": "exact f32 MFMA (v_mfma_f32_32x32x2_f32, bitwise an fmaf chain) for every GEMM, exact f32 elsewhere",
+    "bf16x3": "D=256 GEMM operands split EXACTLY into three bf16 pieces (8+8+8 = 24 significant bits: every fp32 "
+              "value represented without loss), the six piece products of order >= 2^-16 on bf16 MFMAs (exact "
+              "products), fp32 accumulation; dropped cross terms <= 2^-23 |a*w| per product (fp32's own product "
+              "rounding: 2^-24); every other kernel exact f32 (include/iddgcn.h IDDGCN_GEMM_BF16X3, per call)",
 }
 # the arithmetic the path computes in, per GEMM mode (the bench line's "dtype")
-DTYPE = {"split": "f32 (D=256 GEMMs on split-fp16x2 operands, fp32 accumulate)", "exact": "f32"}
+DTYPE = {"split": "f32 (D=256 GEMMs on split-fp16x2 operands, fp32 accumulate)", "exact": "f32", "bf16x3": "f32"}
 DTYPE_BF16 = ("bf16 edge tables (x^l, do^l) with bf16 MFMA for the edge GEMMs (weights as bf16 hi+lo), fp32 node "
               "tables, accumulation and epilogues, node-level GEMMs on split-fp16 operands (perf-only mode, BASELINE "
               "config 5)")
@@ -87,7 +91,7 @@ def launch_ranks(args):
 def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4):
     """Roofline of one edge-level GEMM launch.
 
-    flops: 2*D^2*T algorithmic (x3 f16 MFMA instructions on the f16 peak in split mode);
+    flops: 2*D^2*T algorithmic (x3 f16 MFMA instructions on the f16 peak in split mode, x6 bf16 ones in bf16x3);
     bytes (algorithmic, fp32): fwd reads x^{l-1}, writes x^l, reads W[h_e] (R per edge), t_e and the
     distinct P_r rows (R*N*D once); bwd reads do and the sigma' operand x, writes do' (the layer-2 bwd,
     "rec", rebuilds x^1 from the distinct ES1 / P^1 rows and W^1[h_e] instead of reading it); dS reads
@@ -100,6 +104,8 @@ def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4):
               "tail_dS_tn": 2.0 * eb * D * T}[name]
     if eb == 2:
         hw_flops, peak_f = 2 * flops, MFMA_F16_PEAK_TFLOPS
+    elif gemm == "bf16x3":
+        hw_flops, peak_f = 6 * flops, MFMA_F16_PEAK_TFLOPS
     elif gemm == "split":
         hw_flops, peak_f = 3 * flops, MFMA_F16_PEAK_TFLOPS
     else:
@@ -333,7 +339,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         out["ranks_consistent"] = consist == 0.0
         out["params_max_abs_diff_vs_rank0"] = consist
     if other_mode and feat == "f32":
-        mode2 = "exact" if gemm == "split" else "split"
+        mode2 = "exact" if gemm != "exact" else "bf16x3"
         el2, loss2, _ = timed_run(mode2, False)
         out["other_gemm_mode"] = {"gemm": mode2, "dtype": DTYPE[mode2], "value": M / (el2 / steps),
                                   "ms_per_step": el2 / steps * 1e3, "loss": loss2}
@@ -371,7 +377,7 @@ def main():
                          "row-partitioned SpMMs (A_r E all-gathered, dAE reduce-scattered; node GEMMs replicated)")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],
                     help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
-    ap.add_argument("--gemm", default="exact", choices=["exact", "split"],
+    ap.add_argument("--gemm", default="exact", choices=["exact", "bf16x3", "split"],
                     help="operand precision of the D=256 MFMA GEMMs: exact f32 (the reference's arithmetic, the "
                          "headline) or the opt-in split-fp16 operands (timed too, under other_gemm_mode)")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")

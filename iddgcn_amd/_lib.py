@@ -12,10 +12,10 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
-GEMM_EXACT_F32, GEMM_SPLIT_F16, GEMM_F32_4CHAIN = 0, 1, 2
+GEMM_EXACT_F32, GEMM_SPLIT_F16, GEMM_F32_4CHAIN, GEMM_BF16X3 = 0, 1, 2, 3
 PLANES_A, PLANES_C, PLANES_AUX = 1, 2, 4          # iddgcn_rowgemm_t.planes (pre-split edge tables, ABI 4)
 
 vp = ctypes.c_void_p

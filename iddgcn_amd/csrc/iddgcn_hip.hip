@@ -27,6 +27,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 #define MAX_R 8
 #define EPS_BCE 1e-7f
@@ -1641,6 +1642,532 @@ __global__ __launch_bounds__(512) void gemm_tn256_bf16_kernel(long long M, long 
         }
 }
 
+// ---------------------------------------------------------------------------
+// bf16x3 operands (IDDGCN_GEMM_BF16X3), D = 256.  Every fp32 operand value x is the EXACT sum of three
+// bf16 values:  b0 = bf16_rne(x), b1 = bf16_rne(x - b0), b2 = (x - b0) - b1.  Each difference is exact in
+// fp32 and an fp32 significand has 24 bits = 3 x 8, so b2 is exact (while x is above ~2^-110, where b2 would
+// go subnormal).  A product a*w takes the six piece products of order >= 2^-16:
+//   a0 w0 | a0 w1 + a1 w0 | a1 w1 + a0 w2 + a2 w0
+// on bf16 MFMAs (bf16 x bf16 products are exact, accumulation fp32); the dropped a1 w2 + a2 w1 + a2 w2 are at
+// most 2^-23 |a w| (|a1| <= 2^-8 |a|, |a2| <= 2^-16 |a|), the size of fp32's own rounding of one product.
+// MFMA cost: 6 x v_mfma_f32_16x16x32_bf16 (16 cycles) per 32 k-values against 16 x v_mfma_f32_32x32x2_f32
+// (64 cycles) per 32 k-values x 2 column halves in the exact mode: 2.7x the exact mode's rate per flop.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void split3(float x, __bf16& b0, __bf16& b1, __bf16& b2) {
+    b0 = (__bf16)x;
+    const float r1 = x - (float)b0;
+    b1 = (__bf16)r1;
+    b2 = (__bf16)(r1 - (float)b1);
+}
+__device__ __forceinline__ void split3x4(const f32x4& v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        __bf16 a, b, c;
+        split3(v[q], a, b, c);
+        p0[q] = a;
+        p1[q] = b;
+        p2[q] = c;
+    }
+}
+// a staged fp32 row of 256 values (bytes [0, 1024) of `row`) -> its three bf16 planes in place: plane j at
+// bytes [512 j, 512 j + 512), column k at byte 2k of its plane.  The wave's one ds_read_b128 of the whole row
+// precedes (data dependence) the stores that overwrite it.
+__device__ __forceinline__ void row_to_planes3(char* row, int lane) {
+    const f32x4 x = ld4(reinterpret_cast<const float*>(row) + lane * 4);
+    bf16x4 p0, p1, p2;
+    split3x4(x, p0, p1, p2);
+    *reinterpret_cast<bf16x4*>(row + lane * 8) = p0;
+    *reinterpret_cast<bf16x4*>(row + 512 + lane * 8) = p1;
+    *reinterpret_cast<bf16x4*>(row + 1024 + lane * 8) = p2;
+}
+
+// ---- row GEMM, bf16x3 operands: C = epilogue(A B) over T rows --------------------------------------------
+// The 256 x 256 weight as three bf16 planes is 384 KiB: it cannot live in one CU's registers beside
+// anything else, so each workgroup owns ONE column half (128 columns, 192 KiB of planes = 96 VGPRs per lane
+// in each of 8 waves, 16 columns per wave).  The two halves of a row range run on workgroups 8 apart, i.e.
+// on the same XCD (workgroup b -> XCD b mod 8), so the second workgroup's read of an A tile hits L2.
+//   * MFMA v_mfma_f32_16x16x32_bf16 with the weight planes as operand A (16 columns x 32 k) and the A tile
+//     as operand B: lane l ends with edge rows l&15 and 16 + (l&15), columns c0 + 4(l>>4) .. +3.
+//   * A tiles (32 rows) arrive by LDS-DMA into 1568-B row slots and each wave converts its 4 rows in place
+//     to the three planes; fragment reads are ds_read_b128 (row l&15 at k-chunk l>>4: the 1568-B pitch,
+//     8 banks mod 64, makes every 16-lane group of the read conflict-free).
+//   * accumulators: a0 w0 in one, the five smaller products in a second (fp32), summed at the end.
+//   * epilogue as the v3 kernel: gathered P_r[t] rows (the tile's distinct tails), per-edge coefficients
+//     and sigma' rows DMA'd into wave-private slabs ([32][16] fp32, XOR-swizzled 16-B groups); waves 4-7 run
+//     the epilogue of tile t-1 while waves 0-3 run tile t's MFMAs on the same SIMDs; one barrier per tile.
+#ifndef B3_ABL
+#define B3_ABL 0     // experiment builds only: 1 skip the MFMAs, 2 skip the A DMA, 4 skip the conversion, 8 skip stores
+#endif
+#ifndef B3_PF
+#define B3_PF 2      // L2 prefetch of the A tile this many tiles beyond the one being DMA'd (0: none)
+#endif
+// s_waitcnt vmcnt(min(n, 15)) for a run-time, wave-uniform n: every vector-memory op of this wave but the n
+// youngest has completed (LDS-DMA, loads and stores count together, in issue order)
+__device__ __forceinline__ void wait_vm(int n) {
+#define WVM(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    switch (n < 15 ? n : 15) {
+        WVM(0) WVM(1) WVM(2) WVM(3) WVM(4) WVM(5) WVM(6) WVM(7)
+        WVM(8) WVM(9) WVM(10) WVM(11) WVM(12) WVM(13) WVM(14)
+        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+#undef WVM
+}
+namespace rb3 {
+constexpr int D = 256, NW = 8, TR = 32, CWG = 128, CWV = 16;
+constexpr int PITCH = 1568;                 // A row slot: three 512-B planes + 32 B
+constexpr int ABYTES = TR * PITCH;          // 50,176 B per A buffer (two buffers)
+constexpr int RPW = TR / NW;                // A rows each wave stages and converts
+constexpr int SLAB = TR * CWV;              // floats of a [32 rows][16 columns] slab
+}  // namespace rb3
+// float offset of (slot, 16-B column group g) in a [32][16] slab: groups XOR (-(slot / 4)) & 3, so the
+// epilogue's ds_read_b128 (slot l&15 [+16], group l>>4) is conflict-free in each of its four lane groups
+__device__ __forceinline__ int slab16_off(int slot, int g) { return slot * 16 + 4 * (g ^ ((-(slot >> 2)) & 3)); }
+
+template <int NV, bool AUX>
+__global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ranges) {
+    using namespace rb3;
+    static_assert(NV >= 0 && NV <= 2 && !(NV > 0 && AUX), "b3: gathered forward (NV = R = 1, 2), sigma' backward, plain");
+    constexpr int NSL = NV + (AUX ? 1 : 0);
+    constexpr int WF = NSL * SLAB + 64 + 64 + 32 + 256;         // slabs, coef [32][R], idx [64], cmp [32], prefetch KiB
+    constexpr int LDSB = 2 * ABYTES + NW * WF * 4;
+    static_assert(LDSB <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char lds[LDSB];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int i = lane & 15, g = lane >> 4;
+    const int bx = blockIdx.x;
+    const int half = (bx >> 3) & 1;
+    const int range = ((bx >> 4) << 3) | (bx & 7);
+    if (range >= n_ranges) return;
+    const int c0 = half * CWG + wave * CWV;
+    float* slabw = reinterpret_cast<float*>(lds + 2 * ABYTES) + wave * WF;
+    float* coefw = slabw + NSL * SLAB;
+    int* idxw = reinterpret_cast<int*>(coefw + 64);
+    int* cmpw = idxw + 64;
+    float* pfw = reinterpret_cast<float*>(cmpw + 32);          // L2-prefetch landing KiB (never read)
+
+    const long long ntiles = ((long long)p.M + TR - 1) / TR;
+    const long long t_beg = (long long)range * p.tiles_per_block;
+    long long t_end = t_beg + p.tiles_per_block;
+    if (t_end > ntiles) t_end = ntiles;
+    if (t_beg >= t_end) return;
+    const long long Mlast = (long long)p.M - 1;
+    auto clampe = [&](long long e) __attribute__((always_inline)) { return e > Mlast ? Mlast : e; };
+
+    // weight planes: k-step q (32 k), lane l: column c0 + (l&15), k = 32q + 8(l>>4) + e
+    bf16x8 w0[8], w1[8], w2[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 32 * q + 8 * g + e;
+            const float wv = p.b_trans ? p.B[(c0 + i) * D + k] : p.B[k * D + c0 + i];
+            __bf16 a, b, c;
+            split3(wv, a, b, c);
+            w0[q][e] = a;
+            w1[q][e] = b;
+            w2[q][e] = c;
+        }
+
+    // Every issue site returns its count of vector-memory ops (wave-uniform), so each wait below is the exact
+    // vmcnt for what it needs, never a drain of the prefetches behind it.
+    auto dma_idx = [&](long long t) __attribute__((always_inline)) -> int {
+        if (NV == 0 || !p.v_idx || t >= t_end) return 0;
+        const int* src = p.v_idx + (lane < 32 ? clampe(t * TR + lane) : 0);
+        __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)idxw, 4, 0, 0);
+        return 1;
+    };
+    auto dma_A = [&](long long t, int bb) __attribute__((always_inline)) -> int {
+        if (t >= t_end) return 0;
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int r = wave * RPW + j;
+            const float* src = p.A + ((B3_ABL & 2) ? (long long)r : clampe(t * TR + r)) * D + lane * 4;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(lds + bb * ABYTES + r * PITCH), 16, 0, 0);
+        }
+        return RPW;
+    };
+    // L2 prefetch of this wave's 4 A rows of tile t: one DMA, a 16-B read per 64 B (16 lanes per row) into a
+    // wave-private scratch KiB of LDS that nothing reads; the later A DMA of the tile then hits L2
+    auto prefetch = [&](long long t) __attribute__((always_inline)) -> int {
+        if (B3_PF == 0 || (B3_ABL & 2) || t >= t_end) return 0;
+        const float* src = p.A + clampe(t * TR + wave * RPW + (lane >> 4)) * D + (lane & 15) * 16;
+        __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)pfw, 16, 0, 0);
+        return 1;
+    };
+    auto convert = [&](int bb) __attribute__((always_inline)) {
+        if (B3_ABL & 4) return;
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) row_to_planes3(lds + bb * ABYTES + (wave * RPW + j) * PITCH, lane);
+    };
+    // the tile's distinct V rows (runs of equal v_idx; tail-sorted edges give 1-3 per tile) into slots 0..u-1,
+    // each lane's two rows' slots (vs0: row l&15, vs1: row 16 + (l&15)); sigma' rows; coefficients
+    int vs0 = 0, vs1 = 0;
+    auto dma_slabs = [&](long long t) __attribute__((always_inline)) -> int {
+        int n = 0;
+        if constexpr (NV > 0) {
+            int vi = 0;
+            bool start = false;
+            if (lane < 32) {
+                const long long e = clampe(t * TR + lane);
+                vi = p.v_idx ? idxw[lane] : (int)e;
+                const int prev = p.v_idx ? idxw[lane > 0 ? lane - 1 : 0] : (int)e - 1;
+                start = lane == 0 || vi != prev;
+            }
+            const unsigned long long m = __ballot(start);
+            const int u = __popcll(m);
+            vs0 = __popcll(m & ((2ull << i) - 1)) - 1;
+            vs1 = __popcll(m & ((2ull << (16 + i)) - 1)) - 1;
+            if (start) cmpw[__popcll(m & ((2ull << lane) - 1)) - 1] = vi;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int kb = 0; kb < u; kb += 16) {
+                const int slot = kb + (lane >> 2);
+                const int gg = (lane & 3) ^ ((-(slot >> 2)) & 3);
+                const long long v = cmpw[slot < u ? slot : u - 1];
+#pragma unroll
+                for (int r = 0; r < NV; ++r) {
+                    const float* src = p.V + r * p.v_rel_stride + v * D + c0 + gg * 4;
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(slabw + r * SLAB + kb * 16), 16, 0, 0);
+                }
+                n += NV;
+            }
+            // 32 x R per-edge coefficients, one 4-B DMA per lane (lanes past 32 R re-read the last value)
+            const long long last = (long long)p.M * NV - 1;
+            long long ci = t * TR * NV + lane;
+            if (ci > last) ci = last;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + ci), (lds_vptr)coefw, 4, 0, 0);
+            n += 1;
+        }
+        if constexpr (AUX) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int slot = 16 * k + (lane >> 2);
+                const int gg = (lane & 3) ^ ((-(slot >> 2)) & 3);
+                const float* src = p.aux + clampe(t * TR + slot) * D + c0 + gg * 4;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(slabw + NV * SLAB + k * 256), 16, 0, 0);
+            }
+            n += 2;
+        }
+        return n;
+    };
+    auto epilogue = [&](long long t, const f32x4 (&acc)[2]) __attribute__((always_inline)) -> int {
+        const long long row0 = t * TR;
+        const long long left = (long long)p.M - row0;
+        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
+        const __amdgpu_buffer_rsrc_t rc =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(p.C) + row0 * D * 4, (short)0, nbytes, 0x00020000);
+#pragma unroll
+        for (int rh = 0; rh < 2; ++rh) {
+            const int row = 16 * rh + i;
+            f32x4 v = acc[rh];
+            if constexpr (NV > 0) {
+                const int vs = rh ? vs1 : vs0;
+#pragma unroll
+                for (int r = 0; r < NV; ++r) {
+                    const float cf = coefw[row * NV + r];
+                    const f32x4 s = ld4(slabw + r * SLAB + slab16_off(vs, g));
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = fmaf(cf, s[q], v[q]);
+                }
+            }
+            if (p.act == IDDGCN_ACT_SIGMOID) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
+            } else if (AUX && p.act == IDDGCN_ACT_DSIGMOID) {
+                const f32x4 x = ld4(slabw + NV * SLAB + slab16_off(row, g));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = v[q] * (x[q] * (1.0f - x[q]));
+            }
+            if (B3_ABL & 8) asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+            else __builtin_amdgcn_raw_buffer_store_b128(v, rc, (row * D + c0 + 4 * g) * 4, 0, 0);
+        }
+        return (B3_ABL & 8) ? 0 : 2;
+    };
+    auto mfma_tile = [&](int bb, f32x4 (&acc)[2]) __attribute__((always_inline)) {
+        f32x4 hi0 = {0.f, 0.f, 0.f, 0.f}, lo0 = hi0, hi1 = hi0, lo1 = hi0;
+        // Fragment reads in inline asm, one k-step ahead of the MFMAs that use them, each k-step's MFMAs behind an
+        // s_waitcnt lgkmcnt(6) that "defines" its six fragments (so the MFMAs cannot be scheduled above it): the
+        // compiler's own waits were lgkmcnt(0) right after the next k-step's loads, exposing the LDS latency once
+        // per k-step (8 per tile) in a phase no partner wave covers (tools/bench_gemm.py: ~2x the MFMA time)
+        const unsigned ab = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(lds + bb * ABYTES) +
+                            i * PITCH + 16 * g;
+        u32x4 fx[2][3], fy[2][3];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#define B3_LOADQ(Q, S)                                                                                    \
+        asm volatile("ds_read_b128 %0, %6 offset:%7\n\tds_read_b128 %1, %6 offset:%8\n\t"                 \
+                     "ds_read_b128 %2, %6 offset:%9\n\tds_read_b128 %3, %6 offset:%10\n\t"                \
+                     "ds_read_b128 %4, %6 offset:%11\n\tds_read_b128 %5, %6 offset:%12"                   \
+                     : "=v"(fx[S][0]), "=v"(fx[S][1]), "=v"(fx[S][2]), "=v"(fy[S][0]), "=v"(fy[S][1]),     \
+                       "=v"(fy[S][2])                                                                   \
+                     : "v"(ab), "i"(64 * (Q)), "i"(64 * (Q) + 512), "i"(64 * (Q) + 1024),                \
+                       "i"(64 * (Q) + 16 * PITCH), "i"(64 * (Q) + 16 * PITCH + 512),                      \
+                       "i"(64 * (Q) + 16 * PITCH + 1024)                                                 \
+                     : "memory")
+        if (!(B3_ABL & 1)) B3_LOADQ(0, 0);
+#pragma unroll
+        for (int q = 0; q < ((B3_ABL & 1) ? 0 : 8); ++q) {
+            const int S = q & 1;
+            if (q + 1 < 8) {
+                switch (q) {      // the offsets are immediates: one asm per k-step
+                    case 0: B3_LOADQ(1, 1); break;
+                    case 1: B3_LOADQ(2, 0); break;
+                    case 2: B3_LOADQ(3, 1); break;
+                    case 3: B3_LOADQ(4, 0); break;
+                    case 4: B3_LOADQ(5, 1); break;
+                    case 5: B3_LOADQ(6, 0); break;
+                    default: B3_LOADQ(7, 1); break;
+                }
+                asm volatile("s_waitcnt lgkmcnt(6)"
+                             : "+v"(fx[S][0]), "+v"(fx[S][1]), "+v"(fx[S][2]), "+v"(fy[S][0]), "+v"(fy[S][1]),
+                               "+v"(fy[S][2])::"memory");
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(fx[S][0]), "+v"(fx[S][1]), "+v"(fx[S][2]), "+v"(fy[S][0]), "+v"(fy[S][1]),
+                               "+v"(fy[S][2])::"memory");
+            }
+            const bf16x8 x0 = __builtin_bit_cast(bf16x8, fx[S][0]), x1 = __builtin_bit_cast(bf16x8, fx[S][1]),
+                         x2 = __builtin_bit_cast(bf16x8, fx[S][2]);
+            const bf16x8 y0 = __builtin_bit_cast(bf16x8, fy[S][0]), y1 = __builtin_bit_cast(bf16x8, fy[S][1]),
+                         y2 = __builtin_bit_cast(bf16x8, fy[S][2]);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], x2, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], y2, lo1, 0, 0, 0);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2[q], x0, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2[q], y0, lo1, 0, 0, 0);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[q], x1, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[q], y1, lo1, 0, 0, 0);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], x1, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], y1, lo1, 0, 0, 0);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[q], x0, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[q], y0, lo1, 0, 0, 0);
+            hi0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], x0, hi0, 0, 0, 0);
+            hi1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], y0, hi1, 0, 0, 0);
+        }
+#undef B3_LOADQ
+        acc[0] = hi0 + lo0;
+        acc[1] = hi1 + lo1;
+    };
+
+    // prologue: indices, A and slabs of t_beg; A converted; indices of t_beg + 1; L2 prefetch of the first tiles
+    dma_idx(t_beg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dma_A(t_beg, 0);
+    dma_slabs(t_beg);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    convert(0);
+    dma_idx(t_beg + 1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    for (int k = 1; k <= B3_PF; ++k) prefetch(t_beg + k);
+    __syncthreads();
+
+    // per iteration t: A(t+1) DMA, then the L2 prefetch of A(t+1+B3_PF); waves 4-7 run epilogue(t-1) and the slab /
+    // index DMAs of t, t+1 before MFMA(t), waves 0-3 epilogue(t) and those of t+1, t+2 after it
+#define B3_MAIN_LOOP(LATE)                                                                           \
+    {                                                                                                \
+        f32x4 acc[2];                                                                                \
+        int b = 0;                                                                                   \
+        for (long long t = t_beg; t < t_end; ++t) {                                                  \
+            const bool more = t + 1 < t_end;                                                         \
+            const int nA = dma_A(t + 1, b ^ 1);                                                      \
+            const int npf = prefetch(t + 1 + B3_PF);                                                 \
+            int after_A = npf;                      /* ops issued after A(t+1) */                    \
+            if (LATE && t > t_beg) {                                                                 \
+                wait_vm(nA + npf);                  /* slabs(t-1), idx(t) */                         \
+                after_A += epilogue(t - 1, acc);                                                     \
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
+                after_A += dma_slabs(t);                                                             \
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
+                after_A += dma_idx(t + 1);                                                           \
+            }                                                                                        \
+            mfma_tile(b, acc);                                                                       \
+            if (LATE) {                                                                              \
+                if (more) {                                                                          \
+                    wait_vm(after_A);                                                                \
+                    convert(b ^ 1);                                                                  \
+                }                                                                                    \
+            } else {                                                                                 \
+                wait_vm(nA + npf);                  /* slabs(t), idx(t+1) */                         \
+                after_A += epilogue(t, acc);                                                         \
+                if (more) {                                                                          \
+                    wait_vm(after_A);               /* A(t+1) */                                     \
+                    convert(b ^ 1);                                                                  \
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                               \
+                    dma_slabs(t + 1);                                                                \
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                               \
+                    dma_idx(t + 2);                                                                  \
+                }                                                                                    \
+            }                                                                                        \
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                       \
+            __builtin_amdgcn_s_barrier();                                                            \
+            asm volatile("" ::: "memory");                                                           \
+            b ^= 1;                                                                                  \
+        }                                                                                            \
+        if (LATE) {                                                                                  \
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                         \
+            epilogue(t_end - 1, acc);                                                                \
+        }                                                                                            \
+    }
+    if (wave >= 4) B3_MAIN_LOOP(true) else B3_MAIN_LOOP(false)
+#undef B3_MAIN_LOOP
+}
+
+// ---- TN reduction GEMM, bf16x3 operands: C = A^T B over M rows, partial per workgroup --------------------
+// Wave w owns output rows 32w..32w+31 (columns of A) x all 256 columns (8 accumulator tiles, 128 VGPRs).
+// 16-row tiles of A and B (one v_mfma_f32_32x32x16_bf16 k-step) arrive by LDS-DMA into 1600-B row slots,
+// three buffers deep; each wave converts its 2 rows of each operand in place to the three bf16 planes, and
+// the MFMA fragments (8 consecutive rows of one column) are read with ds_read_b64_tr_b16 from the row-major
+// planes (1600-B pitch = 16 banks mod 64: each 32-lane half's four rows x 64 B are conflict-free).  Six
+// MFMAs per (k-step, column tile) into one fp32 accumulator, the smaller products first.  Waves 4-7 convert
+// tile t+1 before their MFMAs of tile t, waves 0-3 after theirs: a SIMD's two waves overlap conversion and
+// MFMA.  One barrier per tile.
+#ifndef TB3_ABL
+#define TB3_ABL 0    // experiment builds only: 2 skip the MFMAs, 4 skip the conversion, 8 skip the DMA
+#endif
+namespace tb3 {
+constexpr int D = 256, TK = 16, PT = 1600, OPB = TK * PT, BUF = 2 * OPB, NBUF = 3;
+}  // namespace tb3
+__device__ __forceinline__ bf16x8 tr_frag_b3(const char* p0) {
+    typedef __attribute__((address_space(3))) v4s16* l4p;
+    const v4s16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)p0);
+    const v4s16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)(p0 + 4 * tb3::PT));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+__global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long long rows_per_block,
+                                                            const float* __restrict__ A, const float* __restrict__ B,
+                                                            float* __restrict__ slab) {
+    using namespace tb3;
+    static_assert(NBUF * BUF <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * BUF];     // [buf][A | B][TK][PT]
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool late = wave >= 4;
+    f32x16 acc[8];
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[cj][j] = 0.f;
+    const long long r_beg = (long long)blockIdx.x * rows_per_block;
+    long long r_end = r_beg + rows_per_block;
+    if (r_end > M) r_end = M;
+    const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
+
+    // rows 2w, 2w+1 of both operands of tile t into buffer bb (rows past the range as fp32 zeros); returns the
+    // LDS-DMA count (wave-uniform)
+    auto stage = [&](long long t, int bb) __attribute__((always_inline)) {
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = 2 * wave + j;
+            const long long e = r_beg + t * TK + r;
+            char* ra = lds + bb * BUF + r * PT;
+            if (e < r_end) {
+                if (TB3_ABL & 8) continue;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)(A + e * D + lane * 4), (lds_vptr)ra, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gbl_vptr)(B + e * D + lane * 4), (lds_vptr)(ra + OPB), 16, 0, 0);
+                n += 2;
+            } else {
+                st4(reinterpret_cast<float*>(ra) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                st4(reinterpret_cast<float*>(ra + OPB) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+            }
+        }
+        return n;
+    };
+    auto convert = [&](int bb) __attribute__((always_inline)) {
+        if (TB3_ABL & 4) return;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            char* ra = lds + bb * BUF + (2 * wave + j) * PT;
+            row_to_planes3(ra, lane);
+            row_to_planes3(ra + OPB, lane);
+        }
+    };
+    auto wait_newest = [&](int n) __attribute__((always_inline)) {
+        if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    // this lane's transposed-read address: rows 8(l>>5) + ((l>>2)&3) (+4: second read), columns
+    // 16((l>>4)&1) + 4(l&3) of a 32-column block
+    const int roff = (8 * (lane >> 5) + ((lane >> 2) & 3)) * PT + 2 * (16 * ((lane >> 4) & 1) + 4 * (lane & 3));
+    auto mfma_tile = [&](int bb) __attribute__((always_inline)) {
+        const char* pa = lds + bb * BUF + roff + 64 * wave;
+        const bf16x8 a0 = tr_frag_b3(pa), a1 = tr_frag_b3(pa + 512), a2 = tr_frag_b3(pa + 1024);
+        // B fragments of column tile cj+1 in flight during tile cj's MFMAs (two register sets: the 128
+        // accumulator VGPRs leave no room for all eight tiles' fragments)
+        const char* pb0 = lds + bb * BUF + OPB + roff;
+        bf16x8 b0 = tr_frag_b3(pb0), b1 = tr_frag_b3(pb0 + 512), b2 = tr_frag_b3(pb0 + 1024);
+        // per tile the five smaller products start from zero and join the running sum with one fp32 add
+        // (v_add_f32, round-to-nearest-even) in front of the a0 b0 MFMA: all six MFMAs chained on the running sum
+        // over a block's 16k rows gave 1.46x the exact mode's fmaf-chain error (tools/bench_gemm.py)
+#pragma unroll
+        for (int cj = 0; cj < 8; ++cj) {
+            bf16x8 n0 = b0, n1 = b1, n2 = b2;          // column tile cj+1's fragments in flight
+            if (cj + 1 < 8) {
+                const char* pb = pb0 + 64 * (cj + 1);
+                n0 = tr_frag_b3(pb);
+                n1 = tr_frag_b3(pb + 512);
+                n2 = tr_frag_b3(pb + 1024);
+            }
+            f32x16 c;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) c[j] = 0.f;
+            if (!(TB3_ABL & 2)) {
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[cj] + c, 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            b0 = n0;
+            b1 = n1;
+            b2 = n2;
+        }
+    };
+
+    if (nt > 0) {
+        stage(0, 0);
+        const int n1 = nt > 1 ? stage(1, 1) : 0;
+        wait_newest(n1);
+        convert(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // one compile-time copy of the loop per half (one MFMA site each: the register allocator sees each path alone)
+#define TB3_LOOP(LATE)                                                               \
+    {                                                                                \
+        int b = 0;                                                                   \
+        for (long long t = 0; t < nt; ++t) {                                         \
+            const int b1 = b == 2 ? 0 : b + 1, b2 = b1 == 2 ? 0 : b1 + 1;            \
+            const int n2 = t + 2 < nt ? stage(t + 2, b2) : 0;                        \
+            if (LATE && t + 1 < nt) {                                                \
+                wait_newest(n2);                                                     \
+                convert(b1);                                                         \
+            }                                                                        \
+            mfma_tile(b);                                                            \
+            if (!LATE && t + 1 < nt) {                                               \
+                wait_newest(n2);                                                     \
+                convert(b1);                                                         \
+            }                                                                        \
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                       \
+            __builtin_amdgcn_s_barrier();                                            \
+            asm volatile("" ::: "memory");                                           \
+            b = b1;                                                                  \
+        }                                                                            \
+    }
+    if (late) TB3_LOOP(true) else TB3_LOOP(false)
+#undef TB3_LOOP
+    float* out = slab + (long long)blockIdx.x * D * D;
+    const int i = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int cj = 0; cj < 8; ++cj)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int row = 32 * wave + (j & 3) + 8 * (j >> 2) + 4 * h;
+            out[row * D + 32 * cj + i] = acc[cj][j];
+        }
+}
+
 // out[D][R] partial of A^T dz and colsum(dz) per block; slab row layout [(D+1)][R]
 template <int D>
 __global__ __launch_bounds__(D) void gemm_tn_narrow_kernel(long long M, long long rows_per_block, int R,
@@ -2683,7 +3210,7 @@ int check_rowgemm(const iddgcn_rowgemm_t& a) {
     if (!dim_ok(a.D)) return IDDGCN_E_BAD_DIM;
     if (a.R < 0 || a.R > MAX_R) return IDDGCN_E_BAD_REL;
     if (a.precision != IDDGCN_GEMM_EXACT_F32 && a.precision != IDDGCN_GEMM_SPLIT_F16 &&
-        a.precision != IDDGCN_GEMM_F32_4CHAIN)
+        a.precision != IDDGCN_GEMM_F32_4CHAIN && a.precision != IDDGCN_GEMM_BF16X3)
         return IDDGCN_E_BAD_ARG;
     // F32_4CHAIN at D = 256: the plain form (no coefficients, no sigma' operand, no planes)
     if (a.precision == IDDGCN_GEMM_F32_4CHAIN && a.D == 256 && (a.R > 0 || a.act == IDDGCN_ACT_DSIGMOID || a.planes))
@@ -2702,6 +3229,35 @@ int check_rowgemm(const iddgcn_rowgemm_t& a) {
         if (!v3_select(to_p(a), sel)) return IDDGCN_E_BAD_ARG;
     }
     return 0;
+}
+
+// The bf16x3 row GEMM's forms (rowgemm256_b3_kernel<NV, AUX>): plain, sigma' backward (AUX), gathered-combine
+// forward with exactly R = NV in {1, 2} per-edge coefficients; no a_idx, accumulate, coef_idx or planes.
+bool b3_select(const RowGemmP& p, int& nv, bool& aux) {
+    if (p.precision != IDDGCN_GEMM_BF16X3 || p.a_idx || p.accumulate || p.planes) return false;
+    if (p.R > 0) {
+        if (p.R > 2 || p.v_row_stride != 256 || p.coef_idx || p.act == IDDGCN_ACT_DSIGMOID) return false;
+        nv = p.R;
+        aux = false;
+        return true;
+    }
+    nv = 0;
+    aux = p.act == IDDGCN_ACT_DSIGMOID;
+    return true;
+}
+// ~128 row ranges (a multiple of 8) x 2 column halves: one 138-KB workgroup per CU, every one resident
+void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux) {
+    const long long nt = ((long long)p.M + rb3::TR - 1) / rb3::TR;
+    long long nr = nt < 128 ? nt : 128;
+    p.tiles_per_block = (int)((nt + nr - 1) / nr);
+    nr = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
+    nr = (nr + 7) / 8 * 8;
+    const dim3 g((unsigned)(2 * nr)), blk(512);
+    const int n_ranges = (int)nr;
+    if (nv == 1) hipLaunchKernelGGL((rowgemm256_b3_kernel<1, false>), g, blk, 0, st, p, n_ranges);
+    else if (nv == 2) hipLaunchKernelGGL((rowgemm256_b3_kernel<2, false>), g, blk, 0, st, p, n_ranges);
+    else if (aux) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, true>), g, blk, 0, st, p, n_ranges);
+    else hipLaunchKernelGGL((rowgemm256_b3_kernel<0, false>), g, blk, 0, st, p, n_ranges);
 }
 
 // One launch of up to ROWGEMM_BATCH v3 GEMMs of the same variant (blockIdx.y = entry).  The persistent
@@ -2853,6 +3409,15 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     if (a->M == 0) return 0;                 // nothing to do (an empty C may have a null pointer)
     RowGemmP p = to_p(*a);
     hipStream_t st = (hipStream_t)stream;
+    if (p.precision == IDDGCN_GEMM_BF16X3) {
+        int nv;
+        bool aux;
+        if (a->D == 256 && b3_select(p, nv, aux)) {
+            launch_b3(st, p, nv, aux);
+            return launch_status();
+        }
+        p.precision = IDDGCN_GEMM_EXACT_F32;      // the forms the bf16x3 kernel does not take: exact f32
+    }
     V3Sel sel;
     if (a->D == 256 && v3_select(p, sel)) {
         RowGemmBatch pb;
@@ -2883,7 +3448,13 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
 
 int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* a) {
     if (!a || !dim_ok(a->D)) return -1;
-    const RowGemmP p = to_p(*a);
+    RowGemmP p = to_p(*a);
+    if (p.precision == IDDGCN_GEMM_BF16X3) {
+        int nv;
+        bool aux;
+        if (a->D == 256 && b3_select(p, nv, aux)) return 500 + 10 * nv + (aux ? 1 : 0);
+        p.precision = IDDGCN_GEMM_EXACT_F32;
+    }
     V3Sel sel;
     if (a->D == 256 && v3_select(p, sel))
         return 300 + 10 * sel.nv + (sel.aux ? 1 : 0) + (sel.hc ? 2 : 0) + (sel.cw ? 8 : 0) + (sel.split ? 2000 : 0) +
@@ -2899,6 +3470,14 @@ int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* a, int n) {
         if (!dim_ok(a[k].D) || a[k].D != a[0].D) return IDDGCN_E_BAD_DIM;
         if (const int rc = check_rowgemm(a[k])) return rc;
     }
+    for (int k = 0; k < n && !one_launch; ++k)
+        if (a[k].precision == IDDGCN_GEMM_BF16X3) {      // D = 256 bf16x3: one call per entry
+            for (int j = 0; j < n; ++j) {
+                const int rc = iddgcn_rowgemm_f32(stream, a + j);
+                if (rc) return rc;
+            }
+            return 0;
+        }
     if (!one_launch) {          // D = 256: one v3 launch when every entry maps to the same variant
         RowGemmBatch pb;
         V3Sel sel0{}, sel{};
@@ -2959,13 +3538,16 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
                        float* C, int accumulate, int precision) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (M < 0 || n_blocks < 1 || !A || !B || !slab || !C) return IDDGCN_E_BAD_ARG;
-    if (precision != IDDGCN_GEMM_EXACT_F32 && precision != IDDGCN_GEMM_SPLIT_F16) return IDDGCN_E_BAD_ARG;
+    if (precision != IDDGCN_GEMM_EXACT_F32 && precision != IDDGCN_GEMM_SPLIT_F16 && precision != IDDGCN_GEMM_BF16X3)
+        return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;
     long long rpb = (M + n_blocks - 1) / n_blocks;
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
-    if (d == 256 && precision == IDDGCN_GEMM_SPLIT_F16) {
+    if (d == 256 && precision == IDDGCN_GEMM_BF16X3) {
+        hipLaunchKernelGGL(gemm_tn256_b3_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
+    } else if (d == 256 && precision == IDDGCN_GEMM_SPLIT_F16) {
         hipLaunchKernelGGL(gemm_tn256_x3_kernel<>, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab, TnBatch{});
     } else if (d == 256) {
         hipLaunchKernelGGL(gemm_tn256_dma_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
@@ -2986,7 +3568,8 @@ int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n,
                                int precision) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (n < 0 || n > IDDGCN_TN_BATCH || (n > 0 && (!e || !slab))) return IDDGCN_E_BAD_ARG;
-    if (precision != IDDGCN_GEMM_EXACT_F32 && precision != IDDGCN_GEMM_SPLIT_F16) return IDDGCN_E_BAD_ARG;
+    if (precision != IDDGCN_GEMM_EXACT_F32 && precision != IDDGCN_GEMM_SPLIT_F16 && precision != IDDGCN_GEMM_BF16X3)
+        return IDDGCN_E_BAD_ARG;
     for (int k = 0; k < n; ++k)
         if (e[k].M < 0 || (e[k].M > 0 && (!e[k].A || !e[k].B)) || !e[k].C) return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;

@@ -199,8 +199,9 @@ class Workspace:
         self.narrow_slab = e((ops.tn_narrow_blocks(N) + 1) * (D + 1) * R)
 
 
-GEMM_MODES = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16}
-PROJ_MODES = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16, "exact4": L.GEMM_F32_4CHAIN}
+GEMM_MODES = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16, "bf16x3": L.GEMM_BF16X3}
+PROJ_MODES = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16, "exact4": L.GEMM_F32_4CHAIN,
+              "bf16x3": L.GEMM_BF16X3}
 
 
 class Engine:
@@ -209,10 +210,12 @@ class Engine:
     ``gemm`` selects the operand precision of the D=256 MFMA GEMMs, passed with every GEMM call
     (include/iddgcn.h IDDGCN_GEMM_*, ABI 6: no process-global state, so engines in different modes may
     run side by side on different streams or threads): "exact" (default) runs v_mfma_f32_32x32x2_f32,
-    bitwise an fmaf chain — the reference's fp32 arithmetic; "split" splits every fp32 operand into two
-    fp16 halves with power-of-two row/column scales and accumulates in fp32 (within one fp32 ulp per
-    operand, 3 f16 MFMAs per k-step), an opt-in faster mode.  Other widths and all non-GEMM kernels are
-    exact f32 in both modes.
+    bitwise an fmaf chain — the reference's fp32 arithmetic; "bf16x3" splits every fp32 operand EXACTLY
+    into three bf16 pieces (24 significant bits: the whole fp32 value) and sums the six piece products of
+    order >= 2^-16 on bf16 MFMAs with fp32 accumulation (dropped terms <= 2^-23 |a w| per product, fp32's own
+    product rounding is 2^-24): fp32 arithmetic at 2.7x the f32 MFMA rate; "split" splits every fp32 operand
+    into two fp16 halves with power-of-two row/column scales (22 significant bits, 3 f16 MFMAs per k-step), an
+    opt-in faster mode.  Other widths and all non-GEMM kernels are exact f32 in every mode.
     """
 
     def __init__(self, num_entities, num_relations, dim, device=None, gemm="exact", features="f32", planes=True):
@@ -264,6 +267,8 @@ class Engine:
         the engine's ``gemm``."""
         if self._proj_gemm is not None:
             return self._proj_gemm
+        if self._gemm == "bf16x3" and self.D < 256:
+            return "exact4"
         return "exact4" if self._gemm == "exact" else self._gemm
 
     @property
@@ -272,7 +277,7 @@ class Engine:
         except at D < 256 in the exact mode, where the register-staged kernel takes "exact4" for every form (the
         four-chain accumulation costs nothing there and keeps the trained-weight logits of the reference's
         64-wide model further inside the 1e-4 bar)."""
-        return "exact4" if (self._gemm == "exact" and self.D < 256) else self._gemm
+        return "exact4" if (self._gemm in ("exact", "bf16x3") and self.D < 256) else self._gemm
 
     @proj_gemm.setter
     def proj_gemm(self, mode):

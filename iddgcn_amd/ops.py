@@ -25,15 +25,17 @@ def _ptr(t):
 
 
 _PRECISION = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16, "exact4": L.GEMM_F32_4CHAIN,
+              "bf16x3": L.GEMM_BF16X3,
               L.GEMM_EXACT_F32: L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16: L.GEMM_SPLIT_F16,
-              L.GEMM_F32_4CHAIN: L.GEMM_F32_4CHAIN}
+              L.GEMM_F32_4CHAIN: L.GEMM_F32_4CHAIN, L.GEMM_BF16X3: L.GEMM_BF16X3}
 
 
 def _prec(precision):
     """GEMM operand precision of one call (include/iddgcn.h IDDGCN_GEMM_*): "exact" / "split" / "exact4" (f32
-    MFMA with four interleaved accumulation chains: row GEMMs, plain form at D = 256) or the constant."""
+    MFMA with four interleaved accumulation chains: row GEMMs, plain form at D = 256) / "bf16x3" (every fp32
+    operand split exactly into three bf16 pieces, six bf16 MFMA products, fp32 accumulation) or the constant."""
     if precision not in _PRECISION:
-        raise L.IddgcnError(f"precision must be 'exact', 'split' or 'exact4', got {precision!r}")
+        raise L.IddgcnError(f"precision must be 'exact', 'split', 'exact4' or 'bf16x3', got {precision!r}")
     return _PRECISION[precision]
 
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 6
+#define IDDGCN_ABI_VERSION 7
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -52,10 +52,19 @@ extern "C" {
  *     four interleaved fp32 chains (k-block q of 8 values into chain q mod 4), summed pairwise at the end:
  *     4x shorter rounding chains, ~2x less accumulation error at K = 256; deterministic.  The node-level
  *     projections P_r^l = AE_r K_r^l (|P| up to ~1e3: AE_r sums ~20 entity rows) use it in the exact mode.
+ *   IDDGCN_GEMM_BF16X3 (ABI 7): every fp32 operand value is split EXACTLY into three bf16 pieces
+ *     x = b0 + b1 + b2 (b0 = bf16(x), b1 = bf16(x - b0), b2 = x - b0 - b1: 3 x 8 = 24 significant bits, the
+ *     whole fp32 significand, while |x| > ~2^-110), and a product takes the six piece products of order
+ *     >= 2^-16 on bf16 MFMAs (exact products, fp32 accumulation): a0w0 + a0w1 + a1w0 + a1w1 + a0w2 + a2w0.
+ *     The dropped terms are <= 2^-23 |a w| per product (fp32's own product rounding is <= 2^-24 |a w|).
+ *     Row GEMMs: the plain form, the gathered-combine forward with R = 1 or 2 per-edge coefficients (no
+ *     coef_idx) and the sigma' backward, without a_idx / accumulate / planes; every other form takes the
+ *     exact f32 kernel.  TN GEMMs: D = 256.  Deterministic; not bitwise equal to the exact mode.
  * Row GEMMs for D < 256 and every other kernel compute in exact f32 (or F32_4CHAIN where asked). */
 #define IDDGCN_GEMM_EXACT_F32 0
 #define IDDGCN_GEMM_SPLIT_F16 1
 #define IDDGCN_GEMM_F32_4CHAIN 2
+#define IDDGCN_GEMM_BF16X3 3
 
 /* Pre-split edge tables ("planes", ABI 4; D = 256, split-fp16 GEMM mode only).  A row of values in
  * [0, 1] (sigmoid outputs) stored as 8 column blocks of 128 B, block b = [hi f16 of columns 32b..32b+31 |
@@ -111,7 +120,7 @@ typedef struct {
     int act; const float* aux;
     int planes;           /* IDDGCN_PLANES_* flags (ABI 4; 0 = every table fp32).  Nonzero needs D = 256,
                              the split-fp16 mode and no a_idx; invalid combinations return IDDGCN_E_BAD_ARG */
-    int precision;        /* IDDGCN_GEMM_EXACT_F32 (0), _SPLIT_F16 or _F32_4CHAIN (ABI 6: per call) */
+    int precision;        /* IDDGCN_GEMM_EXACT_F32 (0), _SPLIT_F16, _F32_4CHAIN or _BF16X3 (per call) */
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
 
@@ -120,8 +129,8 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
  * form (C or aux planes) + 2000 for split-fp16 operands + 4000 for F32_4CHAIN, for the D = 256 v3 pipeline (NV = gathered V
  * tables: 1, 2, or capacity 4 / 8 for R <= 8, whose LDS slabs keep 7 distinct V rows per 32-row tile
  * and read further ones from L2); 100 for the register-staged kernel (D < 256, and D = 256 forms the v3
- * kernel does not take: a gathered V with the sigma' epilogue, V rows that are not dense); -1 for an
- * invalid D. */
+ * kernel does not take: a gathered V with the sigma' epilogue, V rows that are not dense); 500 + 10*NV + aux
+ * for the bf16x3 row GEMM (IDDGCN_GEMM_BF16X3 forms it takes); -1 for an invalid D. */
 int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* args);
 
 /* C[D][D] (+)= A^T · B over M rows (A, B are M x D).  Two stages: each of n_blocks

@@ -54,7 +54,7 @@ def cfg3(cuda):
 
 
 @pytest.mark.parametrize("init", ["mild", "reference"])
-@pytest.mark.parametrize("gemm", ["split", "exact"])
+@pytest.mark.parametrize("gemm", ["split", "exact", "bf16x3"])
 def test_config3_forward_vs_oracle_sample(cfg3, init, gemm, cuda):
     params = mild_params() if init == "mild" else init_params(N, R, D, seed=89)
     eng, ed, sample = cfg3["eng"], cfg3["ed"], cfg3["sample"]
@@ -80,18 +80,21 @@ def test_config3_step_deterministic_and_modes_agree(cfg3, cuda):
     P = FlatParams(N, R, D, cuda)
     P.load(params)
     out = {}
-    for key, gemm in (("split", "split"), ("split_again", "split"), ("exact", "exact")):
+    for key, gemm in (("split", "split"), ("split_again", "split"), ("exact", "exact"), ("b3", "bf16x3"),
+                      ("b3_again", "bf16x3")):
         eng.gemm = gemm
         G = FlatParams(N, R, D, cuda)
         loss, p = eng.loss_and_grads(P, G, adj, ed)
         out[key] = (float(loss.item()), p.cpu().numpy(), G.to_numpy())
         del G
-    a, b, c = out["split"], out["split_again"], out["exact"]
-    assert a[0] == b[0] and np.array_equal(a[1], b[1])                       # bitwise run to run
-    assert all(np.array_equal(a[2][k], b[2][k]) for k in a[2])
-    assert abs(a[0] - c[0]) <= 1e-6 * abs(c[0])
-    np.testing.assert_allclose(a[1], c[1], rtol=0, atol=1e-5)
-    for k in a[2]:
-        scale = np.abs(c[2][k]).max()
-        assert np.all(np.isfinite(a[2][k])), k
-        assert np.abs(a[2][k] - c[2][k]).max() <= 2e-4 * scale + 1e-30, k
+    c = out["exact"]
+    for m in ("split", "b3"):
+        a, b = out[m], out[m + "_again"]
+        assert a[0] == b[0] and np.array_equal(a[1], b[1]), m                    # bitwise run to run
+        assert all(np.array_equal(a[2][k], b[2][k]) for k in a[2]), m
+        assert abs(a[0] - c[0]) <= 1e-6 * abs(c[0]), m
+        np.testing.assert_allclose(a[1], c[1], rtol=0, atol=1e-5)
+        for k in a[2]:
+            scale = np.abs(c[2][k]).max()
+            assert np.all(np.isfinite(a[2][k])), (m, k)
+            assert np.abs(a[2][k] - c[2][k]).max() <= 2e-4 * scale + 1e-30, (m, k)

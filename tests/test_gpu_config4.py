@@ -63,7 +63,8 @@ def cfg4(cuda):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("init,gemm", [("mild", "exact"), ("reference", "exact"), ("mild", "split")])
+@pytest.mark.parametrize("init,gemm", [("mild", "exact"), ("reference", "exact"), ("mild", "split"),
+                                       ("reference", "bf16x3")])
 def test_config4_forward_vs_oracle_sample(cfg4, init, gemm, cuda):
     params = mild_params() if init == "mild" else init_params(N, R, D, seed=89)
     eng, ed, sample = cfg4["eng"], cfg4["ed"], cfg4["sample"]
@@ -91,20 +92,22 @@ def test_config4_step_deterministic_and_modes_agree(cfg4, cuda):
     P = FlatParams(N, R, D, cuda)
     P.load(mild_params(2))
     out = {}
-    for key, gemm in (("exact", "exact"), ("exact_again", "exact"), ("split", "split")):
+    for key, gemm in (("exact", "exact"), ("exact_again", "exact"), ("split", "split"), ("b3", "bf16x3")):
         eng.gemm = gemm
         G = FlatParams(N, R, D, cuda)
         loss, p = eng.loss_and_grads(P, G, adj, ed)
         out[key] = (float(loss.item()), p.cpu().numpy(), G.to_numpy())
         del G, p
     eng.release()
-    a, b, c = out["exact"], out["exact_again"], out["split"]
+    a, b = out["exact"], out["exact_again"]
     assert np.isfinite(a[0]) and a[0] > 0
     assert a[0] == b[0] and np.array_equal(a[1], b[1])                       # bitwise run to run
     assert all(np.array_equal(a[2][k], b[2][k]) for k in a[2])
-    assert abs(c[0] - a[0]) <= 1e-6 * abs(a[0])
-    np.testing.assert_allclose(c[1], a[1], rtol=0, atol=1e-5)
-    for k in a[2]:
-        scale = np.abs(a[2][k]).max()
-        assert np.all(np.isfinite(a[2][k])), k
-        assert np.abs(c[2][k] - a[2][k]).max() <= 2e-4 * scale + 1e-30, k
+    for m in ("split", "b3"):
+        c = out[m]
+        assert abs(c[0] - a[0]) <= 1e-6 * abs(a[0]), m
+        np.testing.assert_allclose(c[1], a[1], rtol=0, atol=1e-5)
+        for k in a[2]:
+            scale = np.abs(a[2][k]).max()
+            assert np.all(np.isfinite(a[2][k])), k
+            assert np.abs(c[2][k] - a[2][k]).max() <= 2e-4 * scale + 1e-30, (m, k)

@@ -590,6 +590,130 @@ def test_gemm_tn_split_f16_vs_fp64(M, kind, cuda):
     assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
 
 
+B3_FORMS = ["plain", "trans", "combine", "combine_r1", "combine_runs", "combine_random", "dsig", "small_M",
+            "tiny_M", "row_decades", "zero_rows"]
+B3_FALLBACK = ["accumulate", "gatherA", "rank_bcast", "coef_idx"]
+
+
+@pytest.mark.parametrize("mode", B3_FORMS + B3_FALLBACK)
+def test_rowgemm_bf16x3_vs_fp64(mode, cuda):
+    """bf16x3 operand mode (IDDGCN_GEMM_BF16X3, D = 256: every fp32 operand split exactly into three bf16
+    pieces, six bf16 MFMA products, fp32 accumulation): error vs an fp64 torch reference within 1.25x the
+    exact-f32 MFMA path's (floor 1e-6 of max|ref|) on every form the bf16x3 kernel takes (the column-half
+    kernel is asserted: 500 + 10 NV + aux), incl. ragged and tiny M, tiles with up to 32 distinct gathered rows,
+    rows spanning 12 decades (per-row error 1e-5) and zero rows; deterministic run to run.  The forms it does
+    not take (accumulate, gathered A, broadcast V, coef_idx) run the exact kernel: bitwise the exact mode."""
+    g = torch.Generator().manual_seed(sum(map(ord, mode)) + 7)
+    D, N, R = 256, 700, (1 if mode == "combine_r1" else 2)
+    M = {"small_M": 77, "tiny_M": 5}.get(mode, 20_000 + 17)
+    A = torch.rand(M, D, generator=g, dtype=torch.float64)
+    if mode == "row_decades":
+        A = torch.randn(M, D, generator=g, dtype=torch.float64) * 10 ** (12 * torch.rand(M, 1, generator=g,
+                                                                                        dtype=torch.float64) - 6)
+    if mode == "zero_rows":
+        A[::3] = 0
+    S = torch.randn(D, D, generator=g, dtype=torch.float64)
+    A, S = A.to(cuda), S.to(cuda)
+    kw, C0 = {}, None
+    Af, Sf = A.float(), S.float()
+    kid = 500
+    if mode in ("combine", "combine_r1", "combine_runs", "combine_random", "coef_idx"):
+        W = torch.rand(N, R, generator=g, dtype=torch.float64).to(cuda)
+        P = (torch.randn(R, N, D, generator=g, dtype=torch.float64) * 4).to(cuda)
+        h = torch.randint(0, N, (M,), generator=g).to(cuda)
+        t = torch.randint(0, N, (M,), generator=g).sort().values.to(cuda)
+        if mode == "combine_runs":
+            t = _run_structured_idx(M, N, g).to(cuda)
+        if mode == "combine_random":        # up to 32 distinct gathered rows per tile (two DMA rounds)
+            t = torch.randint(0, N, (M,), generator=g).to(cuda)
+        if mode == "coef_idx":
+            kw = dict(coef=W.float(), coef_idx=h.int())
+        else:
+            kw = dict(coef=W[h].float().contiguous())
+        kw.update(V=P.float(), v_idx=t.int(), v_rel_stride=N * D, act=L.ACT_SIGMOID)
+        ref = torch.sigmoid(A @ S + sum(W[h, r:r + 1] * P[r][t] for r in range(R)))
+        kid = 500 + 10 * R
+    elif mode == "dsig":
+        X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
+        kw = dict(b_trans=True, act=L.ACT_DSIGMOID, aux=X.float())
+        ref = (A @ S.t()) * X * (1 - X)
+        kid = 501
+    elif mode == "rank_bcast":
+        X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
+        dz = torch.randn(M, R, generator=g, dtype=torch.float64).to(cuda)
+        Wa = torch.randn(D, R, generator=g, dtype=torch.float64).to(cuda)
+        kw = dict(b_trans=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D, v_row_stride=0,
+                  act=L.ACT_DSIGMOID, aux=X.float())
+        ref = (A @ S.t() + dz @ Wa.t()) * X * (1 - X)
+    elif mode == "accumulate":
+        C0 = torch.randn(M, D, generator=g, dtype=torch.float64).to(cuda)
+        kw = dict(accumulate=True)
+        ref = C0 + A @ S
+    elif mode == "gatherA":
+        ai = torch.randint(0, M, (M,), generator=g).to(cuda)
+        kw = dict(a_idx=ai.int())
+        ref = A[ai] @ S
+    elif mode == "trans":
+        kw = dict(b_trans=True)
+        ref = A @ S.t()
+    else:
+        ref = A @ S
+    errs, outs = {}, {}
+    for gm in (L.GEMM_EXACT_F32, L.GEMM_BF16X3):
+        C = C0.float().clone() if C0 is not None else torch.full((M, D), 7.0, device=cuda)
+        ops.rowgemm(Af, Sf, C, precision=gm, **kw)
+        if gm == L.GEMM_BF16X3:
+            C2 = C0.float().clone() if C0 is not None else torch.empty(M, D, device=cuda)
+            ops.rowgemm(Af, Sf, C2, precision=gm, **kw)
+            assert torch.equal(C, C2)
+        outs[gm], errs[gm] = C, _maxrel(C, ref)
+    b3 = outs[L.GEMM_BF16X3]
+    if mode in B3_FALLBACK:
+        assert ops.rowgemm_kernel_id(Af, Sf, b3, precision="bf16x3", **kw) < 500
+        assert torch.equal(b3, outs[L.GEMM_EXACT_F32])
+        return
+    assert ops.rowgemm_kernel_id(Af, Sf, b3, precision="bf16x3", **kw) == kid
+    if mode == "zero_rows":
+        assert torch.equal(b3[::3], torch.zeros_like(b3[::3]))
+    if mode == "row_decades":
+        rel = ((b3.double() - ref).abs().amax(1) / ref.abs().amax(1)).max().item()
+        assert rel <= 1e-5, rel
+    assert errs[L.GEMM_BF16X3] <= max(1.25 * errs[L.GEMM_EXACT_F32], 1e-6), errs
+
+
+@pytest.mark.parametrize("M,kind", [(31, "plain"), (5003, "plain"), (300_017, "decades"), (70_001, "zero_blocks"),
+                                    (40_000, "growing"), (16, "plain"), (1, "plain")])
+def test_gemm_tn_bf16x3_vs_fp64(M, kind, cuda):
+    """bf16x3 TN GEMM (16-row tiles, transposed LDS reads of the three planes): error vs fp64 within 1.25x the
+    exact path's (floor 1e-6), rows spanning decades, zero stretches, growing magnitudes, ragged and one-row
+    M; deterministic run to run."""
+    g = torch.Generator().manual_seed(M + 3)
+    D = 256
+    A = torch.rand(M, D, generator=g, dtype=torch.float64)
+    B = torch.randn(M, D, generator=g, dtype=torch.float64) * 1e-12
+    if kind == "decades":
+        B = B * 10 ** (6 * torch.rand(M, 1, generator=g, dtype=torch.float64) - 3)
+    elif kind == "zero_blocks":
+        B[: M // 2] = 0
+        A[M // 3: M // 2] = 0
+    elif kind == "growing":
+        B = B * torch.logspace(-4, 4, M, dtype=torch.float64)[:, None]
+        A = A * torch.logspace(3, -3, M, dtype=torch.float64)[:, None]
+    A, B = A.to(cuda), B.to(cuda)
+    ref = A.t() @ B
+    slab = torch.empty(ops.tn_blocks(M, D) * D * D, device=cuda)
+    errs = {}
+    for gm in (L.GEMM_EXACT_F32, L.GEMM_BF16X3):
+        C = torch.empty(D, D, device=cuda)
+        ops.gemm_tn(A.float(), B.float(), C, slab, precision=gm)
+        errs[gm] = _maxrel(C, ref)
+        if gm == L.GEMM_BF16X3:
+            C2 = torch.empty(D, D, device=cuda)
+            ops.gemm_tn(A.float(), B.float(), C2, slab, precision=gm)
+            assert torch.equal(C, C2)
+    assert errs[L.GEMM_BF16X3] <= max(1.25 * errs[L.GEMM_EXACT_F32], 1e-6), errs
+
+
 def _tail_runs(lengths, M):
     """Sorted row indices built from consecutive runs of the given lengths (tail-sorted edges)."""
     idx = torch.repeat_interleave(torch.arange(len(lengths)), torch.as_tensor(lengths))[:M]

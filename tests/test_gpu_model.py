@@ -167,7 +167,8 @@ def test_synth_small_step_parity(golden, cuda):
             assert np.abs((out["params"][name] - params[name]) - (v - params[name])).max() <= 2e-5, name
 
 
-@pytest.mark.parametrize("D,R,gemm", [(256, 2, "split"), (256, 2, "exact"), (128, 3, "exact")])
+@pytest.mark.parametrize("D,R,gemm", [(256, 2, "split"), (256, 2, "exact"), (256, 2, "bf16x3"), (128, 3, "exact"),
+                                      (128, 3, "bf16x3")])
 def test_wide_step_parity_vs_oracle(D, R, gemm, cuda):
     """The headline width (D=256) on a mutation–drug graph, non-saturating init, vs float64 oracle,
     in both GEMM operand modes (same bars)."""
@@ -193,7 +194,7 @@ def test_wide_step_parity_vs_oracle(D, R, gemm, cuda):
     np.testing.assert_allclose(out["logits"], logits, rtol=0, atol=1e-4)
 
 
-@pytest.mark.parametrize("R,gemm", [(3, "split"), (4, "exact"), (8, "split"), (8, "exact")])
+@pytest.mark.parametrize("R,gemm", [(3, "split"), (4, "exact"), (8, "split"), (8, "exact"), (3, "bf16x3")])
 def test_many_relations_wide_step_vs_oracle(R, gemm, cuda):
     """D=256 with R > 2 relations (BASELINE config 5 has 8): the forward edge GEMM runs the capped-slab
     v3 kernel (asserted), the backward its broadcast-coefficient form, the node-level head chain the
@@ -233,7 +234,7 @@ def test_many_relations_wide_step_vs_oracle(R, gemm, cuda):
     assert kid == 300 + 10 * (4 if R <= 4 else 8) + 2 + (2000 if gemm == "split" else 0), kid
 
 
-@pytest.mark.parametrize("gemm", ["split", "exact"])
+@pytest.mark.parametrize("gemm", ["split", "exact", "bf16x3"])
 def test_reference_init_distribution_step_finite(gemm, cuda):
     """Reference-distribution init (E~U[0,1), K,S~N(0,1)) saturates the sigmoids exactly as
     TF does; the step must stay finite and match the oracle's loss."""
@@ -248,7 +249,7 @@ def test_reference_init_distribution_step_finite(gemm, cuda):
         assert np.all(np.isfinite(v))
 
 
-@pytest.mark.parametrize("gemm", ["split", "exact"])
+@pytest.mark.parametrize("gemm", ["split", "exact", "bf16x3"])
 def test_headline_width_saturating_step_vs_fp32_oracle(gemm, cuda):
     """D=256, E ~ U[0,1) as in the reference, S ~ N(0, 9/D) (layer pre-activations up to ~8, the
     sigmoids partly saturated), K ~ N(0, 1/(64 D)): fp32 itself deviates from fp64 here by ~3e-7 of
@@ -291,12 +292,13 @@ def test_split_and_exact_gemm_modes_agree_at_scale(cuda):
     N, R, D = 20000, 2, 256
     pos, neg = synthetic_graph(N, R, 20000, seed=4)
     params = init_params(N, R, D, seed=89)
-    a = run_step(params, pos, neg, N, R, D, cuda, gemm="split")
     b = run_step(params, pos, neg, N, R, D, cuda, gemm="exact")
-    assert abs(a["loss"] - b["loss"]) <= 1e-6 * abs(b["loss"])
-    np.testing.assert_allclose(a["scores"], b["scores"], rtol=0, atol=1e-5)
-    for k in a["grads"]:
-        assert np.all(np.isfinite(a["grads"][k])), k
+    for mode in ("split", "bf16x3"):
+        a = run_step(params, pos, neg, N, R, D, cuda, gemm=mode)
+        assert abs(a["loss"] - b["loss"]) <= 1e-6 * abs(b["loss"]), mode
+        np.testing.assert_allclose(a["scores"], b["scores"], rtol=0, atol=1e-5)
+        for k in a["grads"]:
+            assert np.all(np.isfinite(a["grads"][k])), (mode, k)
 
 
 def test_bitwise_determinism(golden, cuda):

@@ -38,7 +38,7 @@ def _mild(N, R, D, seed):
     return {k: v.astype(np.float32) for k, v in p.items()}
 
 
-@pytest.mark.parametrize("D,gemm", [(64, "split"), (256, "split"), (256, "exact")])
+@pytest.mark.parametrize("D,gemm", [(64, "split"), (256, "split"), (256, "exact"), (256, "bf16x3")])
 def test_two_shards_sum_to_full_batch(D, gemm, cuda):
     N, R = 3000, 2
     pos, neg = synthetic_graph(N, R, 12000, seed=21)

@@ -36,7 +36,7 @@ def test_two_engines_two_modes_two_streams_bitwise(cuda):
     tri = np.concatenate([pos, neg])
     lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
     jobs = {}
-    for mode in ("exact", "split"):
+    for mode in ("exact", "split", "bf16x3"):
         eng = Engine(N, R, D, cuda, gemm=mode)
         P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
         P.load(_params(N, R, D, 3))
@@ -53,6 +53,7 @@ def test_two_engines_two_modes_two_streams_bitwise(cuda):
     torch.cuda.synchronize()
     # the two modes really differ (otherwise the test below would prove nothing)
     assert not torch.equal(alone["exact"][3], alone["split"][3])
+    assert not torch.equal(alone["exact"][3], alone["bf16x3"][3])
 
     results, errors = {}, []
 

@@ -1,12 +1,13 @@
 """Time and check the edge-level GEMM kernels alone at config-3 shape (T = 4M rows, D = 256, R = 2),
-in both operand-precision modes (exact f32 MFMA, split-fp16 MFMA).
+in the operand-precision modes (exact f32 MFMA, split-fp16 MFMA, bf16x3 MFMA).
 
 For each case it prints the time per launch, the algorithmic TFLOP/s, and the max error of each
 mode against an fp64 torch reference on the first `check` rows (absolute, over max |ref|).
 
-usage: python tools/bench_gemm.py [T] [modes=exact,split] [lib.so ...]
+usage: python tools/bench_gemm.py [T] [modes=exact,split,bf16x3] [lib.so ...]
   (each library is loaded in turn on the same inputs: build-flag variants of the same source)
 """
+import os
 import sys
 
 import torch
@@ -30,9 +31,11 @@ def run1(T, N, D, R, reps, check, modes):
     A = torch.rand(T, D, device=dev, generator=g)
     S = torch.randn(D, D, device=dev, generator=g)
     W = torch.rand(N, R, device=dev, generator=g)
+    h_ = torch.randint(0, N, (T,), device=dev, generator=g)
+    Wedge = W[h_].contiguous()             # per-edge coefficients, as the engine passes them
     P = torch.randn(R, N, D, device=dev, generator=g) * 4
     t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
-    h = torch.randint(0, N, (T,), device=dev, generator=g).int()
+    h = h_.int()
     aux = torch.rand(T, D, device=dev, generator=g)
     # gradient-like rows: tiny, spanning 6 decades from row to row (exercises the running scales)
     dO = torch.randn(T, D, device=dev, generator=g) * 1e-12 * 10 ** (6 * torch.rand(T, 1, device=dev, generator=g) - 3)
@@ -48,17 +51,18 @@ def run1(T, N, D, R, reps, check, modes):
         "plain": Ad @ Sd,
     }
     tn_ref = A.double().t() @ dO.double()
-    for mname in ("exact", "split"):
-        if mname not in modes:
-            continue
+    for mname in modes:
         cases = {
-            "fwd_combine": lambda: ops.rowgemm(A, S, C, coef=W, coef_idx=h, V=P, v_idx=t, v_rel_stride=N * D,
+            "fwd_combine": lambda: ops.rowgemm(A, S, C, coef=Wedge, V=P, v_idx=t, v_rel_stride=N * D,
                                                act=L.ACT_SIGMOID, precision=mname),
             "bwd_dsig": lambda: ops.rowgemm(dO, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux, precision=mname),
             "plain": lambda: ops.rowgemm(A, S, C, precision=mname),
             "tn": lambda: ops.gemm_tn(A, dO, dS, slab, precision=mname),
         }
+        only = os.environ.get("IDDGCN_GEMM_CASES")
         for name, fn in cases.items():
+            if only and name not in only.split(","):
+                continue
             fn()
             torch.cuda.synchronize()
             err = ""
