@@ -3233,8 +3233,11 @@ int check_rowgemm(const iddgcn_rowgemm_t& a) {
 
 // The bf16x3 row GEMM's forms (rowgemm256_b3_kernel<NV, AUX>): plain, sigma' backward (AUX), gathered-combine
 // forward with exactly R = NV in {1, 2} per-edge coefficients; no a_idx, accumulate, coef_idx or planes.
+#ifndef B3_DISABLE
+#define B3_DISABLE 0     // experiment builds only: 1 no bf16x3 row GEMM (exact instead), 2 no bf16x3 TN
+#endif
 bool b3_select(const RowGemmP& p, int& nv, bool& aux) {
-    if (p.precision != IDDGCN_GEMM_BF16X3 || p.a_idx || p.accumulate || p.planes) return false;
+    if ((B3_DISABLE & 1) || p.precision != IDDGCN_GEMM_BF16X3 || p.a_idx || p.accumulate || p.planes) return false;
     if (p.R > 0) {
         if (p.R > 2 || p.v_row_stride != 256 || p.coef_idx || p.act == IDDGCN_ACT_DSIGMOID) return false;
         nv = p.R;
@@ -3545,7 +3548,7 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
-    if (d == 256 && precision == IDDGCN_GEMM_BF16X3) {
+    if (d == 256 && precision == IDDGCN_GEMM_BF16X3 && !(B3_DISABLE & 2)) {
         hipLaunchKernelGGL(gemm_tn256_b3_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
     } else if (d == 256 && precision == IDDGCN_GEMM_SPLIT_F16) {
         hipLaunchKernelGGL(gemm_tn256_x3_kernel<>, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab, TnBatch{});
