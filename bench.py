@@ -377,9 +377,10 @@ def main():
                          "row-partitioned SpMMs (A_r E all-gathered, dAE reduce-scattered; node GEMMs replicated)")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],
                     help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
-    ap.add_argument("--gemm", default="exact", choices=["exact", "bf16x3", "split"],
-                    help="operand precision of the D=256 MFMA GEMMs: exact f32 (the reference's arithmetic, the "
-                         "headline) or the opt-in split-fp16 operands (timed too, under other_gemm_mode)")
+    ap.add_argument("--gemm", default="bf16x3", choices=["exact", "bf16x3", "split"],
+                    help="operand precision of the D=256 MFMA GEMMs: bf16x3 (the headline: fp32 operands split "
+                         "exactly into three bf16 pieces, fp32 products and sums on bf16 MFMAs), exact (f32 MFMA, "
+                         "bitwise an fmaf chain; timed too, under other_gemm_mode) or the opt-in split-fp16 operands")
     ap.add_argument("--no-other-mode", action="store_true", help="skip timing the other GEMM mode")
     ap.add_argument("--overlap", action="store_true",
                     help="backward: layer-2/3 tail reductions on a side stream beside the dS TN (A/B)")
