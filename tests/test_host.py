@@ -1,4 +1,5 @@
 """Host logic of the product path (no GPU): graph build, layouts, C-ABI exports."""
+import ctypes
 import os
 import re
 
@@ -218,3 +219,33 @@ def test_rowgemm_precision_is_a_per_call_argument():
     args.precision = _lib.GEMM_SPLIT_F16
     assert lib.iddgcn_rowgemm_f32(None, args) == 0          # M = 0: valid, nothing to do
     assert lib.iddgcn_gemm_tn_f32(None, 32, 256, None, None, None, 1, None, 0, 0) == -3
+
+
+def test_bf16x3_kernel_selection_is_pure_host():
+    """ABI 7: which D = 256 kernel a bf16x3 row GEMM takes (iddgcn_rowgemm_kernel_id, nothing launched, no GPU):
+    the column-half bf16x3 kernel (500 + 10 NV + aux) for the plain form, the sigma' backward and the gathered
+    forward with R = NV <= 2 per-edge coefficients; the exact kernel's id for every form it does not take
+    (gathered A, accumulate, broadcast V, coef_idx, R > 2, D < 256)."""
+    lib = _lib.lib()
+    fake = ctypes.c_void_p(16)          # never dereferenced: kernel_id inspects the arguments only
+
+    def kid(**kw):
+        a = _lib.RowGemmArgs(M=1000, D=kw.pop("D", 256), A=fake, B=fake, C=fake, precision=_lib.GEMM_BF16X3)
+        for k, v in kw.items():
+            setattr(a, k, v)
+        return lib.iddgcn_rowgemm_kernel_id(ctypes.byref(a))
+
+    assert kid() == 500
+    assert kid(act=_lib.ACT_DSIGMOID, aux=fake, b_trans=1) == 501
+    for R in (1, 2):
+        assert kid(R=R, coef=fake, V=fake, v_idx=fake, v_rel_stride=256 * 10, v_row_stride=256,
+                   act=_lib.ACT_SIGMOID) == 500 + 10 * R
+    exact = lambda **kw: kid(precision=_lib.GEMM_EXACT_F32, **kw)  # noqa: E731
+    for kw in (dict(accumulate=1), dict(a_idx=fake),
+               dict(R=2, coef=fake, V=fake, v_rel_stride=256, v_row_stride=0, act=_lib.ACT_DSIGMOID, aux=fake),
+               dict(R=2, coef=fake, coef_idx=fake, V=fake, v_idx=fake, v_rel_stride=2560, v_row_stride=256),
+               dict(R=3, coef=fake, V=fake, v_idx=fake, v_rel_stride=2560, v_row_stride=256),
+               dict(D=64)):
+        assert kid(**kw) == exact(**kw) < 500, kw
+    # the TN entry accepts the mode (invalid arguments still refused before any launch)
+    assert lib.iddgcn_gemm_tn_f32(None, 32, 256, None, None, None, 1, None, 0, _lib.GEMM_BF16X3) == -3
