@@ -141,6 +141,18 @@ __device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+// experiment builds (DP_SC1): 16-B vector store with sc1 (the line leaves the XCD's L2) / a load with sc1
+#ifndef DP_SC1
+#define DP_SC1 0
+#endif
+__device__ __forceinline__ void st4_dp(float* p, f32x4 v) {
+    if constexpr (DP_SC1 & 1) {
+        typedef __attribute__((address_space(1))) float* gfp;
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"((gfp)p), "v"(v) : "memory");
+    } else {
+        st4(p, v);
+    }
+}
 // bf16 edge tables (the bf16-feature mode): 4 values = 8 bytes, round-to-nearest-even on store
 __device__ __forceinline__ f32x4 bf4_to_f32(bf16x4 v) {
     return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
@@ -2961,8 +2973,9 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     }
     if (!live || slot != 0) return;
 #pragma unroll
-    for (int r = 0; r < R; ++r) st4(dP + r * dp_rel_stride + n * D + sub * 4, acc[r]);
-    if (dsum) st4(dsum + n * D + sub * 4, s4);
+    for (int r = 0; r < R; ++r) st4_dp(dP + r * dp_rel_stride + n * D + sub * 4, acc[r]);
+    if (dsum) st4_dp(dsum + n * D + sub * 4, s4);
+    if (DP_SC1 & 2) __threadfence();
 }
 
 // ---------------------------------------------------------------------------
@@ -2986,7 +2999,7 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
     if (live) d = ld4(dO + n * D + sub * 4);
     if (live && dsum) {
         float* sp = dsum + n * D + sub * 4;
-        st4(sp, ld4(sp) + d);
+        st4_dp(sp, ld4(sp) + d);
     }
     const int beg = (live && hseg_ptr) ? hseg_ptr[n] : 0;
     const int end = (live && hseg_ptr) ? hseg_ptr[n + 1] : 0;
@@ -3034,8 +3047,9 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
     for (int r = 0; r < MAX_R; ++r)
         if (r < R) {
             float* pp = dP + r * dp_rel_stride + n * D + sub * 4;
-            st4(pp, ld4(pp) + w[r] * d);
+            st4_dp(pp, ld4(pp) + w[r] * d);
         }
+    if (DP_SC1 & 2) __threadfence();
 }
 
 // dst[e][j] = src[idx[e]][j] for a narrow row width (per-edge copies of node tables)

@@ -8,7 +8,8 @@ mkdir -p var_so
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
-  ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -I include $flags \
+  ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Xclang -target-feature -Xclang -packed-fp32-ops \
+      -c -I include $flags \
       iddgcn_amd/csrc/iddgcn_hip.hip -o var_so/$name.o && \
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC var_so/$name.o build/graph_build.hip.o \
       build/similarity.hip.o build/sampling.hip.o -o var_so/$name.so && rm var_so/$name.o && echo "built $name" ) &

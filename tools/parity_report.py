@@ -86,7 +86,7 @@ def main():
             dr = np.abs(r32 - ref).max()
             out["fold0_layers_first256"][f"layer{l}_{side}"] = rec(np.abs(ours.cpu().numpy() - ref).max(), dr,
                                                                    max(1e-4, 2 * dr))
-    # config 3 at full size, 10k-edge sample, both GEMM modes, mild and reference init
+    # config 3 at full size, 10k-edge sample, every GEMM mode, mild and reference init
     N, R, M, D = 100_000, 2, 2_000_000, 256
     pos, neg = synthetic_graph(N, R, M, seed=0)
     tri = np.concatenate([pos, neg])
@@ -103,7 +103,7 @@ def main():
         p32, s32, l32 = forward_detail(params, tri[sample], coo, N, dtype=torch.float32)
         P = FlatParams(N, R, D, dev)
         P.load(params)
-        for gemm in ("split", "exact"):
+        for gemm in ("split", "exact", "bf16x3"):
             eng.gemm = gemm
             p, s = eng.predict(P, adj, ed, logits=True)
             lay = eng.layer_outputs(ed, rows=sample)
