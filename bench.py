@@ -119,7 +119,7 @@ def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4):
         out = {"kernel": name, "bound": "mfma", "achieved": hw_flops / s / 1e12, "peak": peak_f,
                "unit": "TFLOP/s"}
     out["frac"] = out["achieved"] / out["peak"]
-    out.update({"avg_launch_ms": avg_ms, "bytes_per_launch": nbytes, "flops_per_launch": flops,
+    out.update({"avg_launch_ms": avg_ms, "bytes_per_launch": nbytes, "flops_per_launch": flops, "hw_flops_per_launch": hw_flops,
                 "mfma_frac": hw_flops / s / 1e12 / peak_f, "hbm_frac": nbytes / s / 1e9 / HBM_PEAK_GBS})
     return out
 

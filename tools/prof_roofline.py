@@ -35,7 +35,11 @@ def main(trace, bench, name="rowgemm256_v3_kernel<2, false, true, false, false, 
         print(f"rocprof GB/s      : {rl['bytes_per_launch'] / avg / 1e6:.1f}  vs bench {rl['achieved']:.1f} "
               f"(algorithmic {rl['bytes_per_launch'] / 1e9:.3f} GB per launch)")
     else:
-        print(f"rocprof TFLOP/s   : {rl['flops_per_launch'] / avg / 1e9:.1f}  vs bench {rl['achieved']:.1f}")
+        # achieved is priced on the MFMA work the operand mode issues (bf16x3: 6 products per
+        # algorithmic multiply-add); older bench lines carry only the algorithmic count.
+        hw = rl.get("hw_flops_per_launch") or rl["achieved"] * 1e9 * rl["avg_launch_ms"]
+        print(f"rocprof TFLOP/s   : {hw / avg / 1e9:.1f}  vs bench {rl['achieved']:.1f} "
+              f"(hw {hw / 1e12:.3f} TFLOP, algorithmic {rl['flops_per_launch'] / 1e12:.3f} TFLOP per launch)")
 
 
 if __name__ == "__main__":
