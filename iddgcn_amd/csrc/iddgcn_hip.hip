@@ -2833,7 +2833,12 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
 #ifndef TS_U
 #define TS_U 4
 #endif
-    constexpr int U = TS_U;
+#ifndef TS_UW
+#define TS_UW TS_U
+#endif
+#ifndef TS_NT
+#define TS_NT 0        // experiment builds: nontemporal edge-row loads
+#endif
     const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64;
     const int sub = threadIdx.x % LPR;
     const int slot = (threadIdx.x % 64) / LPR;
@@ -2845,6 +2850,7 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
 #define TS_PF_MINR 4
 #endif
     constexpr bool SCALAR = SLOTS == 1 && R >= TS_PF_MINR;
+    constexpr int U = SCALAR ? TS_UW : TS_U;         // edge rows per group
     if constexpr (SCALAR) {
         beg = __builtin_amdgcn_readfirstlane(beg);
         end = __builtin_amdgcn_readfirstlane(end);
@@ -2866,7 +2872,11 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             // h_idx == NULL: W is already per edge (W[e][r], gathered once per layer)
             hh[u] = a ? (h_idx ? h_idx[beg + k + u] : beg + k + u) : 0;
             if constexpr (SCALAR) hh[u] = __builtin_amdgcn_readfirstlane(hh[u]);     // scalar W loads
-            d[u] = a ? ld4e<BF>(dO, (long long)(beg + k + u) * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (TS_NT && !BF)     // experiment builds: nontemporal row loads
+                d[u] = a ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(dO + (long long)(beg + k + u) * D + sub * 4))
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+            else
+                d[u] = a ? ld4e<BF>(dO, (long long)(beg + k + u) * D + sub * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -2929,8 +2939,12 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             for (int uu = 0; uu < U; ++uu) {
                 const RawT* src = reinterpret_cast<const RawT*>(reinterpret_cast<const char*>(dO) +
                                                                ((long long)(beg + k + uu) * D + sub * 4) * (BF ? 2 : 4));
-                if (k + uu < len) dn[uu] = *src;
-                else dn[uu] = RawT{};
+                if (k + uu < len) {
+                    if constexpr (TS_NT) dn[uu] = __builtin_nontemporal_load(src);
+                    else dn[uu] = *src;
+                } else {
+                    dn[uu] = RawT{};
+                }
             }
         };
         if (len > 0) load_raw(0);
