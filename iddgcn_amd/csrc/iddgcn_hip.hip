@@ -141,18 +141,6 @@ __device__ __forceinline__ float multi_reduce(float (&v)[K], int sub) {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
-// experiment builds (DP_SC1): 16-B vector store with sc1 (the line leaves the XCD's L2) / a load with sc1
-#ifndef DP_SC1
-#define DP_SC1 0
-#endif
-__device__ __forceinline__ void st4_dp(float* p, f32x4 v) {
-    if constexpr (DP_SC1 & 1) {
-        typedef __attribute__((address_space(1))) float* gfp;
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"((gfp)p), "v"(v) : "memory");
-    } else {
-        st4(p, v);
-    }
-}
 // bf16 edge tables (the bf16-feature mode): 4 values = 8 bytes, round-to-nearest-even on store
 __device__ __forceinline__ f32x4 bf4_to_f32(bf16x4 v) {
     return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
@@ -1671,14 +1659,44 @@ __device__ __forceinline__ void split3(float x, __bf16& b0, __bf16& b1, __bf16& 
     b1 = (__bf16)r1;
     b2 = (__bf16)(r1 - (float)b1);
 }
+// Two values at a time: one v_cvt_pk_bf16_f32 rounds both, the pair's dword is unpacked back to fp32 by a
+// shift (low) and a mask (high), then the two exact subtractions; 5.5 VALU per value instead of the 7.5 of
+// per-value conversions followed by a packing conversion.  Same values as split3 (RNE both ways).
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
+}
+__device__ __forceinline__ void split3x2(float x0, float x1, unsigned& p0, unsigned& p1, unsigned& p2) {
+    p0 = cvt_pk_bf16(x0, x1);
+    const float r0 = x0 - __builtin_bit_cast(float, p0 << 16);
+    const float r1 = x1 - __builtin_bit_cast(float, p0 & 0xffff0000u);
+    p1 = cvt_pk_bf16(r0, r1);
+    const float s0 = r0 - __builtin_bit_cast(float, p1 << 16);
+    const float s1 = r1 - __builtin_bit_cast(float, p1 & 0xffff0000u);
+    p2 = cvt_pk_bf16(s0, s1);
+}
 __device__ __forceinline__ void split3x4(const f32x4& v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+#ifndef B3_PAIRSPLIT
+#define B3_PAIRSPLIT 1
+#endif
+    if constexpr (B3_PAIRSPLIT) {
+        unsigned a0, b0, c0, a1, b1, c1;
+        split3x2(v[0], v[1], a0, b0, c0);
+        split3x2(v[2], v[3], a1, b1, c1);
+        const u32x2 a = {a0, a1}, b = {b0, b1}, c = {c0, c1};
+        p0 = __builtin_bit_cast(bf16x4, a);
+        p1 = __builtin_bit_cast(bf16x4, b);
+        p2 = __builtin_bit_cast(bf16x4, c);
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        __bf16 a, b, c;
-        split3(v[q], a, b, c);
-        p0[q] = a;
-        p1[q] = b;
-        p2[q] = c;
+        for (int q = 0; q < 4; ++q) {
+            __bf16 a, b, c;
+            split3(v[q], a, b, c);
+            p0[q] = a;
+            p1[q] = b;
+            p2[q] = c;
+        }
     }
 }
 // a staged fp32 row of 256 values (bytes [0, 1024) of `row`) -> its three bf16 planes in place: plane j at
@@ -2598,7 +2616,14 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                                                              float* __restrict__ loss_slab) {
     constexpr int LPR = D / 4;
     constexpr int GROUPS = 256 / LPR;
-    constexpr int U = 4;
+#ifndef DM_UW
+#define DM_UW 4
+#endif
+#ifndef DM_SC_MINR
+#define DM_SC_MINR 4
+#endif
+    // edges per group; the R >= DM_SC_MINR loop (one head per wave, next group prefetched) takes DM_UW
+    constexpr int U = (64 / LPR == 1 && RT >= DM_SC_MINR) ? DM_UW : 4;
     __shared__ __attribute__((aligned(16))) float red[GROUPS * RT * D];
     __shared__ float lred[GROUPS];
     constexpr int SLOTS = 64 / LPR;      // edge slots per head node (one wave per node)
@@ -2617,7 +2642,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
         int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
         // D = 256 with many relations: the whole wave is one head, so its edges' indices are wave-uniform
         // and go through scalar loads (R = 8: -13%; at R <= 2 the vector loads are faster, +25% otherwise)
-        constexpr bool SCALAR = SLOTS == 1 && RT >= 4;
+        constexpr bool SCALAR = SLOTS == 1 && RT >= DM_SC_MINR;
         if constexpr (SCALAR) {
             beg = __builtin_amdgcn_readfirstlane(beg);
             end = __builtin_amdgcn_readfirstlane(end);
@@ -2833,11 +2858,16 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
 #ifndef TS_U
 #define TS_U 4
 #endif
+// R >= 4 (one node per wave, next group prefetched): 8 edge rows per group, i.e. U x R = 64 coefficients, one
+// per lane.  Rows in flight per wave are what this loop is bound by: at the config-5 shape (R = 8, bf16 rows,
+// degree 50) 4 -> 8 rows per group took a launch from 4.86 to 3.03 ms (tools/bench_tailseg.py)
 #ifndef TS_UW
-#define TS_UW TS_U
+#define TS_UW 8
 #endif
+// fp32 rows at R <= 2: nontemporal loads (the rows are read once; -2% at config 3, the probe's read-only
+// streams gain 10% from it); the R >= 4 loop with 8 rows in flight is slower with them (3.41 vs 3.03 ms)
 #ifndef TS_NT
-#define TS_NT 0        // experiment builds: nontemporal edge-row loads
+#define TS_NT 1
 #endif
     const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64;
     const int sub = threadIdx.x % LPR;
@@ -2872,7 +2902,7 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             // h_idx == NULL: W is already per edge (W[e][r], gathered once per layer)
             hh[u] = a ? (h_idx ? h_idx[beg + k + u] : beg + k + u) : 0;
             if constexpr (SCALAR) hh[u] = __builtin_amdgcn_readfirstlane(hh[u]);     // scalar W loads
-            if constexpr (TS_NT && !BF)     // experiment builds: nontemporal row loads
+            if constexpr (TS_NT && !BF)
                 d[u] = a ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(dO + (long long)(beg + k + u) * D + sub * 4))
                          : f32x4{0.f, 0.f, 0.f, 0.f};
             else
@@ -2939,12 +2969,8 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             for (int uu = 0; uu < U; ++uu) {
                 const RawT* src = reinterpret_cast<const RawT*>(reinterpret_cast<const char*>(dO) +
                                                                ((long long)(beg + k + uu) * D + sub * 4) * (BF ? 2 : 4));
-                if (k + uu < len) {
-                    if constexpr (TS_NT) dn[uu] = __builtin_nontemporal_load(src);
-                    else dn[uu] = *src;
-                } else {
-                    dn[uu] = RawT{};
-                }
+                if (k + uu < len) dn[uu] = *src;
+                else dn[uu] = RawT{};
             }
         };
         if (len > 0) load_raw(0);
@@ -2987,9 +3013,8 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     }
     if (!live || slot != 0) return;
 #pragma unroll
-    for (int r = 0; r < R; ++r) st4_dp(dP + r * dp_rel_stride + n * D + sub * 4, acc[r]);
-    if (dsum) st4_dp(dsum + n * D + sub * 4, s4);
-    if (DP_SC1 & 2) __threadfence();
+    for (int r = 0; r < R; ++r) st4(dP + r * dp_rel_stride + n * D + sub * 4, acc[r]);
+    if (dsum) st4(dsum + n * D + sub * 4, s4);
 }
 
 // ---------------------------------------------------------------------------
@@ -3013,7 +3038,7 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
     if (live) d = ld4(dO + n * D + sub * 4);
     if (live && dsum) {
         float* sp = dsum + n * D + sub * 4;
-        st4_dp(sp, ld4(sp) + d);
+        st4(sp, ld4(sp) + d);
     }
     const int beg = (live && hseg_ptr) ? hseg_ptr[n] : 0;
     const int end = (live && hseg_ptr) ? hseg_ptr[n + 1] : 0;
@@ -3061,9 +3086,8 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
     for (int r = 0; r < MAX_R; ++r)
         if (r < R) {
             float* pp = dP + r * dp_rel_stride + n * D + sub * 4;
-            st4_dp(pp, ld4(pp) + w[r] * d);
+            st4(pp, ld4(pp) + w[r] * d);
         }
-    if (DP_SC1 & 2) __threadfence();
 }
 
 // dst[e][j] = src[idx[e]][j] for a narrow row width (per-edge copies of node tables)

@@ -36,7 +36,49 @@ def run(x):
     ops.tail_seg_reduce(x["tptr"], None, x["W"], x["dO"], x["P"], x["dP"], x["dW"], dsum=x["dsum"])
 
 
+def dm_case(T, N, R, D, bf16, seed=0):
+    """DistMult + BCE + both seeds by head segment (distmult_heads_kernel)."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    h = torch.randint(0, N, (T,), device=dev, generator=g)
+    hperm = torch.argsort(h, stable=True)
+    x = {"hptr": torch.searchsorted(h[hperm], torch.arange(N + 1, device=dev), right=False).int(),
+         "hperm": hperm.int(), "Xh": torch.rand(N, D, device=dev, generator=g),
+         "Xt": torch.rand(T, D, device=dev, generator=g), "r": torch.randint(0, R, (T,), device=dev, generator=g).int(),
+         "rel": torch.rand(R, D, device=dev, generator=g), "y": (torch.rand(T, device=dev, generator=g) > 0.5).float(),
+         "dXh": torch.empty(N, D, device=dev)}
+    if bf16:
+        x["Xt"] = x["Xt"].to(torch.bfloat16)
+    x["do"] = torch.empty_like(x["Xt"])
+    nb = ops.distmult_blocks(T)
+    x["drel"], x["loss"] = torch.empty(nb * R * D, device=dev), torch.empty(nb, device=dev)
+    x["bytes"] = 2 * T * D * (2 if bf16 else 4) + 2 * N * D * 4
+    return x
+
+
+def dm_run(x):
+    ops.distmult_bce_heads(x["hptr"], x["hperm"], x["Xh"], x["Xt"], x["r"], x["rel"], x["y"], x["do"], x["dXh"],
+                           x["drel"], x["loss"], scale=1e-5)
+
+
+def sweep(name, x, fn, outs):
+    ref = None
+    for p in sys.argv[1:]:
+        L._lib = load_lenient(p)
+        ms = timeit(lambda: fn(x))
+        out = [o.clone() for o in outs(x)]
+        same = "ref" if ref is None else ("bitwise" if all(torch.equal(a, b) for a, b in zip(out, ref)) else "DIFFERS")
+        ref = ref or out
+        print(f"{name:18s} {p.split('/')[-1]:14s} {ms:7.3f} ms  {x['bytes'] / ms / 1e9:5.2f} TB/s  {same}", flush=True)
+
+
 if __name__ == "__main__":
+    for name, shp in {"dm_cfg3_R2_f32": (4_000_000, 100_000, 2, 256, False),
+                      "dm_cfg5_R8_bf16": (20_000_000, 400_000, 8, 256, True)}.items():
+        x = dm_case(*shp)
+        sweep(name, x, dm_run, lambda x: [x["do"], x["dXh"], x["drel"], x["loss"]])
+        del x
+        torch.cuda.empty_cache()
     shapes = {"cfg3_R2_f32": (4_000_000, 100_000, 2, 256, False, False),
               "cfg3_R2_f32_dsum": (4_000_000, 100_000, 2, 256, False, True),
               "cfg5_R8_bf16": (20_000_000, 400_000, 8, 256, True, False)}
