@@ -2620,7 +2620,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
 #define DM_UW 4
 #endif
 #ifndef DM_SC_MINR
-#define DM_SC_MINR 4
+#define DM_SC_MINR 2      // R = 2 too: 1.96 -> 1.84 ms at config 3 (tools/bench_tailseg.py), bitwise equal
 #endif
     // edges per group; the R >= DM_SC_MINR loop (one head per wave, next group prefetched) takes DM_UW
     constexpr int U = (64 / LPR == 1 && RT >= DM_SC_MINR) ? DM_UW : 4;
@@ -2640,8 +2640,8 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
         const long long n = n0 + threadIdx.x / 64;
         const bool live = n < n_nodes;
         int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
-        // D = 256 with many relations: the whole wave is one head, so its edges' indices are wave-uniform
-        // and go through scalar loads (R = 8: -13%; at R <= 2 the vector loads are faster, +25% otherwise)
+        // D = 256 and R >= 2: the whole wave is one head, so its edges' indices are wave-uniform and the
+        // software-pipelined loop below applies (R = 8: -13%, R = 2: -6%)
         constexpr bool SCALAR = SLOTS == 1 && RT >= DM_SC_MINR;
         if constexpr (SCALAR) {
             beg = __builtin_amdgcn_readfirstlane(beg);
@@ -2915,10 +2915,17 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     };
     auto group = [&](int k, const f32x4 (&d)[U], const float (&w)[U][R]) __attribute__((always_inline)) {
         constexpr int KV = U * R;
-        constexpr int KP = KV <= 4 ? 4 : KV <= 8 ? 8 : KV <= 16 ? 16 : 32;   // padded to a power of two
-        float dw[KP];
+        // reduced in chunks of at most 32 values (a power of two): 64-value butterflies (U x R = 64) gave
+        // run-to-run different dWedge at the config-5 shape; with 32-value chunks an 8-row group reduces
+        // exactly as two 4-row groups did
+#ifndef TS_KMAX
+#define TS_KMAX 32     // experiment builds: 64 restores the single 64-value butterfly
+#endif
+        constexpr int KP = KV <= 4 ? 4 : KV <= 8 ? 8 : KV <= 16 ? 16 : (KV <= 32 || TS_KMAX == 32) ? 32 : 64;
+        constexpr int NCH = (KV + KP - 1) / KP;
+        float dw[NCH * KP];
 #pragma unroll
-        for (int j = 0; j < KP; ++j) dw[j] = 0.f;
+        for (int j = 0; j < NCH * KP; ++j) dw[j] = 0.f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             s4 += d[u];
@@ -2930,12 +2937,18 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             }
         }
         if constexpr (KP <= LPR) {
-            const float tot = multi_reduce<LPR, KP>(dw, sub);
-            constexpr int SPAN = LPR / KP;                 // lanes sharing one value
-            const int j = sub / SPAN;
-            if (sub % SPAN == 0 && j < KV) {
-                const int u = j / R, r = j % R;
-                if (k + u < len) dWedge[(long long)(beg + k + u) * R + r] = tot;
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) {
+                float part[KP];
+#pragma unroll
+                for (int j = 0; j < KP; ++j) part[j] = dw[ch * KP + j];
+                const float tot = multi_reduce<LPR, KP>(part, sub);
+                constexpr int SPAN = LPR / KP;             // lanes sharing one value
+                const int j = ch * KP + sub / SPAN;
+                if (sub % SPAN == 0 && j < KV) {
+                    const int u = j / R, r = j % R;
+                    if (k + u < len) dWedge[(long long)(beg + k + u) * R + r] = tot;
+                }
             }
         } else {
 #pragma unroll
