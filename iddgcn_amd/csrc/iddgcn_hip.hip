@@ -1723,7 +1723,7 @@ __device__ __forceinline__ void row_to_planes3(char* row, int lane) {
 //     8 banks mod 64, makes every 16-lane group of the read conflict-free).
 //   * accumulators: a0 w0 in one, the five smaller products in a second (fp32), summed at the end.
 //   * epilogue as the v3 kernel: gathered P_r[t] rows (the tile's distinct tails), per-edge coefficients
-//     and sigma' rows DMA'd into wave-private slabs ([32][16] fp32, XOR-swizzled 16-B groups); waves 4-7 run
+//     and sigma' rows (or, accumulating, the old C rows) DMA'd into wave-private slabs ([32][16] fp32, XOR-swizzled 16-B groups); waves 4-7 run
 //     the epilogue of tile t-1 while waves 0-3 run tile t's MFMAs on the same SIMDs; one barrier per tile.
 #ifndef B3_ABL
 #define B3_ABL 0     // experiment builds only: 1 skip the MFMAs, 2 skip the A DMA, 4 skip the conversion, 8 skip stores
@@ -1900,7 +1900,9 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf, s[q], v[q]);
                 }
             }
-            if (p.act == IDDGCN_ACT_SIGMOID) {
+            if (AUX && p.accumulate) {
+                v += ld4(slabw + NV * SLAB + slab16_off(row, g));
+            } else if (p.act == IDDGCN_ACT_SIGMOID) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
             } else if (AUX && p.act == IDDGCN_ACT_DSIGMOID) {
@@ -2915,13 +2917,9 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     };
     auto group = [&](int k, const f32x4 (&d)[U], const float (&w)[U][R]) __attribute__((always_inline)) {
         constexpr int KV = U * R;
-        // reduced in chunks of at most 32 values (a power of two): 64-value butterflies (U x R = 64) gave
-        // run-to-run different dWedge at the config-5 shape; with 32-value chunks an 8-row group reduces
-        // exactly as two 4-row groups did
-#ifndef TS_KMAX
-#define TS_KMAX 32     // experiment builds: 64 restores the single 64-value butterfly
-#endif
-        constexpr int KP = KV <= 4 ? 4 : KV <= 8 ? 8 : KV <= 16 ? 16 : (KV <= 32 || TS_KMAX == 32) ? 32 : 64;
+        // reduced in chunks of at most 32 values (a power of two); every value is summed over the 64 lanes in
+        // the same butterfly order whatever the chunk size, so an 8-row group gives bitwise the 4-row sums
+        constexpr int KP = KV <= 4 ? 4 : KV <= 8 ? 8 : KV <= 16 ? 16 : 32;
         constexpr int NCH = (KV + KP - 1) / KP;
         float dw[NCH * KP];
 #pragma unroll
@@ -3302,15 +3300,17 @@ int check_rowgemm(const iddgcn_rowgemm_t& a) {
 #define B3_DISABLE 0     // experiment builds only: 1 no bf16x3 row GEMM (exact instead), 2 no bf16x3 TN
 #endif
 bool b3_select(const RowGemmP& p, int& nv, bool& aux) {
-    if ((B3_DISABLE & 1) || p.precision != IDDGCN_GEMM_BF16X3 || p.a_idx || p.accumulate || p.planes) return false;
+    if ((B3_DISABLE & 1) || p.precision != IDDGCN_GEMM_BF16X3 || p.a_idx || p.planes) return false;
     if (p.R > 0) {
-        if (p.R > 2 || p.v_row_stride != 256 || p.coef_idx || p.act == IDDGCN_ACT_DSIGMOID) return false;
+        if (p.R > 2 || p.v_row_stride != 256 || p.coef_idx || p.act == IDDGCN_ACT_DSIGMOID || p.accumulate) return false;
         nv = p.R;
         aux = false;
         return true;
     }
+    // C += A B (act none): the sigma' kernel's aux slab carries the old C rows (read before the tile is stored)
+    if (p.accumulate && p.act != IDDGCN_ACT_NONE) return false;
     nv = 0;
-    aux = p.act == IDDGCN_ACT_DSIGMOID;
+    aux = p.act == IDDGCN_ACT_DSIGMOID || p.accumulate;
     return true;
 }
 // ~128 row ranges (a multiple of 8) x 2 column halves: one 138-KB workgroup per CU, every one resident
@@ -3322,6 +3322,7 @@ void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux) {
     nr = (nr + 7) / 8 * 8;
     const dim3 g((unsigned)(2 * nr)), blk(512);
     const int n_ranges = (int)nr;
+    if (p.accumulate) p.aux = p.C;
     if (nv == 1) hipLaunchKernelGGL((rowgemm256_b3_kernel<1, false>), g, blk, 0, st, p, n_ranges);
     else if (nv == 2) hipLaunchKernelGGL((rowgemm256_b3_kernel<2, false>), g, blk, 0, st, p, n_ranges);
     else if (aux) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, true>), g, blk, 0, st, p, n_ranges);

@@ -57,9 +57,9 @@ extern "C" {
  *     whole fp32 significand, while |x| > ~2^-110), and a product takes the six piece products of order
  *     >= 2^-16 on bf16 MFMAs (exact products, fp32 accumulation): a0w0 + a0w1 + a1w0 + a1w1 + a0w2 + a2w0.
  *     The dropped terms are <= 2^-23 |a w| per product (fp32's own product rounding is <= 2^-24 |a w|).
- *     Row GEMMs: the plain form, the gathered-combine forward with R = 1 or 2 per-edge coefficients (no
- *     coef_idx) and the sigma' backward, without a_idx / accumulate / planes; every other form takes the
- *     exact f32 kernel.  TN GEMMs: D = 256.  Deterministic; not bitwise equal to the exact mode.
+ *     Row GEMMs: the plain form, C += A B (accumulate with act none), the gathered-combine forward with
+ *     R = 1 or 2 per-edge coefficients (no coef_idx) and the sigma' backward, without a_idx / planes; every
+ *     other form takes the exact f32 kernel.  TN GEMMs: D = 256.  Deterministic; not bitwise equal to the exact mode.
  * Row GEMMs for D < 256 and every other kernel compute in exact f32 (or F32_4CHAIN where asked). */
 #define IDDGCN_GEMM_EXACT_F32 0
 #define IDDGCN_GEMM_SPLIT_F16 1

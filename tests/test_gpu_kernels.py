@@ -526,10 +526,14 @@ def test_rowgemm_split_f16_vs_fp64(mode, cuda):
         kw = dict(b_trans=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D, v_row_stride=0,
                   act=L.ACT_DSIGMOID, aux=X.float())
         ref = (A @ S.t() + dz @ Wa.t()) * X * (1 - X)
-    elif mode == "accumulate":
+    elif mode in ("accumulate", "accumulate_trans", "accumulate_sigmoid"):
         C0 = torch.randn(M, D, generator=g, dtype=torch.float64).to(cuda)
-        kw = dict(accumulate=True)
-        ref = C0 + A @ S
+        kw = dict(accumulate=True, b_trans=mode == "accumulate_trans")
+        ref = C0 + A @ (S.t() if mode == "accumulate_trans" else S)
+        if mode == "accumulate_sigmoid":
+            kw.update(act=L.ACT_SIGMOID)
+            ref = torch.sigmoid(ref)
+        kid = 501
     elif mode == "gatherA":
         ai = torch.randint(0, M, (M,), generator=g).to(cuda)
         kw = dict(a_idx=ai.int())
@@ -591,8 +595,8 @@ def test_gemm_tn_split_f16_vs_fp64(M, kind, cuda):
 
 
 B3_FORMS = ["plain", "trans", "combine", "combine_r1", "combine_runs", "combine_random", "dsig", "small_M",
-            "tiny_M", "row_decades", "zero_rows"]
-B3_FALLBACK = ["accumulate", "gatherA", "rank_bcast", "coef_idx"]
+            "tiny_M", "row_decades", "zero_rows", "accumulate", "accumulate_trans"]
+B3_FALLBACK = ["gatherA", "rank_bcast", "coef_idx", "accumulate_sigmoid"]
 
 
 @pytest.mark.parametrize("mode", B3_FORMS + B3_FALLBACK)
@@ -601,8 +605,9 @@ def test_rowgemm_bf16x3_vs_fp64(mode, cuda):
     pieces, six bf16 MFMA products, fp32 accumulation): error vs an fp64 torch reference within 1.25x the
     exact-f32 MFMA path's (floor 1e-6 of max|ref|) on every form the bf16x3 kernel takes (the column-half
     kernel is asserted: 500 + 10 NV + aux), incl. ragged and tiny M, tiles with up to 32 distinct gathered rows,
-    rows spanning 12 decades (per-row error 1e-5) and zero rows; deterministic run to run.  The forms it does
-    not take (accumulate, gathered A, broadcast V, coef_idx) run the exact kernel: bitwise the exact mode."""
+    rows spanning 12 decades (per-row error 1e-5), zero rows and C += A B (in place, the old C rows through
+    the aux slab); deterministic run to run.  The forms it does not take (gathered A, broadcast V, coef_idx,
+    accumulate with an activation) run the exact kernel: bitwise the exact mode."""
     g = torch.Generator().manual_seed(sum(map(ord, mode)) + 7)
     D, N, R = 256, 700, (1 if mode == "combine_r1" else 2)
     M = {"small_M": 77, "tiny_M": 5}.get(mode, 20_000 + 17)
@@ -645,10 +650,14 @@ def test_rowgemm_bf16x3_vs_fp64(mode, cuda):
         kw = dict(b_trans=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D, v_row_stride=0,
                   act=L.ACT_DSIGMOID, aux=X.float())
         ref = (A @ S.t() + dz @ Wa.t()) * X * (1 - X)
-    elif mode == "accumulate":
+    elif mode in ("accumulate", "accumulate_trans", "accumulate_sigmoid"):
         C0 = torch.randn(M, D, generator=g, dtype=torch.float64).to(cuda)
-        kw = dict(accumulate=True)
-        ref = C0 + A @ S
+        kw = dict(accumulate=True, b_trans=mode == "accumulate_trans")
+        ref = C0 + A @ (S.t() if mode == "accumulate_trans" else S)
+        if mode == "accumulate_sigmoid":
+            kw.update(act=L.ACT_SIGMOID)
+            ref = torch.sigmoid(ref)
+        kid = 501
     elif mode == "gatherA":
         ai = torch.randint(0, M, (M,), generator=g).to(cuda)
         kw = dict(a_idx=ai.int())
