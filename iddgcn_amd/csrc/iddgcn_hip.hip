@@ -592,6 +592,17 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // Slab 0 holds 32 rows (it also stages the C tile); WIDE slabs r >= 1 hold GATHER_CAP rows.
     constexpr int CAPV = WIDE ? GATHER_CAP : (CAPPED ? V3_CAP2 : 32);
     constexpr int SLABC = CAPV * 32;
+    // WIDE forward, slot-major V (V3_SLOTV): the tile's distinct V rows as [slot][relation][32 columns] after
+    // slab 0, so ONE LDS-DMA instruction (64 lanes x 16 B, each lane its own relation row and 16-B group)
+    // fetches a distinct row's 32 columns for all R <= 8 relations (two rows at R <= 4) instead of one
+    // instruction per relation; CAPN slots in the bytes the capped per-relation slabs used
+#ifndef V3_SLOTV
+#define V3_SLOTV 1
+#endif
+    constexpr bool SLOTV = WIDE && !AUX && V3_SLOTV;
+    constexpr int RPI = WIDE ? 64 / (NV * 8) : 1;      // distinct rows per DMA instruction (SLOTV)
+    constexpr int CAPN = WIDE ? ((NSL - 1) * SLABC) / (NV * 32) / RPI * RPI : 0;
+    static_assert(!SLOTV || CAPN >= 2, "slot-major V: at least two distinct rows");
     constexpr int SLABS = SLAB + (NSL - 1) * SLABC;    // floats of all slabs of one wave
     // coefficient slots: 32 rows x R; up to 8 relations for WIDE and for broadcast V (NV = 0)
     static_assert(!CW || (NV == 0 && HAS_COEF), "CW: broadcast V rows only");
@@ -778,6 +789,20 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             vslot = __popcll(m & ((2ull << (lane & 31)) - 1)) - 1;
             if (start) cmpw[vslot] = vi;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (SLOTV) {
+                const int un = u < CAPN ? u : CAPN;          // rows past CAPN are read from L2 in the epilogue
+                const int rl = (lane >> 3) & (NV - 1);       // this lane's relation (past R: relation 0, never read)
+                // element offset of this lane's relation row and 16-B group (32-bit: R N D < 2^32)
+                const unsigned loff = (unsigned)((rl < R ? rl : 0) * p.v_rel_stride) + (unsigned)c0;
+                for (int kb = 0; kb < un; kb += RPI) {
+                    const int slot = kb + lane / (NV * 8);
+                    const unsigned g = (unsigned)((lane & 7) ^ (slot & 7));
+                    // RPI = 1: one row per instruction, its index wave-uniform (a scalar base)
+                    const int vr = RPI == 1 ? __builtin_amdgcn_readfirstlane(cmpw[kb]) : cmpw[slot < un ? slot : un - 1];
+                    const float* gp = p.V + (long long)vr * D + (loff + 4 * g);
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(slabw + SLAB + kb * NV * 32), 16, 0, 0);
+                }
+            } else
             for (int kb = 0; kb < u; kb += 8) {
                 const int row = kb + (lane >> 3);
                 const int g = (lane & 7) ^ ((row >> 1) & 7);
@@ -898,15 +923,18 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                     v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (i * D + col) * 4, 0, 0));
             }
             if (NV > 0 && !(V3_ABL & 2)) {
-                const int offv = vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
+                // (SLOTV: a slot past CAPN reads slot 0's words, then takes the L2 row below)
+                const int offv = SLOTV ? SLAB + (vslot < CAPN ? vslot : 0) * NV * 32 + 4 * ((2 * j + h) ^ (vslot & 7))
+                                       : vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
 #pragma unroll
                 for (int r = 0; r < NV; ++r) {
                     if constexpr (WIDE) {
                         if (r >= R) break;
                     }
-                    f32x4 s = ld4(slabw + soff(r) + offv);
+                    f32x4 s = ld4(slabw + (SLOTV ? offv + r * 32 : soff(r) + offv));
                     if constexpr (CAPPED) {
-                        if (r > 0 && vslot >= CAPV) {    // a distinct row past the capped slab: from L2
+                        // a distinct row past the slots (SLOTV) or the capped slab r >= 1: from L2
+                        if ((SLOTV || r > 0) && vslot >= (SLOTV ? CAPN : CAPV)) {
                             const int vrow = cmpw[vslot];
                             typedef const __attribute__((address_space(1))) f32x4* gf4p;
                             s = *(gf4p)(p.V + r * p.v_rel_stride + (long long)vrow * D + col);
