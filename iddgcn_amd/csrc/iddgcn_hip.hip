@@ -2736,45 +2736,95 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
             auto load_perm = [&](int k) __attribute__((always_inline)) {
                 return (sub < U && k + sub < len) ? perm[beg + k + sub] : -1;
             };
-            int evn = -1, rvn = 0;
-            float yvn = 0.f;
-            RawT bn[U];
-            auto load_group = [&](int ev) __attribute__((always_inline)) {
-                rvn = ev >= 0 ? r_idx[ev] : 0;
-                yvn = (ev >= 0 && y) ? y[ev] : 0.f;
-                evn = ev;
+#ifndef DM_PF2
+#define DM_PF2 0
+#endif
+            // one group's indices (lane u: edge u), relations, labels and raw tail rows
+            struct Grp {
+                int ev, rv;
+                float yv;
+                RawT bn[U];
+            };
+            auto load_group = [&](int ev, Grp& G) __attribute__((always_inline)) {
+                G.rv = ev >= 0 ? r_idx[ev] : 0;
+                G.yv = (ev >= 0 && y) ? y[ev] : 0.f;
+                G.ev = ev;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int eu = __builtin_amdgcn_readlane(ev, u);
                     const RawT* src = reinterpret_cast<const RawT*>(reinterpret_cast<const char*>(Xt) +
                                                                    ((long long)eu * D + sub * 4) * (BF ? 2 : 4));
-                    if (eu >= 0) bn[u] = *src;
-                    else bn[u] = RawT{};
+                    if (eu >= 0) G.bn[u] = *src;
+                    else G.bn[u] = RawT{};
                 }
             };
-            int ev2 = -1;
-            if (len > 0) {
-                const int ev1 = load_perm(0);
-                ev2 = load_perm(U);
-                load_group(ev1);
-            }
-            for (int k0 = 0; k0 < len; k0 += U) {
-                long long e[U];
-                int rr[U];
-                float yy[U];
-                f32x4 b[U];
+            auto unpack = [&](const Grp& G, long long (&e)[U], int (&rr)[U], float (&yy)[U], f32x4 (&b)[U])
+                __attribute__((always_inline)) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    e[u] = __builtin_amdgcn_readlane(evn, u);
-                    rr[u] = __builtin_amdgcn_readlane(rvn, u);
-                    yy[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, yvn), u));
-                    if constexpr (BF) b[u] = bf4_to_f32(bn[u]);
-                    else b[u] = bn[u];
+                    e[u] = __builtin_amdgcn_readlane(G.ev, u);
+                    rr[u] = __builtin_amdgcn_readlane(G.rv, u);
+                    yy[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, G.yv), u));
+                    if constexpr (BF) b[u] = bf4_to_f32(G.bn[u]);
+                    else b[u] = G.bn[u];
                 }
-                const int ev3 = load_perm(k0 + 2 * U);
-                if (k0 + U < len) load_group(ev2);
-                ev2 = ev3;
-                body(e, rr, yy, b);
+            };
+            if constexpr (DM_PF2) {
+                // two groups in flight (DM_PF2): while group i is computed, the rows of groups i+1 and i+2
+                // and the perm entries of group i+3 load; the group registers alternate between two sets
+                // (the loop is unrolled by two, so every index into them is static)
+                Grp GA, GB;
+                int evp = -1;
+                if (len > 0) {
+                    const int ev0 = load_perm(0), ev1 = load_perm(U);
+                    evp = load_perm(2 * U);
+                    load_group(ev0, GA);
+                    if (U < len) load_group(ev1, GB);
+                }
+                for (int k0 = 0; k0 < len; k0 += 2 * U) {
+                    {
+                        long long e[U];
+                        int rr[U];
+                        float yy[U];
+                        f32x4 b[U];
+                        unpack(GA, e, rr, yy, b);
+                        const int evq = load_perm(k0 + 3 * U);
+                        if (k0 + 2 * U < len) load_group(evp, GA);
+                        evp = evq;
+                        body(e, rr, yy, b);
+                    }
+                    if (k0 + U >= len) break;
+                    {
+                        long long e[U];
+                        int rr[U];
+                        float yy[U];
+                        f32x4 b[U];
+                        unpack(GB, e, rr, yy, b);
+                        const int evq = load_perm(k0 + 4 * U);
+                        if (k0 + 3 * U < len) load_group(evp, GB);
+                        evp = evq;
+                        body(e, rr, yy, b);
+                    }
+                }
+            } else {
+                Grp G;
+                int ev2 = -1;
+                if (len > 0) {
+                    const int ev1 = load_perm(0);
+                    ev2 = load_perm(U);
+                    load_group(ev1, G);
+                }
+                for (int k0 = 0; k0 < len; k0 += U) {
+                    long long e[U];
+                    int rr[U];
+                    float yy[U];
+                    f32x4 b[U];
+                    unpack(G, e, rr, yy, b);
+                    const int ev3 = load_perm(k0 + 2 * U);
+                    if (k0 + U < len) load_group(ev2, G);
+                    ev2 = ev3;
+                    body(e, rr, yy, b);
+                }
             }
         } else {
             // slot s takes edge groups k = (it*SLOTS + s)*U: same trip count for the whole wave
