@@ -1781,10 +1781,11 @@ constexpr int SLAB = TR * CWV;              // floats of a [32 rows][16 columns]
 // epilogue's ds_read_b128 (slot l&15 [+16], group l>>4) is conflict-free in each of its four lane groups
 __device__ __forceinline__ int slab16_off(int slot, int g) { return slot * 16 + 4 * (g ^ ((-(slot >> 2)) & 3)); }
 
-template <int NV, bool AUX>
+template <int NV, bool AUX, bool BC = false>
 __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ranges) {
     using namespace rb3;
     static_assert(NV >= 0 && NV <= 2 && !(NV > 0 && AUX), "b3: gathered forward (NV = R = 1, 2), sigma' backward, plain");
+    static_assert(!BC || NV == 0, "BC: one broadcast V row per relation (R <= 2), e.g. dz W_a^T");
     constexpr int NSL = NV + (AUX ? 1 : 0);
     constexpr int WF = NSL * SLAB + 64 + 64 + 32 + 256;         // slabs, coef [32][R], idx [64], cmp [32], prefetch KiB
     constexpr int LDSB = 2 * ABYTES + NW * WF * 4;
@@ -1827,6 +1828,13 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
             w2[q][e] = c;
         }
 
+    // BC: the broadcast V rows (v_row_stride 0: the same R <= 2 rows for every output row), this lane's columns
+    f32x4 vb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    if constexpr (BC) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+            if (r < p.R) vb[r] = ld4(p.V + r * p.v_rel_stride + c0 + 4 * g);
+    }
     // Every issue site returns its count of vector-memory ops (wave-uniform), so each wait below is the exact
     // vmcnt for what it needs, never a drain of the prefetches behind it.
     auto dma_idx = [&](long long t) __attribute__((always_inline)) -> int {
@@ -1896,6 +1904,13 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
             __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + ci), (lds_vptr)coefw, 4, 0, 0);
             n += 1;
         }
+        if constexpr (BC) {      // the tile's 32 x R row coefficients, one 4-B DMA per lane
+            const long long last = (long long)p.M * p.R - 1;
+            long long ci = t * TR * p.R + lane;
+            if (ci > last) ci = last;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + ci), (lds_vptr)coefw, 4, 0, 0);
+            n += 1;
+        }
         if constexpr (AUX) {
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -1926,6 +1941,15 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
                     const f32x4 s = ld4(slabw + r * SLAB + slab16_off(vs, g));
 #pragma unroll
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf, s[q], v[q]);
+                }
+            }
+            if constexpr (BC) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    if (r >= p.R) break;
+                    const float cf = coefw[row * p.R + r];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = fmaf(cf, vb[r][q], v[q]);
                 }
             }
             if (AUX && p.accumulate) {
@@ -2737,7 +2761,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 return (sub < U && k + sub < len) ? perm[beg + k + sub] : -1;
             };
 #ifndef DM_PF2
-#define DM_PF2 0
+#define DM_PF2 1      // two groups in flight at R >= 4: config-5 shape 7.22 -> 6.91 ms; R = 2: +3%, not taken
 #endif
             // one group's indices (lane u: edge u), relations, labels and raw tail rows
             struct Grp {
@@ -2769,7 +2793,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                     else b[u] = G.bn[u];
                 }
             };
-            if constexpr (DM_PF2) {
+            if constexpr (DM_PF2 && RT >= 4) {
                 // two groups in flight (DM_PF2): while group i is computed, the rows of groups i+1 and i+2
                 // and the perm entries of group i+3 load; the group registers alternate between two sets
                 // (the loop is unrolled by two, so every index into them is static)
@@ -3372,13 +3396,23 @@ int check_rowgemm(const iddgcn_rowgemm_t& a) {
     return 0;
 }
 
-// The bf16x3 row GEMM's forms (rowgemm256_b3_kernel<NV, AUX>): plain, sigma' backward (AUX), gathered-combine
-// forward with exactly R = NV in {1, 2} per-edge coefficients; no a_idx, accumulate, coef_idx or planes.
+// The bf16x3 row GEMM's forms (rowgemm256_b3_kernel<NV, AUX, BC>): plain, C += A B, sigma' backward (AUX),
+// gathered-combine forward with exactly R = NV in {1, 2} per-edge coefficients, broadcast V with R <= 2 row
+// coefficients (BC, plain or sigma'); no a_idx, coef_idx or planes.
 #ifndef B3_DISABLE
 #define B3_DISABLE 0     // experiment builds only: 1 no bf16x3 row GEMM (exact instead), 2 no bf16x3 TN
 #endif
-bool b3_select(const RowGemmP& p, int& nv, bool& aux) {
+bool b3_select(const RowGemmP& p, int& nv, bool& aux, bool& bc) {
+    bc = false;
     if ((B3_DISABLE & 1) || p.precision != IDDGCN_GEMM_BF16X3 || p.a_idx || p.planes) return false;
+    if (p.R > 0 && p.v_row_stride == 0 && !p.v_idx) {
+        // broadcast V (one row per relation for every output row: dz W_a^T), plain or with the sigma' factor
+        if (p.R > 2 || p.coef_idx || p.accumulate || p.act == IDDGCN_ACT_SIGMOID) return false;
+        nv = 0;
+        aux = p.act == IDDGCN_ACT_DSIGMOID;
+        bc = true;
+        return true;
+    }
     if (p.R > 0) {
         if (p.R > 2 || p.v_row_stride != 256 || p.coef_idx || p.act == IDDGCN_ACT_DSIGMOID || p.accumulate) return false;
         nv = p.R;
@@ -3392,7 +3426,7 @@ bool b3_select(const RowGemmP& p, int& nv, bool& aux) {
     return true;
 }
 // ~128 row ranges (a multiple of 8) x 2 column halves: one 138-KB workgroup per CU, every one resident
-void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux) {
+void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux, bool bc) {
     const long long nt = ((long long)p.M + rb3::TR - 1) / rb3::TR;
     long long nr = nt < 128 ? nt : 128;
     p.tiles_per_block = (int)((nt + nr - 1) / nr);
@@ -3401,7 +3435,9 @@ void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux) {
     const dim3 g((unsigned)(2 * nr)), blk(512);
     const int n_ranges = (int)nr;
     if (p.accumulate) p.aux = p.C;
-    if (nv == 1) hipLaunchKernelGGL((rowgemm256_b3_kernel<1, false>), g, blk, 0, st, p, n_ranges);
+    if (bc && aux) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, true, true>), g, blk, 0, st, p, n_ranges);
+    else if (bc) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, false, true>), g, blk, 0, st, p, n_ranges);
+    else if (nv == 1) hipLaunchKernelGGL((rowgemm256_b3_kernel<1, false>), g, blk, 0, st, p, n_ranges);
     else if (nv == 2) hipLaunchKernelGGL((rowgemm256_b3_kernel<2, false>), g, blk, 0, st, p, n_ranges);
     else if (aux) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, true>), g, blk, 0, st, p, n_ranges);
     else hipLaunchKernelGGL((rowgemm256_b3_kernel<0, false>), g, blk, 0, st, p, n_ranges);
@@ -3558,9 +3594,9 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     hipStream_t st = (hipStream_t)stream;
     if (p.precision == IDDGCN_GEMM_BF16X3) {
         int nv;
-        bool aux;
-        if (a->D == 256 && b3_select(p, nv, aux)) {
-            launch_b3(st, p, nv, aux);
+        bool aux, bc;
+        if (a->D == 256 && b3_select(p, nv, aux, bc)) {
+            launch_b3(st, p, nv, aux, bc);
             return launch_status();
         }
         p.precision = IDDGCN_GEMM_EXACT_F32;      // the forms the bf16x3 kernel does not take: exact f32
@@ -3598,8 +3634,8 @@ int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* a) {
     RowGemmP p = to_p(*a);
     if (p.precision == IDDGCN_GEMM_BF16X3) {
         int nv;
-        bool aux;
-        if (a->D == 256 && b3_select(p, nv, aux)) return 500 + 10 * nv + (aux ? 1 : 0);
+        bool aux, bc;
+        if (a->D == 256 && b3_select(p, nv, aux, bc)) return 500 + 10 * nv + (aux ? 1 : 0) + (bc ? 2 : 0);
         p.precision = IDDGCN_GEMM_EXACT_F32;
     }
     V3Sel sel;

@@ -58,8 +58,8 @@ extern "C" {
  *     >= 2^-16 on bf16 MFMAs (exact products, fp32 accumulation): a0w0 + a0w1 + a1w0 + a1w1 + a0w2 + a2w0.
  *     The dropped terms are <= 2^-23 |a w| per product (fp32's own product rounding is <= 2^-24 |a w|).
  *     Row GEMMs: the plain form, C += A B (accumulate with act none), the gathered-combine forward with
- *     R = 1 or 2 per-edge coefficients (no coef_idx) and the sigma' backward, without a_idx / planes; every
- *     other form takes the exact f32 kernel.  TN GEMMs: D = 256.  Deterministic; not bitwise equal to the exact mode.
+ *     R = 1 or 2 per-edge coefficients (no coef_idx), broadcast V rows (v_row_stride 0, R <= 2, plain or
+ *     sigma') and the sigma' backward, without a_idx / planes; every other form takes the exact f32 kernel.  TN GEMMs: D = 256.  Deterministic; not bitwise equal to the exact mode.
  * Row GEMMs for D < 256 and every other kernel compute in exact f32 (or F32_4CHAIN where asked). */
 #define IDDGCN_GEMM_EXACT_F32 0
 #define IDDGCN_GEMM_SPLIT_F16 1
@@ -130,7 +130,7 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
  * tables: 1, 2, or capacity 4 / 8 for R <= 8, whose LDS slabs keep 7 distinct V rows per 32-row tile
  * and read further ones from L2); 100 for the register-staged kernel (D < 256, and D = 256 forms the v3
  * kernel does not take: a gathered V with the sigma' epilogue, V rows that are not dense); 500 + 10*NV + aux
- * for the bf16x3 row GEMM (IDDGCN_GEMM_BF16X3 forms it takes); -1 for an invalid D. */
+ * (+ 2 for broadcast V rows) for the bf16x3 row GEMM (IDDGCN_GEMM_BF16X3 forms it takes); -1 for an invalid D. */
 int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* args);
 
 /* C[D][D] (+)= A^T · B over M rows (A, B are M x D).  Two stages: each of n_blocks

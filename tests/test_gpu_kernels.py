@@ -519,13 +519,20 @@ def test_rowgemm_split_f16_vs_fp64(mode, cuda):
         X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
         kw = dict(b_trans=True, act=L.ACT_DSIGMOID, aux=X.float())
         ref = (A @ S.t()) * X * (1 - X)
-    elif mode == "rank_bcast":
+    elif mode in ("rank_bcast", "bcast", "bcast_r1"):
+        # dO S^T + dz W_a^T (broadcast V: one row per relation for every output row), with the sigma' factor
+        # (head-chain backward, layers 2-3) or without (dE, layer 1)
+        Rb = 1 if mode == "bcast_r1" else R
         X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
-        dz = torch.randn(M, R, generator=g, dtype=torch.float64).to(cuda)
-        Wa = torch.randn(D, R, generator=g, dtype=torch.float64).to(cuda)
-        kw = dict(b_trans=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D, v_row_stride=0,
-                  act=L.ACT_DSIGMOID, aux=X.float())
-        ref = (A @ S.t() + dz @ Wa.t()) * X * (1 - X)
+        dz = torch.randn(M, Rb, generator=g, dtype=torch.float64).to(cuda)
+        Wa = torch.randn(D, Rb, generator=g, dtype=torch.float64).to(cuda)
+        kw = dict(b_trans=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D, v_row_stride=0)
+        ref = A @ S.t() + dz @ Wa.t()
+        kid = 502
+        if mode == "rank_bcast":
+            kw.update(act=L.ACT_DSIGMOID, aux=X.float())
+            ref = ref * X * (1 - X)
+            kid = 503
     elif mode in ("accumulate", "accumulate_trans", "accumulate_sigmoid"):
         C0 = torch.randn(M, D, generator=g, dtype=torch.float64).to(cuda)
         kw = dict(accumulate=True, b_trans=mode == "accumulate_trans")
@@ -595,8 +602,9 @@ def test_gemm_tn_split_f16_vs_fp64(M, kind, cuda):
 
 
 B3_FORMS = ["plain", "trans", "combine", "combine_r1", "combine_runs", "combine_random", "dsig", "small_M",
-            "tiny_M", "row_decades", "zero_rows", "accumulate", "accumulate_trans"]
-B3_FALLBACK = ["gatherA", "rank_bcast", "coef_idx", "accumulate_sigmoid"]
+            "tiny_M", "row_decades", "zero_rows", "accumulate", "accumulate_trans", "rank_bcast", "bcast",
+            "bcast_r1"]
+B3_FALLBACK = ["gatherA", "coef_idx", "accumulate_sigmoid"]
 
 
 @pytest.mark.parametrize("mode", B3_FORMS + B3_FALLBACK)
@@ -605,9 +613,10 @@ def test_rowgemm_bf16x3_vs_fp64(mode, cuda):
     pieces, six bf16 MFMA products, fp32 accumulation): error vs an fp64 torch reference within 1.25x the
     exact-f32 MFMA path's (floor 1e-6 of max|ref|) on every form the bf16x3 kernel takes (the column-half
     kernel is asserted: 500 + 10 NV + aux), incl. ragged and tiny M, tiles with up to 32 distinct gathered rows,
-    rows spanning 12 decades (per-row error 1e-5), zero rows and C += A B (in place, the old C rows through
-    the aux slab); deterministic run to run.  The forms it does not take (gathered A, broadcast V, coef_idx,
-    accumulate with an activation) run the exact kernel: bitwise the exact mode."""
+    rows spanning 12 decades (per-row error 1e-5), zero rows, C += A B (in place, the old C rows through the
+    aux slab) and broadcast V rows (dz W_a^T, R = 1, 2, with and without the sigma' factor); deterministic run
+    to run.  The forms it does not take (gathered A, coef_idx, accumulate with an activation) run the exact
+    kernel: bitwise the exact mode."""
     g = torch.Generator().manual_seed(sum(map(ord, mode)) + 7)
     D, N, R = 256, 700, (1 if mode == "combine_r1" else 2)
     M = {"small_M": 77, "tiny_M": 5}.get(mode, 20_000 + 17)
@@ -643,13 +652,20 @@ def test_rowgemm_bf16x3_vs_fp64(mode, cuda):
         kw = dict(b_trans=True, act=L.ACT_DSIGMOID, aux=X.float())
         ref = (A @ S.t()) * X * (1 - X)
         kid = 501
-    elif mode == "rank_bcast":
+    elif mode in ("rank_bcast", "bcast", "bcast_r1"):
+        # dO S^T + dz W_a^T (broadcast V: one row per relation for every output row), with the sigma' factor
+        # (head-chain backward, layers 2-3) or without (dE, layer 1)
+        Rb = 1 if mode == "bcast_r1" else R
         X = torch.rand(M, D, generator=g, dtype=torch.float64).to(cuda)
-        dz = torch.randn(M, R, generator=g, dtype=torch.float64).to(cuda)
-        Wa = torch.randn(D, R, generator=g, dtype=torch.float64).to(cuda)
-        kw = dict(b_trans=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D, v_row_stride=0,
-                  act=L.ACT_DSIGMOID, aux=X.float())
-        ref = (A @ S.t() + dz @ Wa.t()) * X * (1 - X)
+        dz = torch.randn(M, Rb, generator=g, dtype=torch.float64).to(cuda)
+        Wa = torch.randn(D, Rb, generator=g, dtype=torch.float64).to(cuda)
+        kw = dict(b_trans=True, coef=dz.float(), V=Wa.t().contiguous().float(), v_rel_stride=D, v_row_stride=0)
+        ref = A @ S.t() + dz @ Wa.t()
+        kid = 502
+        if mode == "rank_bcast":
+            kw.update(act=L.ACT_DSIGMOID, aux=X.float())
+            ref = ref * X * (1 - X)
+            kid = 503
     elif mode in ("accumulate", "accumulate_trans", "accumulate_sigmoid"):
         C0 = torch.randn(M, D, generator=g, dtype=torch.float64).to(cuda)
         kw = dict(accumulate=True, b_trans=mode == "accumulate_trans")

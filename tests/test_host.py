@@ -223,9 +223,10 @@ def test_rowgemm_precision_is_a_per_call_argument():
 
 def test_bf16x3_kernel_selection_is_pure_host():
     """ABI 7: which D = 256 kernel a bf16x3 row GEMM takes (iddgcn_rowgemm_kernel_id, nothing launched, no GPU):
-    the column-half bf16x3 kernel (500 + 10 NV + aux) for the plain form, C += A B, the sigma' backward and the
-    gathered forward with R = NV <= 2 per-edge coefficients; the exact kernel's id for every form it does not
-    take (gathered A, accumulate with an activation, broadcast V, coef_idx, R > 2, D < 256)."""
+    the column-half bf16x3 kernel (500 + 10 NV + aux + 2 bc) for the plain form, C += A B, the sigma' backward,
+    the gathered forward with R = NV <= 2 per-edge coefficients and broadcast V rows (R <= 2); the exact
+    kernel's id for every form it does not take (gathered A, accumulate with an activation, coef_idx, R > 2,
+    D < 256)."""
     lib = _lib.lib()
     fake = ctypes.c_void_p(16)          # never dereferenced: kernel_id inspects the arguments only
 
@@ -242,8 +243,11 @@ def test_bf16x3_kernel_selection_is_pure_host():
                    act=_lib.ACT_SIGMOID) == 500 + 10 * R
     exact = lambda **kw: kid(precision=_lib.GEMM_EXACT_F32, **kw)  # noqa: E731
     assert kid(accumulate=1) == 501 and kid(accumulate=1, b_trans=1) == 501      # C += A B: old C via the aux slab
+    # broadcast V (dz W_a^T), with and without the sigma' factor
+    assert kid(R=2, coef=fake, V=fake, v_rel_stride=256, v_row_stride=0, act=_lib.ACT_DSIGMOID, aux=fake, b_trans=1) == 503
+    assert kid(R=1, coef=fake, V=fake, v_rel_stride=256, v_row_stride=0, b_trans=1) == 502
     for kw in (dict(accumulate=1, act=_lib.ACT_SIGMOID), dict(a_idx=fake),
-               dict(R=2, coef=fake, V=fake, v_rel_stride=256, v_row_stride=0, act=_lib.ACT_DSIGMOID, aux=fake),
+               dict(R=3, coef=fake, V=fake, v_rel_stride=256, v_row_stride=0, act=_lib.ACT_DSIGMOID, aux=fake),
                dict(R=2, coef=fake, coef_idx=fake, V=fake, v_idx=fake, v_rel_stride=2560, v_row_stride=256),
                dict(R=3, coef=fake, V=fake, v_idx=fake, v_rel_stride=2560, v_row_stride=256),
                dict(D=64)):
