@@ -26,8 +26,8 @@ SYMBOLS = {
               "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, false,",
               "tail_dS_tn": "gemm_tn256_x3_kernel<"},
     # bf16x3 operands (ABI 7): the column-half row GEMM and the transposed-read TN
-    "bf16x3": {"tail_fwd_gemm": "rowgemm256_b3_kernel<2, false>",
-               "tail_bwd_gemm": "rowgemm256_b3_kernel<0, true>",
+    "bf16x3": {"tail_fwd_gemm": "rowgemm256_b3_kernel<2, false, false>",
+               "tail_bwd_gemm": "rowgemm256_b3_kernel<0, true, false>",
                "tail_dS_tn": "gemm_tn256_b3_kernel"},
     "exact": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, false, false, false, false, false>",
               "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, false, false, false, false, false>",
