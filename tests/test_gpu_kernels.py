@@ -874,9 +874,9 @@ def test_tail_seg_per_edge_w(R, case, dsum, cuda):
         assert _maxrel(dWe, dWe1) <= 1e-6
 
 
-@pytest.mark.parametrize("D,mode", [(256, "split"), (256, "exact"), (64, "exact")])
+@pytest.mark.parametrize("D,mode", [(256, "split"), (256, "bf16x3"), (256, "exact"), (64, "exact")])
 def test_gemm_tn_batched(D, mode, cuda):
-    """iddgcn_gemm_tn_batched_f32 (one launch, blockIdx.y = entry, at D = 256 split; the single-call kernels in
+    """iddgcn_gemm_tn_batched_f32 (one launch, blockIdx.y = entry, at D = 256 split / bf16x3; the single-call kernels in
     turn otherwise) against float64 references and the single-call results: entries of different row counts
     (one empty), accumulate on / off, up to TN_BATCH entries; the batched launch is deterministic."""
     g = torch.Generator().manual_seed(D + len(mode))
