@@ -192,11 +192,27 @@ def reference_init(np, N, R, D, seed):
     return p
 
 
-def cpu_baseline(cfg, frac=0.1, budget_s=30.0):
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), for the cpu_baseline record (core count and CPU
+    model next to every CPU number)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, frac=0.05, min_steps=3, budget_s=60.0):
     """The reference formulation on the host cores (one full step: pos + neg forward, autograd backward,
     Keras Adam), on a bounded sample of the same workload: the same N, D, R and a `frac` share of its
     adjacency edges (and as many negatives).  The reference formulation's cost is linear in the edges
-    (per-edge GEMMs, SpMM per layer), so edges/s on the sample is the full step's rate."""
+    (per-edge GEMMs, SpMM per layer), so edges/s on the sample is the full step's rate (its per-layer dense
+    N x D SpMM outputs are a fixed cost that a smaller sample weighs more: the sample's rate is a lower bound
+    of the full workload's).  Protocol: one warm-up step, then the median of `min_steps` timed
+    steps (more while the budget allows)."""
     import numpy as np
     import torch
     from oracle.ref_model import KerasAdam, adj_to_torch, keras_bce, model_forward, to_torch_params
@@ -221,23 +237,49 @@ def cpu_baseline(cfg, frac=0.1, budget_s=30.0):
         return opt.step(params, {k: g.numpy() for k, g in zip(keys, grads)}, dtype=np.float32)
 
     M_s = max(1, int(round(cfg["M"] * frac)))
-    # warm-up (thread pool, allocator) on a 2% graph, then the timed steps on the frac sample
-    step(*make(max(1, min(M_s, int(cfg["M"] * 0.02)))))
     pos, neg, params, adj, opt = make(M_s)
+    params = step(pos, neg, params, adj, opt)           # warm-up (thread pool, allocator) on the same sample
     times = []
     while True:
         t0 = time.perf_counter()
         params = step(pos, neg, params, adj, opt)
         times.append(time.perf_counter() - t0)
-        if len(times) >= 3 or sum(times) + times[-1] > budget_s:
+        if len(times) >= min_steps and (len(times) >= 5 or sum(times) + times[-1] > budget_s):
             break
     t = statistics.median(times)
     return {"value": M_s / t, "unit": "adjacency edges/s", "cores": threads, "kind": "port",
-            "fraction_of_workload": M_s / cfg["M"],
+            "host_cpu_count": os.cpu_count(), "cpu_model": cpu_model(),
+            "fraction_of_workload": M_s / cfg["M"], "step_s": times,
+            "scored_edges_per_s": 2 * M_s / t,
             "sample": (f"oracle/ref_model.py reference formulation (torch-CPU fp32: per-edge GEMMs, A_r.E per layer, "
                        f"Keras BCE, autograd backward, Keras Adam), N={N} D={D} R={R}, {M_s} of the workload's "
                        f"{cfg['M']} adjacency edges ({100 * M_s / cfg['M']:.0f}%) + {M_s} negatives; median of "
-                       f"{len(times)} step(s) after a warm-up step, {t:.2f} s/step")}
+                       f"{len(times)} steps after a warm-up step, {t:.2f} s/step, {threads} torch threads on a "
+                       f"{os.cpu_count()}-CPU host ({cpu_model()})")}
+
+
+def step_roofline(N, R, D, T, M, gemm, features, ms_per_step):
+    """Whole-step roofline (T_roof = W_gemm / P_mfma + Q_hbm / BW, fraction =
+    T_roof / T_measured), for one rank's step.  Two forms: the BASELINE formula as written (W_gemm on the f32 MFMA
+    peak), and the same work on the peak of the MFMAs this mode issues (bf16x3: 6 bf16 products per fp32 product on
+    the 2.5 PF peak; split: 3 f16 products; the bf16-feature mode: 2 bf16 MFMAs per k-step, bf16 edge tables)."""
+    from iddgcn_amd.engine import step_bytes, step_flops
+    W = float(step_flops(N, R, D, T, M))
+    Q = float(step_bytes(N, R, D, T, M))
+    if features == "bf16":          # BASELINE.md: "for bf16, use 2.5 PFLOP/s and halve the D-terms"
+        Q = Q - 0.5 * (40.0 * T * D + 8.0 * 3 * R * T * D)
+    hw, peak = {"exact": (1, MFMA_F32_PEAK_TFLOPS), "split": (3, MFMA_F16_PEAK_TFLOPS),
+                "bf16x3": (6, MFMA_F16_PEAK_TFLOPS)}[gemm]
+    if features == "bf16":
+        hw, peak = 2, MFMA_F16_PEAK_TFLOPS
+    t_hbm = Q / (HBM_PEAK_GBS * 1e9) * 1e3
+    t_f32 = W / (MFMA_F32_PEAK_TFLOPS * 1e12) * 1e3
+    t_mode = hw * W / (peak * 1e12) * 1e3
+    return {"W_gemm_flop": W, "Q_hbm_bytes": Q, "t_hbm_ms": t_hbm,
+            "baseline_formula": {"t_mfma_ms": t_f32, "t_roof_ms": t_f32 + t_hbm, "frac": (t_f32 + t_hbm) / ms_per_step,
+                                 "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS},
+            "mode": {"gemm": gemm, "features": features, "mfma_products_per_flop": hw, "peak_TFLOPs": peak,
+                     "t_mfma_ms": t_mode, "t_roof_ms": t_mode + t_hbm, "frac": (t_mode + t_hbm) / ms_per_step}}
 
 
 def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=True, shard=None, steps=None,
@@ -334,10 +376,16 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
                       "parallelism": f"edge-dp{world}" + ("+relation-sharded-nodes" if eng.node_shard else "")
                       + ("+row-partitioned-spmm" if eng.spmm_shard else ""),
                       "gemm": gemm, "features": feat},
-           "scored_edges_per_s": T / (elapsed / steps), "loss": loss_val, "steps": steps, "warmup": warmup}
+           "scored_edges_per_s": T / (elapsed / steps), "loss": loss_val, "steps": steps, "warmup": warmup,
+           "step_roofline": step_roofline(N, R, D, ed.T, M, gemm, feat,
+                                          elapsed / steps * 1e3)}
     if world > 1:
         out["ranks_consistent"] = consist == 0.0
         out["params_max_abs_diff_vs_rank0"] = consist
+        # the RCCL-only branches (BucketedAllReduce's asynchronous in-place buckets, RelationShard's collectives, this
+        # consistency check and the secondary workloads' fit vote) have run over gloo only: every builder box has one
+        # GPU
+        out["rccl_paths_verified_before_this_run"] = False
     if other_mode and feat == "f32":
         mode2 = "exact" if gemm != "exact" else "bf16x3"
         el2, loss2, _ = timed_run(mode2, False)

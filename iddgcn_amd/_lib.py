@@ -37,7 +37,7 @@ class RowGemmArgs(ctypes.Structure):
         ("v_rel_stride", cll), ("v_row_stride", cll),
         ("act", ci), ("aux", vp),
         ("planes", ci),
-        ("precision", ci),     # ABI 6: GEMM operand precision per call (GEMM_EXACT_F32 / GEMM_SPLIT_F16)
+        ("precision", ci),     # ABI 6/7: operand precision per call (GEMM_EXACT_F32 / F32_4CHAIN / SPLIT_F16 / BF16X3)
     ]
 
 

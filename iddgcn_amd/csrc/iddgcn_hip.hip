@@ -792,11 +792,12 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             if constexpr (SLOTV) {
                 const int un = u < CAPN ? u : CAPN;          // rows past CAPN are read from L2 in the epilogue
                 const int rl = (lane >> 3) & (NV - 1);       // this lane's relation (past R: relation 0, never read)
-                // element offset of this lane's relation row and 16-B group (32-bit: R N D < 2^32)
-                const unsigned loff = (unsigned)((rl < R ? rl : 0) * p.v_rel_stride) + (unsigned)c0;
+                // element offset of this lane's relation row and 16-B group, 64-bit: (R-1)·v_rel_stride passes
+                // 2^32 elements at R = 8, D = 256 from N > 2.1M
+                const long long loff = (long long)(rl < R ? rl : 0) * p.v_rel_stride + c0;
                 for (int kb = 0; kb < un; kb += RPI) {
                     const int slot = kb + lane / (NV * 8);
-                    const unsigned g = (unsigned)((lane & 7) ^ (slot & 7));
+                    const int g = (lane & 7) ^ (slot & 7);
                     // RPI = 1: one row per instruction, its index wave-uniform (a scalar base)
                     const int vr = RPI == 1 ? __builtin_amdgcn_readfirstlane(cmpw[kb]) : cmpw[slot < un ? slot : un - 1];
                     const float* gp = p.V + (long long)vr * D + (loff + 4 * g);

@@ -344,8 +344,9 @@ class Engine:
     def forward(self, P, adj, ed, ws, train):
         N, R, D, T = self.N, self.R, self.D, ed.T
         E = P["E"]
-        pk = dict(precision=self.gemm)          # every GEMM call carries this engine's operand precision
-        pn = dict(precision=self.proj_gemm)     # (the plain node-level projections)
+        # every GEMM call carries this engine's operand precision: pn for the plain node-level projections, pr for
+        # the other row GEMMs
+        pn = dict(precision=self.proj_gemm)
         pr = dict(precision=self.row_gemm)      # (the other row GEMMs)
         sh = self.node_shard
         if sh is None and self.spmm_shard is not None:

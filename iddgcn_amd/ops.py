@@ -128,8 +128,10 @@ def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=
                   precision="exact"):
     """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32).  planes: L.PLANES_* flags,
     which of A / C / aux are pre-split planes tables (fp32-shaped tensors holding [hi | lo] fp16 rows;
-    D = 256, split GEMM mode).  precision: "exact" (v_mfma_f32_32x32x2_f32) or "split" (split-fp16
-    operands), per call (D = 256; other widths are exact f32)."""
+    D = 256, split GEMM mode).  precision, per call: "exact" (v_mfma_f32_32x32x2_f32, bitwise an fmaf chain),
+    "exact4" (the same MFMA, four interleaved accumulation chains: the node-level projections), "bf16x3" (fp32
+    operands split exactly into three bf16 pieces, six bf16 MFMA products, fp32 accumulation) or "split"
+    (split-fp16 operands, 22 significant bits); D < 256 runs exact f32 in every mode."""
     D = B.shape[0]
     M = C.shape[0] if M is None else M
     R = 0 if coef is None else coef.shape[-1]
@@ -163,10 +165,19 @@ def tn_blocks(M, D):
     return int(L.lib().iddgcn_gemm_tn_blocks(int(M), int(D)))
 
 
+def _tn_prec(precision):
+    """Operand precision of a TN GEMM: "exact", "bf16x3" or "split" (include/iddgcn.h; the TN kernels take no
+    four-chain form, so "exact4" is refused here rather than by the C side's IDDGCN_E_BAD_ARG)."""
+    if precision == "exact4":
+        raise L.IddgcnError("gemm_tn: precision 'exact4' is a row-GEMM form; use 'exact', 'bf16x3' or 'split'")
+    return _prec(precision)
+
+
 def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False, precision="exact"):
     """C (+)= A^T B; bf16 A and B (the bf16-feature mode) select iddgcn_gemm_tn_bf16; a_planes: A is a
     pre-split planes table (iddgcn_gemm_tn_planes_f32, D = 256, split GEMM mode); precision: the fp32 form's
-    operand precision ("exact" / "split", D = 256)."""
+    operand precision ("exact", "bf16x3" or "split" at D = 256; other widths exact f32)."""
+    prec = _tn_prec(precision)
     M, D = A.shape
     et = _BF16 if A.dtype == _BF16 else _F32
     _req(A, et, (M, D), "A")
@@ -177,20 +188,21 @@ def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False, precision="exact"):
         raise L.IddgcnError("gemm_tn slab too small")
     args = (_stream(), M, D, _ptr(A), _ptr(B), _ptr(slab), nb, _ptr(C), int(accumulate))
     if a_planes:
-        if et != _F32 or _prec(precision) != L.GEMM_SPLIT_F16:
+        if et != _F32 or prec != L.GEMM_SPLIT_F16:
             raise L.IddgcnError("gemm_tn: planes A takes an fp32-shaped table in the split mode")
         rc = L.lib().iddgcn_gemm_tn_planes_f32(*args)
     elif et == _BF16:
         rc = L.lib().iddgcn_gemm_tn_bf16(*args)
     else:
-        rc = L.lib().iddgcn_gemm_tn_f32(*args, _prec(precision))
+        rc = L.lib().iddgcn_gemm_tn_f32(*args, prec)
     L.check(rc, "gemm_tn")
 
 
 def gemm_tn_batched(entries, slab, precision="exact"):
     """Up to L.TN_BATCH independent C (+)= A^T B, entries = [(A, B, C, accumulate), ...] (fp32, same D), in one
-    launch (iddgcn_gemm_tn_batched_f32, ABI 5; one launch at D = 256 in the split mode); slab holds the
-    partials of all entries."""
+    launch (iddgcn_gemm_tn_batched_f32, ABI 5; one launch at D = 256 in the split and bf16x3 modes); slab holds
+    the partials of all entries.  precision: as gemm_tn."""
+    prec = _tn_prec(precision)
     if not entries:
         return
     if len(entries) > L.TN_BATCH:
@@ -204,8 +216,8 @@ def gemm_tn_batched(entries, slab, precision="exact"):
         _req(C, _F32, (D, D), "C")
         arr[k] = L.TnArgs(M, _ptr(A), _ptr(B), _ptr(C), int(bool(acc)))
     _req(slab, _F32, None, "slab")
-    L.check(L.lib().iddgcn_gemm_tn_batched_f32(_stream(), D, arr, len(entries), _ptr(slab), slab.numel(),
-                                               _prec(precision)), "gemm_tn_batched")
+    L.check(L.lib().iddgcn_gemm_tn_batched_f32(_stream(), D, arr, len(entries), _ptr(slab), slab.numel(), prec),
+            "gemm_tn_batched")
 
 
 def tn_narrow_blocks(M):

@@ -122,12 +122,15 @@ def to_torch_params(params, dtype=torch.float64, requires_grad=True):
             for k, v in params.items()}
 
 
-def train_step_grads(params, pos, neg, adj_coo, num_entities, dtype=torch.float64):
+def train_step_grads(params, pos, neg, adj_coo, num_entities, dtype=torch.float64, scale_entities=None):
     """IDDGCN.py:123-178 up to tape.gradient.
 
     pos/neg are (B,3) int arrays of (head, rel, tail).  Returns
     (unscaled_loss, scores[pos..., neg...], grads dict).  ``relation_weights``
     receive no gradient (they are not used in IDDGCN_Layer.call).
+    ``scale_entities`` (default ``num_entities``): the entity count of the loss
+    scale ×1/num_entities (:168), for a problem relabelled onto a subset of a
+    larger graph's entities (tests/fullsize_grads.py).
     """
     P = to_torch_params(params, dtype)
     adj = adj_to_torch(adj_coo, num_entities, dtype)
@@ -138,7 +141,7 @@ def train_step_grads(params, pos, neg, adj_coo, num_entities, dtype=torch.float6
     y_pred = torch.cat([y_pos, y_neg])
     y_true = torch.cat([torch.ones_like(y_pos), torch.zeros_like(y_neg)])
     loss = keras_bce(y_true, y_pred)
-    scaled = loss * (1.0 / num_entities)                          # :168
+    scaled = loss * (1.0 / (num_entities if scale_entities is None else scale_entities))   # :168
     keys = [k for k in P if P[k].requires_grad]
     grads = torch.autograd.grad(scaled, [P[k] for k in keys])
     return float(loss.detach()), y_pred.detach().numpy(), {k: g.numpy() for k, g in zip(keys, grads)}

@@ -7,7 +7,11 @@ Bars (as tests/test_gpu_model.py):
   * logits: per edge, 1e-4 or 2x that edge's fp32-oracle drift (tests/parity.py);
   * probabilities 1e-4; layer-3 outputs x_h^3, x_t^3 max(1e-4, 2x fp32 drift);
   * a training step is bitwise deterministic; the split-fp16 and exact-f32 GEMM modes agree on every
-    gradient to 2e-4 of its max |g| at a non-saturating init (N(0, 1/D)-scaled weights).
+    gradient to 2e-4 of its max |g| at a non-saturating init (N(0, 1/D)-scaled weights);
+  * the backward at this size against the oracle (tests/fullsize_grads.py): every gradient of a sampled step
+    (random scored edges + complete tail / head segments) run with the FULL adjacency and node tables, exact
+    and bf16x3, vs float64 autograd of the reference formulation (IDDGCN.py:146-174): 2e-4 of max|g| at the
+    mild init, max(2e-4, 2x the fp32 oracle's drift) at the reference init.
 """
 import numpy as np
 import pytest
@@ -18,6 +22,7 @@ from iddgcn_amd.graph import get_adj_mats
 from iddgcn_amd.utils import synthetic_graph
 from oracle.ref_model import forward_detail, init_params
 from oracle.ref_utils import get_adj_coo
+from fullsize_grads import check_sampled_grads, grad_sample
 from parity import assert_logits
 
 pytestmark = pytest.mark.gpu
@@ -48,7 +53,7 @@ def cfg3(cuda):
     rng = np.random.default_rng(0)
     sample = np.sort(rng.choice(len(tri), 10_000, replace=False))
     coo = get_adj_coo(pos, N, R)
-    yield {"eng": eng, "adj": adj, "ed": ed, "tri": tri, "sample": sample, "coo": coo}
+    yield {"eng": eng, "adj": adj, "ed": ed, "tri": tri, "sample": sample, "coo": coo, "pos": pos, "lab": lab}
     del eng, adj, ed
     torch.cuda.empty_cache()
 
@@ -98,3 +103,11 @@ def test_config3_step_deterministic_and_modes_agree(cfg3, cuda):
             scale = np.abs(c[2][k]).max()
             assert np.all(np.isfinite(a[2][k])), (m, k)
             assert np.abs(a[2][k] - c[2][k]).max() <= 2e-4 * scale + 1e-30, (m, k)
+
+
+@pytest.mark.parametrize("init", ["mild", "reference"])
+def test_config3_step_grads_vs_oracle_sample(cfg3, init, cuda):
+    params = mild_params(3) if init == "mild" else init_params(N, R, D, seed=89)
+    idx = grad_sample(cfg3["tri"], seed=3)
+    check_sampled_grads(cfg3["eng"], cfg3["adj"], params, cfg3["pos"], cfg3["tri"][idx], cfg3["lab"][idx],
+                        ("exact", "bf16x3"), cuda, saturating=init == "reference", what=f"config 3 {init}")

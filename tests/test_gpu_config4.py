@@ -10,7 +10,11 @@ Bars (as tests/test_gpu_config3.py):
   * logits: per edge, 1e-4 or 2x that edge's fp32-oracle drift (tests/parity.py); probabilities 1e-4;
     layer-3 rows max(1e-4, 2x the fp32 oracle's drift);
   * a full training step (forward + backward) is bitwise deterministic run to run (exact mode), and the
-    split-fp16 GEMM mode agrees with it on every gradient to 2e-4 of max|g| at a non-saturating init.
+    split-fp16 GEMM mode agrees with it on every gradient to 2e-4 of max|g| at a non-saturating init;
+  * the backward at this size against the oracle (tests/fullsize_grads.py): a sampled step with the FULL
+    20M-entry adjacency and million-row node tables, exact and bf16x3, every gradient vs float64 autograd of
+    the reference formulation (IDDGCN.py:146-174): 2e-4 of max|g| (mild init), max(2e-4, 2x fp32 drift)
+    (reference init).
 """
 import numpy as np
 import pytest
@@ -21,6 +25,7 @@ from iddgcn_amd.graph import get_adj_mats
 from iddgcn_amd.utils import synthetic_graph
 from oracle.ref_model import forward_detail, init_params
 from oracle.ref_utils import get_adj_coo
+from fullsize_grads import check_sampled_grads, grad_sample
 from parity import assert_logits
 
 pytestmark = pytest.mark.gpu
@@ -57,7 +62,8 @@ def cfg4(cuda):
     ed = eng.edges(tri, lab)
     sample = np.sort(np.random.default_rng(0).choice(len(tri), 10_000, replace=False))
     coo = restricted_coo(pos, tri[sample], N, R)
-    yield {"eng": eng, "adj": adj, "ed": ed, "tri": tri[sample], "sample": sample, "coo": coo}
+    yield {"eng": eng, "adj": adj, "ed": ed, "tri": tri[sample], "sample": sample, "coo": coo, "pos": pos,
+           "tri_all": tri, "lab_all": lab}
     eng.release()
     del eng, adj, ed
     torch.cuda.empty_cache()
@@ -111,3 +117,12 @@ def test_config4_step_deterministic_and_modes_agree(cfg4, cuda):
             scale = np.abs(a[2][k]).max()
             assert np.all(np.isfinite(a[2][k])), k
             assert np.abs(c[2][k] - a[2][k]).max() <= 2e-4 * scale + 1e-30, (m, k)
+
+
+@pytest.mark.parametrize("init", ["mild", "reference"])
+def test_config4_step_grads_vs_oracle_sample(cfg4, init, cuda):
+    cfg4["eng"].release()
+    params = mild_params(3) if init == "mild" else init_params(N, R, D, seed=89)
+    idx = grad_sample(cfg4["tri_all"], seed=4)
+    check_sampled_grads(cfg4["eng"], cfg4["adj"], params, cfg4["pos"], cfg4["tri_all"][idx], cfg4["lab_all"][idx],
+                        ("exact", "bf16x3"), cuda, saturating=init == "reference", what=f"config 4 {init}")

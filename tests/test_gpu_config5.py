@@ -12,6 +12,11 @@ D=256, the bf16-feature mode: edge tables x^1..x^3 stored as bf16, edge GEMMs on
     ulp, up to 2^-9, and the next layers carry it on); bars: logits 2e-2 at most and 5e-3 on 99% of the
     edges, probabilities 5e-3.
   * A full training step is finite and bitwise deterministic run to run.
+  * The backward at this size against the oracle (tests/fullsize_grads.py): a sampled step with the FULL
+    40M-entry adjacency and the R = 8 node tables (R·N·D = 2^31 elements: offsets past 32 bits), every gradient
+    vs float64 autograd of the reference formulation (IDDGCN.py:146-174) — with fp32 edge tables in the exact
+    and bf16x3 modes at the fp32 bars (2e-4 of max|g|, loss 1e-5 rel, probabilities 1e-5), and in the
+    bf16-feature mode at its bars (5e-2 of max|g|, loss and probabilities 2e-2: tests/test_gpu_bf16.py).
 """
 import numpy as np
 import pytest
@@ -23,6 +28,7 @@ from iddgcn_amd.sampling import negative_samples
 from iddgcn_amd.utils import synthetic_graph
 from oracle.ref_model import forward_detail
 from oracle.ref_utils import generate_negative_samples_np, get_adj_coo
+from fullsize_grads import check_sampled_grads, grad_sample
 
 pytestmark = pytest.mark.gpu
 N, R, M, D, NEG_EVERY = 1_000_000, 8, 40_000_000, 256, 4
@@ -55,7 +61,7 @@ def cfg5(cuda):
     need = np.unique(np.concatenate([tri[sample, 0], tri[sample, 2]]))
     coo = get_adj_coo(pos[np.isin(pos[:, 0], need)], N, R)
     yield {"eng": eng, "adj": adj, "ed": ed, "tri": tri[sample], "sample": sample, "coo": coo, "src": src,
-           "neg": neg}
+           "neg": neg, "pos": pos, "tri_all": tri, "lab_all": lab}
     eng.release()
     del eng, adj, ed
     torch.cuda.empty_cache()
@@ -104,3 +110,18 @@ def test_config5_step_finite_and_deterministic(cfg5, cuda):
     assert np.isfinite(la) and la > 0
     assert la == lb and np.array_equal(pa, pb) and torch.equal(ga, gb)
     assert bool(torch.isfinite(ga).all())
+
+
+@pytest.mark.parametrize("features", ["f32", "bf16"])
+def test_config5_step_grads_vs_oracle_sample(cfg5, features, cuda):
+    cfg5["eng"].release()
+    idx = grad_sample(cfg5["tri_all"], n_random=3000, n_tail=10, n_head=10, seed=5)
+    tri_s, lab_s = cfg5["tri_all"][idx], cfg5["lab_all"][idx]
+    if features == "f32":
+        eng = Engine(N, R, D, cuda)
+        check_sampled_grads(eng, cfg5["adj"], mild_params(3), cfg5["pos"], tri_s, lab_s, ("exact", "bf16x3"), cuda,
+                            saturating=False, what="config 5 f32")
+        eng.release()
+    else:
+        check_sampled_grads(cfg5["eng"], cfg5["adj"], mild_params(3), cfg5["pos"], tri_s, lab_s, ("exact",), cuda,
+                            saturating=False, what="config 5 bf16", bar=5e-2, loss_bar=2e-2, p_bar=2e-2)

@@ -785,6 +785,36 @@ def test_rowgemm256_many_relations_gather(R, gm, order, cuda):
         assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
 
 
+@pytest.mark.parametrize("gm", ["exact", "split"])
+def test_rowgemm256_many_relations_gather_offsets_past_2e32(gm, cuda):
+    """The slot-major V slabs of the R = 8 gathered forward address relation r's row as r·v_rel_stride + the
+    row offset: with N = 2.2M nodes (R·N·D = 4.5e9 elements > 2^32) the last relations' rows sit past 32-bit
+    element offsets.  Rows gathered from the top of the table (tail runs), vs fp64 (exact 2e-5; split 2x)."""
+    g = torch.Generator(device=cuda).manual_seed(31)
+    D, R, N, M = 256, 8, 2_200_000, 4096
+    assert (R - 1) * N * D > 2 ** 32
+    P = torch.randn(R, N, D, device=cuda, generator=g)
+    t = (N - 1 - torch.sort(torch.randint(0, 600, (M,), device=cuda, generator=g), descending=True)[0]).int()
+    A = torch.rand(M, D, device=cuda, generator=g)
+    S = torch.randn(D, D, device=cuda, generator=g) / 16
+    W = torch.rand(M, R, device=cuda, generator=g)
+    ref = torch.sigmoid(A.double() @ S.double() + sum(W[:, r:r + 1].double() * P[r][t.long()].double()
+                                                      for r in range(R)))
+    kw = dict(coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)
+    errs = {}
+    for mode in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16) if gm == "split" else (L.GEMM_EXACT_F32,):
+        C = torch.empty(M, D, device=cuda)
+        assert ops.rowgemm_kernel_id(A, S, C, precision=mode, **kw) == \
+            300 + 10 * 8 + 2 + (2000 if mode == L.GEMM_SPLIT_F16 else 0)
+        ops.rowgemm(A, S, C, precision=mode, **kw)
+        errs[mode] = _maxrel(C, ref)
+    del P
+    torch.cuda.empty_cache()
+    assert errs[L.GEMM_EXACT_F32] <= 2e-5, errs
+    if gm == "split":
+        assert errs[L.GEMM_SPLIT_F16] <= max(2 * errs[L.GEMM_EXACT_F32], 1e-6), errs
+
+
 @pytest.mark.parametrize("R", [4, 8])
 @pytest.mark.parametrize("gm", ["exact", "split"])
 def test_rowgemm256_rank_update_many_relations(R, gm, cuda):

@@ -4,6 +4,10 @@ The GEMM operand precision is an argument of every GEMM call, not process state:
 modes (exact f32 and split-fp16 operands) running at the same time — each on its own HIP stream, issued from
 its own host thread, so their launches interleave on the host and their kernels overlap on the device —
 each give bitwise the results of the same engine run alone.
+
+The same holds inside one engine: ``Engine.overlap`` runs the layer-2/3 tail reductions of the backward on a side
+stream beside the dS TN and the sigma' GEMM (engine.Engine.backward); four training steps with it are bitwise the
+steps without it, eagerly and through the HIP-graph replay (engine.GraphedTrainStep captures the fork / join).
 """
 import threading
 
@@ -11,7 +15,7 @@ import numpy as np
 import pytest
 import torch
 
-from iddgcn_amd.engine import Engine, FlatParams
+from iddgcn_amd.engine import Engine, FlatParams, GraphedTrainStep, KerasAdam
 from iddgcn_amd.graph import get_adj_mats
 from iddgcn_amd.utils import synthetic_graph
 
@@ -76,3 +80,35 @@ def test_two_engines_two_modes_two_streams_bitwise(cuda):
     for mode in jobs:
         for a, b in zip(alone[mode], results[mode]):
             assert torch.equal(a, b), mode
+
+
+@pytest.mark.parametrize("gemm", ["exact", "bf16x3"])
+def test_overlap_backward_bitwise_eager_and_graphed(gemm, cuda):
+    N, R, D = 4000, 2, 256
+    pos, neg = synthetic_graph(N, R, 40_000, seed=17)
+    tri = np.concatenate([pos, neg])
+    lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+    params = _params(N, R, D, 5)
+
+    def four_steps(overlap, graphed):
+        eng = Engine(N, R, D, cuda, gemm=gemm)
+        eng.overlap = overlap
+        P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
+        P.load(params)
+        opt = KerasAdam(P)
+        adj, ed = eng.adjacency(get_adj_mats(pos, N, R)), eng.edges(tri, lab)
+        eng.train_step(P, G, opt, adj, ed)              # eager first step (creates every workspace)
+        if graphed:
+            step = GraphedTrainStep(eng, P, G, opt, adj, ed, n_steps=3)
+            for _ in range(3):
+                step.replay()
+        else:
+            for _ in range(3):
+                eng.train_step(P, G, opt, adj, ed)
+        torch.cuda.synchronize()
+        return P.buf.clone(), G.buf.clone()
+
+    base = four_steps(False, False)
+    for overlap, graphed in ((True, False), (True, True), (False, True)):
+        got = four_steps(overlap, graphed)
+        assert torch.equal(got[0], base[0]) and torch.equal(got[1], base[1]), (gemm, overlap, graphed)

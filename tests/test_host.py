@@ -30,6 +30,38 @@ def test_library_exports_every_header_symbol():
     assert lib.iddgcn_abi_version() == _lib.ABI_VERSION
 
 
+def test_library_has_no_packed_fp32_valu():
+    """The product library is built without packed-fp32 VALU (iddgcn_amd/csrc/device_flags.txt; DESIGN.md
+    §Determinism): disassemble the gfx950 code object of libiddgcn_hip.so and find no v_pk_fma_f32 / v_pk_mul_f32 /
+    v_pk_add_f32 / v_pk_mov_b32."""
+    import subprocess
+    import tempfile
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-objdump")):
+        pytest.skip("no ROCm llvm tools")
+    asm = ""
+    with tempfile.TemporaryDirectory() as d:
+        fat = os.path.join(d, "fat.bin")
+        subprocess.run([os.path.join(llvm, "llvm-objcopy"), "--dump-section=.hip_fatbin=" + fat, _lib.LIB_PATH,
+                        os.path.join(d, "stripped.so")], check=True, capture_output=True)
+        blob = open(fat, "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts = [m.start() for m in re.finditer(re.escape(magic), blob)]
+        assert len(starts) >= 4, "one offload bundle per source file"
+        for i, a in enumerate(starts):         # one bundle per translation unit, concatenated by the link
+            part, dev = os.path.join(d, f"b{i}.bin"), os.path.join(d, f"b{i}.o")
+            open(part, "wb").write(blob[a:starts[i + 1] if i + 1 < len(starts) else len(blob)])
+            subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + part,
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + dev], check=True,
+                           capture_output=True)
+            asm += subprocess.run([os.path.join(llvm, "llvm-objdump"), "-d", dev], check=True, capture_output=True,
+                                  text=True).stdout
+    assert "radix" in asm and "tail_seg_reduce" in asm     # every translation unit's kernels were disassembled
+    assert asm.count("s_endpgm") > 50          # the kernels really were disassembled
+    bad = sorted(set(re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", asm)))
+    assert not bad, f"packed-fp32 VALU in the product library: {bad}"
+
+
 def test_block_helpers_are_pure_host():
     lib = _lib.lib()
     assert lib.iddgcn_gemm_tn_blocks(4_000_000, 256) == 256

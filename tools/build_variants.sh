@@ -8,7 +8,7 @@ mkdir -p var_so
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
-  ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Xclang -target-feature -Xclang -packed-fp32-ops \
+  ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $(cat iddgcn_amd/csrc/device_flags.txt) \
       -c -I include $flags \
       iddgcn_amd/csrc/iddgcn_hip.hip -o var_so/$name.o && \
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC var_so/$name.o build/graph_build.hip.o \

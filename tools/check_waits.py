@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main(pats, src=None):
     src = src or os.path.join(ROOT, "iddgcn_amd", "csrc", "iddgcn_hip.hip")
     out = os.path.join(tempfile.gettempdir(), "iddgcn_hip_gfx950.s")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I",
+    flags = open(os.path.join(ROOT, "iddgcn_amd", "csrc", "device_flags.txt")).read().split()
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", *flags, "-I",
                     os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
                     src, "-o", out], check=True,
                    stderr=subprocess.DEVNULL)
