@@ -16,6 +16,9 @@ The sample is random scored edges plus every scored edge of a few tails and head
 head segments at the workload's natural lengths, ~100-200 edges at the drug nodes), so the segmented reductions see
 long segments as well as the scattered single edges.
 """
+import json
+import os
+
 import numpy as np
 import torch
 
@@ -38,7 +41,7 @@ def grad_sample(tri, n_random=6000, n_tail=24, n_head=24, seed=0):
 
 def local_oracle(params, pos, tri_s, lab_s, N, R, dtype):
     """train_step_grads on the sampled scored edges, relabelled onto the entities the forward touches.
-    Returns (mean loss, probabilities in tri_s order, grads with E scattered back to N rows)."""
+    Returns (mean loss, probabilities in tri_s order, grads with E scattered back to N rows, those entities)."""
     rows = np.unique(np.concatenate([tri_s[:, 0], tri_s[:, 2]]))
     sub = pos[np.isin(pos[:, 0], rows)]
     for r in range(R):
@@ -55,7 +58,7 @@ def local_oracle(params, pos, tri_s, lab_s, N, R, dtype):
     gE = np.zeros((N, params["E"].shape[1]), dtype=g["E"].dtype)
     gE[ents] = g["E"]
     g["E"] = gE
-    return loss, scores, g
+    return loss, scores, g, ents
 
 
 def engine_grads(eng, P, adj, tri_s, lab_s, gemm, cuda):
@@ -78,9 +81,11 @@ def check_sampled_grads(eng, adj, params, pos, tri_s, lab_s, gemms, cuda, satura
     gradient within ``bar`` (2e-4) of its max |g|.  Reference init (saturating sigmoids): each quantity within max(bar, 2x the fp32 oracle's own
     distance from float64), the bar the fold-0 trained-weights step uses (tests/test_gpu_model.py)."""
     N, R = eng.N, eng.R
-    l64, s64, g64 = local_oracle(params, pos, tri_s, lab_s, N, R, torch.float64)
+    l64, s64, g64, ents = local_oracle(params, pos, tri_s, lab_s, N, R, torch.float64)
     if saturating:
-        l32, s32, g32 = local_oracle(params, pos, tri_s, lab_s, N, R, torch.float32)
+        l32, s32, g32, _ = local_oracle(params, pos, tri_s, lab_s, N, R, torch.float32)
+    outside = np.ones(N, bool)
+    outside[ents] = False
     assert all(np.all(np.isfinite(v)) for v in g64.values())
     P = FlatParams(N, R, eng.D, cuda)
     P.load(params)
@@ -102,9 +107,15 @@ def check_sampled_grads(eng, adj, params, pos, tri_s, lab_s, gemms, cuda, satura
             kb = max(bar, 2 * np.abs(g32[k].astype(np.float64) - ref).max() / scale) if saturating else bar
             rep[k] = (err, kb)
             assert err <= kb, f"{what} {gemm}: grad {k} max err {err:.2e} of max|g| > bar {kb:.2e}"
-        # rows of dE outside the sampled edges' reach are exactly zero
-        touched = np.abs(g64["E"]).max(axis=1) > 0
-        assert not np.any(g["E"][~touched]), f"{what} {gemm}: nonzero dE rows outside the sample's entities"
-        report[gemm] = rep
+        # rows of dE outside the sampled edges' reach (no path from the loss: not a sampled head / tail, not in
+        # their adjacency rows) are exactly zero
+        assert not np.any(g["E"][outside]), f"{what} {gemm}: nonzero dE rows outside the sample's entities"
+        report[gemm] = {"loss_rel_err": lerr, "loss_bar": lbar, "p_err": float(perr), "p_bar": pbar,
+                        "grads": {k: {"err_of_max": float(e), "bar": float(b)} for k, (e, b) in rep.items()}}
     del P
+    log = os.environ.get("IDDGCN_PARITY_LOG")    # e.g. gpurun_out/<tag>/fullsize_grads.jsonl: the measured record
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"what": what, "n_scored": int(len(tri_s)), "n_entities_reached": int(len(ents)),
+                                "modes": report}) + "\n")
     return report

@@ -788,10 +788,10 @@ def test_rowgemm256_many_relations_gather(R, gm, order, cuda):
 @pytest.mark.parametrize("gm", ["exact", "split"])
 def test_rowgemm256_many_relations_gather_offsets_past_2e32(gm, cuda):
     """The slot-major V slabs of the R = 8 gathered forward address relation r's row as r·v_rel_stride + the
-    row offset: with N = 2.2M nodes (R·N·D = 4.5e9 elements > 2^32) the last relations' rows sit past 32-bit
+    row offset: with N = 2.5M nodes ((R-1)·N·D = 4.5e9 elements > 2^32) the last relation's rows sit past 32-bit
     element offsets.  Rows gathered from the top of the table (tail runs), vs fp64 (exact 2e-5; split 2x)."""
     g = torch.Generator(device=cuda).manual_seed(31)
-    D, R, N, M = 256, 8, 2_200_000, 4096
+    D, R, N, M = 256, 8, 2_500_000, 4096
     assert (R - 1) * N * D > 2 ** 32
     P = torch.randn(R, N, D, device=cuda, generator=g)
     t = (N - 1 - torch.sort(torch.randint(0, 600, (M,), device=cuda, generator=g), descending=True)[0]).int()

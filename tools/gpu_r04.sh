@@ -11,6 +11,7 @@ TAG=$1; WHAT=$2; shift 2
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+export IDDGCN_PARITY_LOG=$PWD/$OUT/fullsize_grads.jsonl
 rc=0
 if [ $# -gt 0 ]; then
   timeout -k 10 1000 python -u -m pytest "$@" -m gpu -v -rf --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
