@@ -2095,6 +2095,520 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
 #undef B3_MAIN_LOOP
 }
 
+// ---- row GEMM, bf16x3 operands on 32 x 32 x 16 MFMAs (round 4): C = epilogue(A B) over T rows -------------
+// One wave per SIMD (256-thread workgroups), 32 output columns per wave.  The weight's three bf16 planes of
+// those columns are 192 registers per lane, which the 512-entry register file of a lone wave holds beside two
+// accumulator pairs; a workgroup owns one 128-column half, the two halves of a row range run 8 workgroups
+// apart (workgroup b -> XCD b mod 8: the same XCD, so the second read of an A tile is an L2 hit).
+//   * v_mfma_f32_32x32x16_bf16 with the weight planes as operand A (32 columns x 16 k) and the A tile as
+//     operand B (16 k x 32 rows): lane l ends with edge row l&31, columns c0 + 8q + 4(l>>5) + {0..3}, q = 0..3.
+//     The MFMA holds the SIMD's vector issue for 8 of its 32 cycles (the 16x16x32 form of the round-3 kernel:
+//     8 of 16), so 3/4 of the MFMA phase's issue slots are left to the same wave's operand conversion,
+//     epilogue and DMA issue — the round-3 kernel was vector-issue bound (2 waves x (96 MFMA x 8 + 241 VALU x 4)
+//     cycles per SIMD per tile against 3072 MFMA cycles).
+//   * Each wave's fragment reads serve 32 columns: 192 KB of LDS reads per 32-row tile per CU instead of 384.
+//   * A rows (fp32) arrive by LDS-DMA into 1552-B row slots (388 dwords = 4 mod 64 banks: the 16 rows of every
+//     16-lane group of a fragment ds_read_b128 are conflict-free) and each wave converts 8 of the tile's 32 rows
+//     in place to the three planes, one row per k-step in the second half of the MFMA phase.
+//   * Iteration t: the slab DMAs of tile t (the tile's distinct gathered rows, the per-row coefficients, the
+//     sigma' / old-C rows: double-buffered per wave), the index DMA of t+1, the A DMAs of t+1 and an L2
+//     prefetch of A(t+1+PF); the epilogue of t-1 beside k-steps 0..3 of MFMA(t); the conversion of A(t+1)
+//     beside k-steps 8..15.  One barrier per tile.  Every vmcnt wait is an exact compile-time count: the
+//     conversion of row j of A(t+1) waits for everything but the ops issued after it (the younger A rows, the
+//     prefetch, the epilogue's 4 stores), which also covers the slab and index DMAs of the iteration.
+// Epilogue forms (template ACT): 0 none, 1 sigmoid, 2 sigma' (AUX: the aux rows), 3 accumulate (AUX: old C).
+namespace rw3 {
+constexpr int D = 256, NW = 4, TR = 32, CWG = 128, CWV = 32;
+constexpr int PITCH = 1552;                 // A row slot: three 512-B planes + 16 B
+constexpr int ABYTES = TR * PITCH;          // 49,664 B per A buffer (two buffers)
+constexpr int RPW = TR / NW;                // A rows each wave stages and converts
+constexpr int CAP = 16;                     // V-slab slots (distinct gathered rows) per relation; more: from L2
+constexpr int VSLAB = CAP * CWV;            // floats of a V slab [16 slots][32 columns]
+constexpr int XSLAB = TR * CWV;             // floats of an aux slab [32 rows][32 columns]
+constexpr int PF = 2;                       // L2 prefetch distance beyond the tile being DMA'd
+}  // namespace rw3
+// float offset of (slot, 16-B column group g) in a [slots][32] slab: groups XOR ((slot >> 1) & 7), so the
+// epilogue's ds_read_b128 (slot of row l&31, group 2q + (l>>5)) is conflict-free in each 16-lane group for any
+// 16 rows of distinct slot & 15 (and broadcast for equal slots)
+__device__ __forceinline__ int slab32_off(int slot, int g) { return slot * 32 + 4 * (g ^ ((slot >> 1) & 7)); }
+// explicit-address-space loads: an LDS read and a global read that the compiler may not merge into one FLAT load
+// (a FLAT op counts in both vmcnt and lgkmcnt, and its wait drains every DMA in flight)
+__device__ __forceinline__ f32x4 ld4_lds(const float* p) {
+    return *(const __attribute__((address_space(3))) f32x4*)(p);
+}
+__device__ __forceinline__ float ld_lds(const float* p) { return *(const __attribute__((address_space(3))) float*)(p); }
+__device__ __forceinline__ f32x4 ld4_gbl(const float* p) {
+    return *(const __attribute__((address_space(1))) f32x4*)(p);
+}
+// s_waitcnt vmcnt(N) for a compile-time N
+template <int N>
+__device__ __forceinline__ void wait_vm_c() {
+    static_assert(N >= 0 && N <= 63, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NV, bool AUX, bool BC, int ACT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void rowgemm256_b3w_kernel(RowGemmP p, int n_ranges) {
+    using namespace rw3;
+    static_assert(NV >= 0 && NV <= 2 && !(NV > 0 && (AUX || BC)), "b3w: gathered forward (NV = R = 1, 2), sigma' / accumulate (AUX), plain");
+    static_assert(!BC || NV == 0, "BC: one broadcast V row per relation (R <= 2), e.g. dz W_a^T");
+    static_assert(AUX == (ACT >= 2), "ACT 2 (sigma') and 3 (accumulate) read the aux slab");
+    // per wave (floats): two slab sets {NV V slabs, the aux slab, coefficients [32][R]}, idx [64], cmp [32],
+    // prefetch landing [256] (never read)
+    constexpr int SET = NV * VSLAB + (AUX ? XSLAB : 0) + 64;
+    constexpr int WF = 2 * SET + 64 + 32 + 256;
+    constexpr int LDSB = 2 * ABYTES + NW * WF * 4;
+    static_assert(LDSB <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char lds[LDSB];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int e = lane & 31, h = lane >> 5;
+    const int bx = blockIdx.x;
+    const int half = (bx >> 3) & 1;
+    const int range = ((bx >> 4) << 3) | (bx & 7);
+    if (range >= n_ranges) return;
+    const int c0 = half * CWG + wave * CWV;
+    float* wbase = reinterpret_cast<float*>(lds + 2 * ABYTES) + wave * WF;
+    int* idxw = reinterpret_cast<int*>(wbase + 2 * SET);
+    int* cmpw = idxw + 64;
+    float* pfw = reinterpret_cast<float*>(cmpw + 32);
+
+    const long long ntiles = ((long long)p.M + TR - 1) / TR;
+    const long long t_beg = (long long)range * p.tiles_per_block;
+    long long t_end = t_beg + p.tiles_per_block;
+    if (t_end > ntiles) t_end = ntiles;
+    if (t_beg >= t_end) return;
+    const long long Mlast = (long long)p.M - 1;
+    auto clampe = [&](long long x) __attribute__((always_inline)) { return x > Mlast ? Mlast : x; };
+    auto clampt = [&](long long t) __attribute__((always_inline)) { return t < t_end ? t : t_end - 1; };
+
+    // weight planes: k-step s (16 k), lane l: column c0 + (l&31), k = 16 s + 8 (l>>5) + j
+    bf16x8 w0[16], w1[16], w2[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * s + 8 * h + j;
+            const float wv = p.b_trans ? p.B[(c0 + e) * D + k] : p.B[k * D + c0 + e];
+            __bf16 a, b, c;
+            split3(wv, a, b, c);
+            w0[s][j] = a;
+            w1[s][j] = b;
+            w2[s][j] = c;
+        }
+    // BC: the broadcast V rows (v_row_stride 0: the same R <= 2 rows for every output row), this lane's columns
+    f32x4 vb[2][4];
+    if constexpr (BC) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                vb[r][q] = r < p.R ? ld4(p.V + r * p.v_rel_stride + c0 + 8 * q + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    // ---- DMA issue sites (each returns its count of vector-memory ops) ----
+    auto dma_idx = [&](long long t) __attribute__((always_inline)) -> int {
+        if constexpr (NV == 0) {
+            return 0;
+        } else {
+            // identity rows (v_idx NULL): a harmless 4-B read keeps the count compile-time
+            const int* src = p.v_idx ? p.v_idx + clampe(t * TR + e) : reinterpret_cast<const int*>(p.A);
+            __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)idxw, 4, 0, 0);
+            return 1;
+        }
+    };
+    auto dma_A = [&](long long t, int bb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int r = wave * RPW + j;
+            const float* src = p.A + clampe(t * TR + r) * D + lane * 4;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(lds + bb * ABYTES + r * PITCH), 16, 0, 0);
+        }
+    };
+    auto dma_A1 = [&](long long t, int bb, int j) __attribute__((always_inline)) {
+        const int r = wave * RPW + j;
+        const float* src = p.A + clampe(t * TR + r) * D + lane * 4;
+        __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(lds + bb * ABYTES + r * PITCH), 16, 0, 0);
+    };
+    // L2 prefetch of this wave's 8 A rows of tile t: a 16-B read per 128-B line into a scratch KiB of LDS
+    auto prefetch = [&](long long t) __attribute__((always_inline)) {
+        const float* src = p.A + clampe(clampt(t) * TR + wave * RPW + (lane >> 3)) * D + (lane & 7) * 32;
+        __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)pfw, 16, 0, 0);
+    };
+    // slabs of tile t into set `set`: the tile's distinct V rows (runs of equal v_idx: tail-sorted edges give 1-3
+    // per tile; identity rows give 32) into slots 0..min(u, CAP)-1; the slot and V row of this lane's row e
+    auto dma_slabs = [&](long long t, int set, int& vsl, int& vrow) __attribute__((always_inline)) {
+        float* sb = wbase + set * SET;
+        if constexpr (NV > 0) {
+            int vi = 0;
+            bool start = false;
+            if (lane < 32) {
+                const long long ee = clampe(t * TR + lane);
+                vi = p.v_idx ? ((const __attribute__((address_space(3))) int*)idxw)[lane] : (int)ee;
+                const int prev = p.v_idx ? ((const __attribute__((address_space(3))) int*)idxw)[lane > 0 ? lane - 1 : 0]
+                                         : (int)ee - 1;
+                start = lane == 0 || vi != prev;
+            }
+            const unsigned long long m = __ballot(start);
+            const int u = __popcll(m);
+            vsl = __popcll(m & ((2ull << e) - 1)) - 1;
+            if (start) cmpw[__popcll(m & ((2ull << lane) - 1)) - 1] = vi;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const __attribute__((address_space(3))) int* cmpl = (const __attribute__((address_space(3))) int*)cmpw;
+            vrow = cmpl[vsl];
+            const int un = u < CAP ? u : CAP;
+            for (int kb = 0; kb < un; kb += 8) {
+                const int slot = kb + (lane >> 3);
+                const int g = (lane & 7) ^ ((slot >> 1) & 7);
+                const long long v = cmpl[slot < u ? slot : u - 1];
+#pragma unroll
+                for (int r = 0; r < NV; ++r) {
+                    const float* src = p.V + r * p.v_rel_stride + v * D + c0 + 4 * g;
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(sb + r * VSLAB + kb * 32), 16, 0, 0);
+                }
+            }
+            // 32 x R per-edge coefficients, one 4-B DMA per lane (lanes past 32 R re-read the last value)
+            const long long last = (long long)p.M * NV - 1;
+            long long ci = t * TR * NV + lane;
+            if (ci > last) ci = last;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + ci), (lds_vptr)(sb + NV * VSLAB), 4, 0, 0);
+        }
+        if constexpr (BC) {
+            const long long last = (long long)p.M * p.R - 1;
+            long long ci = t * TR * p.R + lane;
+            if (ci > last) ci = last;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + ci), (lds_vptr)(sb + (AUX ? XSLAB : 0)), 4, 0, 0);
+        }
+        if constexpr (AUX) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int slot = 8 * k + (lane >> 3);
+                const int g = (lane & 7) ^ ((slot >> 1) & 7);
+                const float* src = p.aux + clampe(t * TR + slot) * D + c0 + 4 * g;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(sb + NV * VSLAB + k * 256), 16, 0, 0);
+            }
+        }
+    };
+    // The epilogue of tile t, quarter q (columns c0 + 8q + 4(l>>5) .. +3), in two halves one k-step apart: epi_load
+    // reads the accumulator pair and the LDS operands, epi_fin (a k-step later, the reads landed) combines, applies
+    // the activation and stores.  Rows whose gathered V row is past the slab's CAP slots take epi_fix afterwards.
+    struct EpiIn {
+        f32x4 v, x;
+        f32x4 sv[NV > 0 ? NV : 1];
+        float cf[(NV > 0 || BC) ? 2 : 1];
+    };
+    auto epi_load = [&](int set, int vsl, const f32x16& hi, const f32x16& lo, int q, EpiIn& in)
+        __attribute__((always_inline)) {
+        const float* sb = wbase + set * SET;
+        const int g = 2 * q + h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) in.v[i] = hi[4 * q + i] + lo[4 * q + i];
+        if constexpr (NV > 0) {
+#pragma unroll
+            for (int r = 0; r < NV; ++r) {
+                in.cf[r] = ld_lds(sb + NV * VSLAB + e * NV + r);
+                in.sv[r] = ld4_lds(sb + r * VSLAB + slab32_off(vsl < CAP ? vsl : CAP - 1, g));
+            }
+        }
+        if constexpr (BC) {
+            const float* cb = sb + (AUX ? XSLAB : 0) + e * p.R;
+            in.cf[0] = ld_lds(cb);
+            in.cf[1] = p.R > 1 ? ld_lds(cb + 1) : 0.f;
+        }
+        if constexpr (ACT >= 2) in.x = ld4_lds(sb + NV * VSLAB + slab32_off(e, g));
+    };
+    auto epi_act_store = [&](long long t, int q, f32x4 v, const f32x4& x) __attribute__((always_inline)) {
+        if constexpr (ACT == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = sigmoid_fast(v[i]);
+        } else if constexpr (ACT == 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = v[i] * (x[i] * (1.0f - x[i]));
+        } else if constexpr (ACT == 3) {
+            v += x;
+        }
+        const long long row0 = t * TR;
+        const long long left = (long long)p.M - row0;
+        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
+        const __amdgpu_buffer_rsrc_t rc =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(p.C) + row0 * D * 4, (short)0, nbytes, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rc, (e * D + c0 + 8 * q + 4 * h) * 4, 0, 0);
+    };
+    auto epi_fin = [&](long long t, int q, const EpiIn& in) __attribute__((always_inline)) {
+        f32x4 v = in.v;
+        if constexpr (NV > 0) {
+#pragma unroll
+            for (int r = 0; r < NV; ++r)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = fmaf(in.cf[r], in.sv[r][i], v[i]);
+        }
+        if constexpr (BC) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = fmaf(in.cf[r], vb[r][q][i], v[i]);
+        }
+        epi_act_store(t, q, v, in.x);
+    };
+    // rows past the CAP slab slots (more than CAP distinct gathered rows in the tile: identity or random rows):
+    // recompute their four quarters with the V rows read from L2 and store again (same lane, same address: the
+    // later store wins).  Tail-sorted edge tiles never take it.
+    auto epi_fix = [&](long long t, int set, int vsl, int vrow, const f32x16& hi, const f32x16& lo)
+        __attribute__((always_inline)) {
+        if constexpr (NV > 0) {
+            if (__ballot(vsl >= CAP) == 0) return;
+            if (vsl >= CAP) {
+                const float* sb = wbase + set * SET;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int g = 2 * q + h;
+                    f32x4 v;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[i] = hi[4 * q + i] + lo[4 * q + i];
+#pragma unroll
+                    for (int r = 0; r < NV; ++r) {
+                        const float cf = ld_lds(sb + NV * VSLAB + e * NV + r);
+                        const f32x4 sv = ld4_gbl(p.V + r * p.v_rel_stride + (long long)vrow * D + c0 + 4 * g);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) v[i] = fmaf(cf, sv[i], v[i]);
+                    }
+                    epi_act_store(t, q, v, f32x4{0.f, 0.f, 0.f, 0.f});
+                }
+            }
+        }
+    };
+    // the A-row conversion, split so that the fp32 row is read one k-step before it is converted and written
+    auto conv_read = [&](int bb, int j) __attribute__((always_inline)) -> f32x4 {
+        return ld4_lds(reinterpret_cast<const float*>(lds + bb * ABYTES + (wave * RPW + j) * PITCH) + lane * 4);
+    };
+    auto conv_write = [&](int bb, int j, const f32x4& x) __attribute__((always_inline)) {
+        typedef __attribute__((address_space(3))) bf16x4* lbf4;
+        char* row = lds + bb * ABYTES + (wave * RPW + j) * PITCH;
+        bf16x4 p0, p1, p2;
+        split3x4(x, p0, p1, p2);
+        *(lbf4)(row + lane * 8) = p0;
+        *(lbf4)(row + 512 + lane * 8) = p1;
+        *(lbf4)(row + 1024 + lane * 8) = p2;
+    };
+
+    const unsigned ab0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds + e * PITCH + 16 * h;
+#define W3_LOAD(S, B)                                                                                     \
+    asm volatile("ds_read_b128 %0, %3 offset:%4\n\tds_read_b128 %1, %3 offset:%5\n\tds_read_b128 %2, %3 offset:%6" \
+                 : "=v"(fr[B][0]), "=v"(fr[B][1]), "=v"(fr[B][2])                                          \
+                 : "v"(ab), "i"(32 * (S)), "i"(32 * (S) + 512), "i"(32 * (S) + 1024)                       \
+                 : "memory")
+    constexpr int NIDX = NV > 0 ? 1 : 0;
+
+    // One tile: MFMA(t) on buffer bb into (hi, lo); beside it the epilogue of t-1 (from (phi, plo), slab set bb^1),
+    // the slab DMAs of t (set bb), the index DMA of t+1, the A DMAs of t+1 into buffer bb^1 and their conversion.
+    // Program order of the vector-memory ops: slabs(t) | A(t+1) rows 0-3 [+ store q0] (k-step 0) | rows 4-7 [+ store
+    // q0] (1) | idx(t+1), prefetch, stores q1..q3 (2..4).  Before the conversion reads (k-step 7) every A row must
+    // have landed: only the ops of k-steps 2..4 are surely younger (idx, prefetch, 3 stores), so vmcnt(NIDX + 1 +
+    // 3); that wait also covers slabs(t) and idx(t+1)'s predecessor for the next iteration.
+    auto tile = [&](auto first_c, long long t, int bb, f32x16& hi, f32x16& lo, const f32x16& phi, const f32x16& plo,
+                    int& vsl_cur, int& vrow_cur, int vsl_prev, int vrow_prev) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(first_c)::value;
+        constexpr int WAIT_A = NIDX + 1 + (FIRST ? 0 : 3);
+        const int set = bb;
+        dma_slabs(t, set, vsl_cur, vrow_cur);
+        const unsigned ab = ab0 + bb * ABYTES;
+        u32x4 fr[2][3];
+        EpiIn ein = {};
+        f32x4 xr = {0.f, 0.f, 0.f, 0.f};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        W3_LOAD(0, 0);
+        // conversion state of the A row being converted (read one k-step earlier), in four VALU chunks + writes
+        unsigned cp0a = 0, cp1a = 0, cp2a = 0, cp0b = 0, cp1b = 0, cp2b = 0;
+        float cr0 = 0.f, cr1 = 0.f, cr2 = 0.f, cr3 = 0.f;
+        f32x4 ev = {0.f, 0.f, 0.f, 0.f};
+        // work placed after MFMA m (0..5) of k-step s; every chunk ends in an empty-asm fence on what it produced,
+        // and every MFMA result passes one: the fences are ordered volatile asm, so each chunk stays in its gap
+        auto slot = [&](int s, int m) __attribute__((always_inline)) {
+#ifndef W3_ABL
+#define W3_ABL 0
+#endif
+            if (!(W3_ABL & 4) && s == 0 && m < 4) dma_A1(clampt(t + 1), bb ^ 1, m);
+            if (!(W3_ABL & 4) && s == 1 && m < 4) dma_A1(clampt(t + 1), bb ^ 1, m + 4);
+            if (s == 2 && m == 0) dma_idx(t + 1);
+            if (s == 2 && m == 1) prefetch(t + 1 + PF);
+            if constexpr (!FIRST && !(W3_ABL & 8)) {
+                // epilogue of t-1: quarter q = s - 1 finishes in k-step s (1..4), quarter s is loaded in k-step s (0..3)
+                if (s >= 1 && s <= 4) {
+                    const int q = s - 1;
+                    if (m == 0) {
+                        ev = ein.v;
+                        if constexpr (NV > 0) {
+#pragma unroll
+                            for (int r = 0; r < NV; ++r)
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) ev[i] = fmaf(ein.cf[r], ein.sv[r][i], ev[i]);
+                        }
+                        if constexpr (BC) {
+#pragma unroll
+                            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) ev[i] = fmaf(ein.cf[r], vb[r][q][i], ev[i]);
+                        }
+                        asm volatile("" : "+v"(ev));
+                    } else if (m == 1 || m == 2) {
+#pragma unroll
+                        for (int i = 2 * (m - 1); i < 2 * m; ++i) {
+                            if constexpr (ACT == 1) ev[i] = sigmoid_fast(ev[i]);
+                            else if constexpr (ACT == 2) ev[i] = ev[i] * (ein.x[i] * (1.0f - ein.x[i]));
+                            else if constexpr (ACT == 3) ev[i] += ein.x[i];
+                        }
+                        asm volatile("" : "+v"(ev));
+                    } else if (m == 3) {
+                        const long long row0 = (t - 1) * TR;
+                        const long long left = (long long)p.M - row0;
+                        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
+                        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+                            reinterpret_cast<char*>(p.C) + row0 * D * 4, (short)0, nbytes, 0x00020000);
+                        __builtin_amdgcn_raw_buffer_store_b128(ev, rc, (e * D + c0 + 8 * q + 4 * h) * 4, 0, 0);
+                    }
+                }
+                if (s <= 3 && m == 4) epi_load(bb ^ 1, vsl_prev, phi, plo, s, ein);
+            }
+            if (s == 7 && m == 0) {
+                wait_vm_c<WAIT_A>();
+                xr = conv_read(bb ^ 1, 0);
+            }
+            if (s >= 8 && !(W3_ABL & 2)) {
+                if (m == 0) {          // pair (x0, x1): b0 and the first remainder
+                    cp0a = cvt_pk_bf16(xr[0], xr[1]);
+                    cr0 = xr[0] - __builtin_bit_cast(float, cp0a << 16);
+                    cr1 = xr[1] - __builtin_bit_cast(float, cp0a & 0xffff0000u);
+                    asm volatile("" : "+v"(cp0a), "+v"(cr0), "+v"(cr1));
+                } else if (m == 1) {   // pair (x0, x1): b1, b2
+                    cp1a = cvt_pk_bf16(cr0, cr1);
+                    const float s0 = cr0 - __builtin_bit_cast(float, cp1a << 16);
+                    const float s1 = cr1 - __builtin_bit_cast(float, cp1a & 0xffff0000u);
+                    cp2a = cvt_pk_bf16(s0, s1);
+                    asm volatile("" : "+v"(cp1a), "+v"(cp2a));
+                } else if (m == 2) {   // pair (x2, x3)
+                    cp0b = cvt_pk_bf16(xr[2], xr[3]);
+                    cr2 = xr[2] - __builtin_bit_cast(float, cp0b << 16);
+                    cr3 = xr[3] - __builtin_bit_cast(float, cp0b & 0xffff0000u);
+                    asm volatile("" : "+v"(cp0b), "+v"(cr2), "+v"(cr3));
+                } else if (m == 3) {
+                    cp1b = cvt_pk_bf16(cr2, cr3);
+                    const float s2 = cr2 - __builtin_bit_cast(float, cp1b << 16);
+                    const float s3 = cr3 - __builtin_bit_cast(float, cp1b & 0xffff0000u);
+                    cp2b = cvt_pk_bf16(s2, s3);
+                    asm volatile("" : "+v"(cp1b), "+v"(cp2b));
+                } else if (m == 4) {   // the three planes of row s - 8, then the fp32 read of the next row
+                    typedef __attribute__((address_space(3))) u32x2* lu2;
+                    char* row = lds + (bb ^ 1) * ABYTES + (wave * RPW + (s - 8)) * PITCH + lane * 8;
+                    *(lu2)(row) = u32x2{cp0a, cp0b};
+                    *(lu2)(row + 512) = u32x2{cp1a, cp1b};
+                    *(lu2)(row + 1024) = u32x2{cp2a, cp2b};
+                    if (s < 15) xr = conv_read(bb ^ 1, s - 7);
+                }
+            }
+        };
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int S = s & 1;
+            if (W3_ABL & 16) asm volatile("" : "+v"(fr[S][0]), "+v"(fr[S][1]), "+v"(fr[S][2])::"memory");
+            else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fr[S][0]), "+v"(fr[S][1]), "+v"(fr[S][2])::"memory");
+            // the LDS values read in the previous k-step and consumed in this one landed with the wait above: the
+            // empty asm "redefines" them, so the compiler sees no pending read (and places no wait) at their use
+            if (s >= 8) asm volatile("" : "+v"(xr));
+            if constexpr (!FIRST) {
+                if (s >= 1 && s <= 4) {
+                    asm volatile("" : "+v"(ein.v), "+v"(ein.x));
+#pragma unroll
+                    for (int r = 0; r < (NV > 0 ? NV : 1); ++r) asm volatile("" : "+v"(ein.sv[r]));
+#pragma unroll
+                    for (int r = 0; r < ((NV > 0 || BC) ? 2 : 1); ++r) asm volatile("" : "+v"(ein.cf[r]));
+                }
+            }
+            if (s + 1 < 16) {
+                switch (s) {
+                    case 0: W3_LOAD(1, 1); break;
+                    case 1: W3_LOAD(2, 0); break;
+                    case 2: W3_LOAD(3, 1); break;
+                    case 3: W3_LOAD(4, 0); break;
+                    case 4: W3_LOAD(5, 1); break;
+                    case 5: W3_LOAD(6, 0); break;
+                    case 6: W3_LOAD(7, 1); break;
+                    case 7: W3_LOAD(8, 0); break;
+                    case 8: W3_LOAD(9, 1); break;
+                    case 9: W3_LOAD(10, 0); break;
+                    case 10: W3_LOAD(11, 1); break;
+                    case 11: W3_LOAD(12, 0); break;
+                    case 12: W3_LOAD(13, 1); break;
+                    case 13: W3_LOAD(14, 0); break;
+                    default: W3_LOAD(15, 1); break;
+                }
+            }
+            const bf16x8 x0 = __builtin_bit_cast(bf16x8, fr[S][0]), x1 = __builtin_bit_cast(bf16x8, fr[S][1]),
+                         x2 = __builtin_bit_cast(bf16x8, fr[S][2]);
+            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[s], x2, s == 0 ? f32x16{} : lo, 0, 0, 0);
+            asm volatile("" : "+a"(lo));
+            slot(s, 0);
+            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2[s], x0, lo, 0, 0, 0);
+            asm volatile("" : "+a"(lo));
+            slot(s, 1);
+            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], x1, lo, 0, 0, 0);
+            asm volatile("" : "+a"(lo));
+            slot(s, 2);
+            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[s], x1, lo, 0, 0, 0);
+            asm volatile("" : "+a"(lo));
+            slot(s, 3);
+            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], x0, lo, 0, 0, 0);
+            asm volatile("" : "+a"(lo));
+            slot(s, 4);
+            if (!(W3_ABL & 1)) hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[s], x0, s == 0 ? f32x16{} : hi, 0, 0, 0);
+            asm volatile("" : "+a"(hi));
+            slot(s, 5);
+        }
+        if constexpr (!FIRST) epi_fix(t - 1, bb ^ 1, vsl_prev, vrow_prev, phi, plo);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    // prologue: indices and A of t_beg; A converted
+    dma_idx(t_beg);
+    dma_A(t_beg, 0);
+    for (int k = 1; k <= PF; ++k) prefetch(t_beg + k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) row_to_planes3(lds + (wave * RPW + j) * PITCH, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    f32x16 hA, lA, hB, lB;
+    int vsA = 0, vrA = 0, vsB = 0, vrB = 0;
+    tile(std::integral_constant<bool, true>{}, t_beg, 0, hA, lA, hB, lB, vsA, vrA, vsB, vrB);
+    long long t = t_beg + 1;
+    for (; t + 1 < t_end; t += 2) {
+        tile(std::integral_constant<bool, false>{}, t, 1, hB, lB, hA, lA, vsB, vrB, vsA, vrA);
+        tile(std::integral_constant<bool, false>{}, t + 1, 0, hA, lA, hB, lB, vsA, vrA, vsB, vrB);
+    }
+    // the last tile's epilogue (its slabs: vmcnt(0)); the MFMA results: the waits below are no MFMA interlock,
+    // the s_nop pad is (32x32x16 result -> VALU read)
+    auto last_epi = [&](long long tl, int set, int vsl, int vrow, const f32x16& hi, const f32x16& lo)
+        __attribute__((always_inline)) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            EpiIn in;
+            epi_load(set, vsl, hi, lo, q, in);
+            epi_fin(tl, q, in);
+        }
+        epi_fix(tl, set, vsl, vrow, hi, lo);
+    };
+    if (t < t_end) {
+        tile(std::integral_constant<bool, false>{}, t, 1, hB, lB, hA, lA, vsB, vrB, vsA, vrA);
+        last_epi(t, 1, vsB, vrB, hB, lB);
+    } else {
+        last_epi(t - 1, (int)((t - 1 - t_beg) & 1), vsA, vrA, hA, lA);
+    }
+#undef W3_LOAD
+}
+
 // ---- TN reduction GEMM, bf16x3 operands: C = A^T B over M rows, partial per workgroup --------------------
 // Wave w owns output rows 32w..32w+31 (columns of A) x all 256 columns (8 accumulator tiles, 128 VGPRs).
 // 16-row tiles of A and B (one v_mfma_f32_32x32x16_bf16 k-step) arrive by LDS-DMA into 1600-B row slots,
@@ -3426,16 +3940,32 @@ bool b3_select(const RowGemmP& p, int& nv, bool& aux, bool& bc) {
     aux = p.act == IDDGCN_ACT_DSIGMOID || p.accumulate;
     return true;
 }
-// ~128 row ranges (a multiple of 8) x 2 column halves: one 138-KB workgroup per CU, every one resident
+// ~128 row ranges (a multiple of 8) x 2 column halves: one workgroup per CU, every one resident
+#ifndef B3W
+#define B3W 1
+#endif
 void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux, bool bc) {
     const long long nt = ((long long)p.M + rb3::TR - 1) / rb3::TR;
     long long nr = nt < 128 ? nt : 128;
     p.tiles_per_block = (int)((nt + nr - 1) / nr);
     nr = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
     nr = (nr + 7) / 8 * 8;
-    const dim3 g((unsigned)(2 * nr)), blk(512);
     const int n_ranges = (int)nr;
     if (p.accumulate) p.aux = p.C;
+    if (B3W) {
+        const dim3 g((unsigned)(2 * nr)), blk(256);
+        const bool sig = p.act == IDDGCN_ACT_SIGMOID;
+#define W3K(NV, AX, BCC, ACT) hipLaunchKernelGGL((rowgemm256_b3w_kernel<NV, AX, BCC, ACT>), g, blk, 0, st, p, n_ranges)
+        if (bc && aux) W3K(0, true, true, 2);
+        else if (bc) W3K(0, false, true, 0);
+        else if (nv == 1) { if (sig) W3K(1, false, false, 1); else W3K(1, false, false, 0); }
+        else if (nv == 2) { if (sig) W3K(2, false, false, 1); else W3K(2, false, false, 0); }
+        else if (aux) { if (p.accumulate) W3K(0, true, false, 3); else W3K(0, true, false, 2); }
+        else { if (sig) W3K(0, false, false, 1); else W3K(0, false, false, 0); }
+#undef W3K
+        return;
+    }
+    const dim3 g((unsigned)(2 * nr)), blk(512);
     if (bc && aux) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, true, true>), g, blk, 0, st, p, n_ranges);
     else if (bc) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, false, true>), g, blk, 0, st, p, n_ranges);
     else if (nv == 1) hipLaunchKernelGGL((rowgemm256_b3_kernel<1, false>), g, blk, 0, st, p, n_ranges);

@@ -94,21 +94,26 @@ def _glorot_uniform(rng, shape):
     return rng.uniform(-lim, lim, shape)
 
 
-# Initialisation schemes.  TF's bits cannot be replayed, but the reference's seeding STRUCTURE can:
-# Keras 2.7's seeded initialisers (RandomNormal / RandomUniform with seed=...) run stateless ops keyed on
-# [seed, 0], so every seeded call draws the SAME stream, element i depending only on (seed, i).  All three
-# IDDGCN_Layers get seed=SEED (IDDGCN.py:238-274), hence in the reference
-#   relation_kernels = N[:R*D*D],  self_kernel = N[:D*D] (== relation_kernels[0]),  DistMult rel = N[:R*D]
-# for one normal stream N, identical in the three layers, while the unseeded initialisers (W_alpha
-# glorot_uniform, relation_weights 'uniform') draw fresh values per layer from the global seed.
-#   "stateless" (default): that structure, numpy's seeded streams standing in for Philox;
-#   "independent": every weight an independent draw from the layer's seeded generator (round 1).
-INIT_SCHEMES = ("stateless", "independent")
+# Initialisation schemes.
+#   "tf27" (default): TensorFlow 2.7 / Keras 2.7's own draws, replayed (iddgcn_amd/tf_random.py): after
+#       tf.random.set_seed(seed) (IDDGCN.py:292) the seeded initialisers (RandomUniform / RandomNormal with
+#       seed=SEED) are stateful Philox ops keyed (SEED, SEED) whose cached kernel continues its stream from call to
+#       call, and the unseeded ones ('uniform' relation_weights, glorot_uniform W_alpha) take op seeds from the
+#       eager context's Random(SEED).  Bit for bit the reference's initial relation_weights (all 5 bundled folds)
+#       and the untouched entity rows (folds 0, 1, 4); the Box-Muller normals go through the host libm as TF's
+#       CPU kernel does (their bits are not pinned by any reference file: every normal-initialised weight is
+#       trained).  A model replays a fresh process's draws; ``tf_models_before`` / ``tf_extra_op_seeds`` place
+#       it later in a process (the bundled fold 3: 1 and 1).
+#   "independent": every weight an independent numpy draw of the same distribution (round 1).
+INIT_SCHEMES = ("tf27", "independent")
 
 
-def _normal_prefix(seed, n):
-    """The first n values of the seeded standard-normal stream (prefix-consistent, as a stateless op)."""
-    return np.random.default_rng([int(seed), 0]).standard_normal(n)
+def _session(seed, tf_random):
+    """The TFRandom state a weight is drawn from: the model's shared one, or a fresh set_seed(seed) state."""
+    if tf_random is not None:
+        return tf_random
+    from .tf_random import TFRandom
+    return TFRandom(seed)
 
 
 class Layer:
@@ -131,10 +136,13 @@ class Layer:
 class Embedding(Layer):
     """Keras Embedding(input_dim=N, output_dim=D), RandomUniform(0, 1) init (IDDGCN.py:215-225)."""
 
-    def __init__(self, input_dim, output_dim, seed=None, name="entity_embeddings", init="stateless"):
+    def __init__(self, input_dim, output_dim, seed=None, name="entity_embeddings", init="tf27", tf_random=None):
         super().__init__(name)
-        rng = np.random.default_rng([int(seed), 1] if init == "stateless" and seed is not None else seed)
-        self._weights = [rng.random((input_dim, output_dim)).astype(np.float32)]
+        if init == "tf27" and seed is not None:
+            w = _session(seed, tf_random).uniform((input_dim, output_dim), 0, 1, seed=int(seed))
+        else:
+            w = np.random.default_rng(seed).random((input_dim, output_dim))
+        self._weights = [w.astype(np.float32)]
 
 
 class IDDGCN_Layer(Layer):
@@ -143,25 +151,27 @@ class IDDGCN_Layer(Layer):
     ``relation_weights`` is created (it occupies a slot of the h5 layout) but,
     as in the reference, never used by ``call`` and never trained."""
 
-    def __init__(self, num_entities, num_relations, output_dim, seed, name="iddgcn__layer", init="stateless",
-                 layer_index=0, **kwargs):
+    def __init__(self, num_entities, num_relations, output_dim, seed, name="iddgcn__layer", init="tf27",
+                 layer_index=0, tf_random=None, **kwargs):
         super().__init__(kwargs.get("name", name))
         self.num_entities, self.num_relations, self.output_dim, self.seed = (num_entities, num_relations,
                                                                              output_dim, seed)
         if init not in INIT_SCHEMES:
             raise ValueError(f"init must be one of {INIT_SCHEMES}")
         R, D = num_relations, output_dim
-        if init == "stateless":
-            K = _normal_prefix(seed, R * D * D).reshape(R, D, D)     # RandomNormal(0, 1, seed) (:26-30)
-            S = _normal_prefix(seed, D * D).reshape(D, D)            # the same stream (:31-36): == K[0]
-            rng = np.random.default_rng([int(seed), 2, int(layer_index)])   # unseeded: fresh per layer
+        if init == "tf27":
+            tf = _session(seed, tf_random)
+            K = tf.normal((R, D, D), 0.0, 1.0, seed=int(seed))      # RandomNormal(0, 1, seed) (:25-30)
+            S = tf.normal((D, D), 0.0, 1.0, seed=int(seed))         # the same kernel, its stream continued (:31-36)
+            relw = tf.uniform((R,), -0.05, 0.05)                    # 'uniform' (:39-44), an op seed
+            Wa = tf.glorot_uniform((D, R))                          # glorot_uniform (:47-52), an op seed
         else:
             rng = np.random.default_rng(seed)
             K = rng.standard_normal((R, D, D))
             S = rng.standard_normal((D, D))
-        self._weights = [K.astype(np.float32), S.astype(np.float32),
-                         rng.uniform(-0.05, 0.05, (R,)).astype(np.float32),       # 'uniform' (:39-44)
-                         _glorot_uniform(rng, (D, R)).astype(np.float32),          # glorot_uniform (:47-52)
+            relw = rng.uniform(-0.05, 0.05, (R,))
+            Wa = _glorot_uniform(rng, (D, R))
+        self._weights = [K.astype(np.float32), S.astype(np.float32), relw.astype(np.float32), Wa.astype(np.float32),
                          np.zeros((R,), np.float32)]
 
     def __call__(self, inputs, weights=None):
@@ -193,17 +203,19 @@ class IDDGCN_Layer(Layer):
 class DistMult(Layer):
     """IDDGCN.py:82-109: rel_embedding (R, D) ~ N(0,1); score = sigmoid(sum h*r*t), shape (1, B)."""
 
-    def __init__(self, num_relations, seed, name="DistMult", embedding_dim=None, init="stateless", **kwargs):
+    def __init__(self, num_relations, seed, name="DistMult", embedding_dim=None, init="tf27", tf_random=None,
+                 **kwargs):
         super().__init__(name)
         self.num_relations, self.seed, self.init = num_relations, seed, init
+        self._tf = tf_random
         self._weights = []
         if embedding_dim is not None:
             self.build(embedding_dim)
 
     def build(self, embedding_dim):
         R, D = self.num_relations, embedding_dim
-        if self.init == "stateless":      # RandomNormal(0, 1, seed) (:90-99): the layers' stream, first R*D values
-            w = _normal_prefix(self.seed, R * D).reshape(R, D)
+        if self.init == "tf27":           # RandomNormal(0, 1, seed) (:90-99): the layers' normal kernel, continued
+            w = _session(self.seed, self._tf).normal((R, D), 0.0, 1.0, seed=int(self.seed))
         else:
             w = np.random.default_rng(self.seed).standard_normal((R, D))
         self._weights = [w.astype(np.float32)]
@@ -251,15 +263,26 @@ class IDDGCN_Model:
     """IDDGCN.py:112-178 (custom train_step) + get_IDDGCN_Model wiring (:201-285)."""
 
     def __init__(self, num_entities, num_relations, embedding_dim, output_dim, seed, mode=0, fold=0,
-                 neg_weight=1.0, init="stateless"):
+                 neg_weight=1.0, init="tf27", tf_models_before=0, tf_extra_op_seeds=0):
         if embedding_dim != output_dim:
             raise ValueError("embedding_dim must equal output_dim (IDDGCN.py:307-308)")
         self.num_entities, self.num_relations, self.dim = num_entities, num_relations, embedding_dim
         self.seed, self.mode, self.fold, self.neg_weight = seed, mode, fold, neg_weight
-        self.entity_embeddings = Embedding(num_entities, embedding_dim, seed, init=init)
+        if init not in INIT_SCHEMES:
+            raise ValueError(f"init must be one of {INIT_SCHEMES}")
+        tf = None
+        if init == "tf27":      # one eager random state for the whole model, drawn in the reference's order
+            from .tf_random import TFRandom, draw_model
+            tf = TFRandom(seed)
+            for _ in range(tf_models_before):
+                draw_model(tf, num_entities, num_relations, embedding_dim, seed)
+            for _ in range(tf_extra_op_seeds):
+                tf.get_seed()
+        self.entity_embeddings = Embedding(num_entities, embedding_dim, seed, init=init, tf_random=tf)
         self.gcn_layers = [IDDGCN_Layer(num_entities, num_relations, output_dim, seed, init=init, layer_index=i,
-                                        name="iddgcn__layer" + ("" if i == 0 else f"_{i}")) for i in range(3)]
-        self.distmult = DistMult(num_relations, seed, embedding_dim=embedding_dim, init=init)
+                                        tf_random=tf, name="iddgcn__layer" + ("" if i == 0 else f"_{i}"))
+                           for i in range(3)]
+        self.distmult = DistMult(num_relations, seed, embedding_dim=embedding_dim, init=init, tf_random=tf)
         self.layers = [self.entity_embeddings, *self.gcn_layers, self.distmult]
         self.neg_triples = None         # set to override the reference's .npy negatives
         self.neg_path_template = "../datasets/prediction_datasets/mode{mode}_fold{fold}_X_train_neg.npy"
@@ -474,7 +497,8 @@ class IDDGCN_Model:
 
 
 def get_IDDGCN_Model(num_entities, num_relations, embedding_dim, output_dim, seed, all_feature_matrix=None, mode=0,
-                     fold=0, init="stateless"):
+                     fold=0, init="tf27", **init_kw):
     """IDDGCN.py:201-285.  ``all_feature_matrix`` is accepted and unused, as in the
     reference (the Embedding's ``weights=`` argument is commented out, :219)."""
-    return IDDGCN_Model(num_entities, num_relations, embedding_dim, output_dim, seed, mode=mode, fold=fold, init=init)
+    return IDDGCN_Model(num_entities, num_relations, embedding_dim, output_dim, seed, mode=mode, fold=fold, init=init,
+                        **init_kw)

@@ -184,22 +184,28 @@ def test_model_surface_cpu_only():
     assert w.shape == (845, 64) and w.min() >= 0 and w.max() < 1
 
 
-def test_init_schemes_seeding_structure():
-    """model.INIT_SCHEMES (IDDGCN.py:17-58, 90-99 under Keras 2.7's stateless seeded initialisers): with
-    "stateless" every seeded normal is a prefix of ONE stream — self_kernel == relation_kernels[0], the three
-    layers identical, DistMult rel = the stream's first R*D values — while the unseeded W_alpha differs per
-    layer; "independent" draws every weight on its own.  Same distributions, deterministic per seed."""
+def test_init_schemes():
+    """model.INIT_SCHEMES: the default "tf27" replays TF 2.7's draws (iddgcn_amd/tf_random.py, pinned against the
+    bundled weights in tests/test_tf_random.py): the model's weights equal tf_random.reference_init's in the
+    reference's creation order, the seeded normal kernel continues its stream (self_kernel is not
+    relation_kernels[0]), W_alpha differs per layer, b_alpha = 0; "independent" draws the same distributions from
+    numpy.  Both deterministic per seed."""
     from iddgcn_amd import get_IDDGCN_Model
+    from iddgcn_amd.tf_random import reference_init
     m = get_IDDGCN_Model(845, 4, 64, 64, 89, None, 0, 0)
-    L = [m.get_layer(n).get_weights() for n in ("iddgcn__layer", "iddgcn__layer_1", "iddgcn__layer_2")]
-    K, S = L[0][0], L[0][1]
-    assert np.array_equal(S, K[0])
-    assert all(np.array_equal(l[0], K) and np.array_equal(l[1], S) for l in L[1:])
-    assert np.array_equal(m.get_layer("DistMult").get_weights()[0], S.reshape(-1)[:4 * 64].reshape(4, 64))
-    assert not np.array_equal(L[0][3], L[1][3])                       # W_alpha: fresh per layer
-    assert abs(K.std() - 1.0) < 0.01 and abs(K.mean()) < 0.01
+    ref = reference_init(845, 4, 64, 89)
+    assert np.array_equal(m.get_layer("entity_embeddings").get_weights()[0], ref["E"])
+    for l, name in enumerate(("iddgcn__layer", "iddgcn__layer_1", "iddgcn__layer_2"), 1):
+        K, S, relw, Wa, ba = m.get_layer(name).get_weights()
+        for a, b in ((K, ref[f"K{l}"]), (S, ref[f"S{l}"]), (relw, ref[f"relw{l}"]), (Wa, ref[f"Wa{l}"]),
+                     (ba, ref[f"ba{l}"])):
+            assert np.array_equal(a, b), (name, a.shape)
+    assert np.array_equal(m.get_layer("DistMult").get_weights()[0], ref["rel"])
+    K, S = ref["K1"], ref["S1"]
+    assert not np.array_equal(S, K[0]) and not np.array_equal(ref["K2"], K)
+    assert abs(K.std() - 1.0) < 0.02 and abs(K.mean()) < 0.03
     lim = np.sqrt(6.0 / (64 + 4))
-    assert np.abs(L[0][3]).max() <= lim and np.array_equal(L[0][4], np.zeros(4, np.float32))
+    assert np.abs(ref["Wa1"]).max() <= lim and not np.array_equal(ref["Wa1"], ref["Wa2"])
     again = get_IDDGCN_Model(845, 4, 64, 64, 89, None, 0, 0).get_weights()
     assert all(np.array_equal(a, b) for a, b in zip(m.get_weights(), again))
     ind = get_IDDGCN_Model(845, 4, 64, 64, 89, None, 0, 0, init="independent")

@@ -5,10 +5,12 @@ BinaryCrossentropy + Adam(1e-3), full-batch fit for 5000 epochs on the fold's X_
 negatives) followed by its evaluation (IDDGCN_eval.py:35-122: adjacency from X_train plus the test
 positives, predict on test positives + negatives, ROC-AUC / AUPR / accuracy at 0.5), on the HIP path
 through the Keras-shaped API.  Fold data are the reference's bundled files (tests/golden/fold*_data.npz).
-TF's seeded initializers cannot be replayed, so each (fold, seed) starts from this package's seeded
-initialisation of the same distributions; the published-weights AUCs are the yardstick.
+With the default init "tf27" and seed 89 each fold starts from the reference's own initial weights (TF 2.7's
+draws replayed, iddgcn_amd/tf_random.py; fold 3 as the second model of its process, as its bundled
+relation_weights show), so a fold's AUC is compared with the AUC of the weights the reference trained from that
+same start; other seeds / "independent" give the spread.
 
-usage: python tools/train_folds.py [--folds 0,1,2,3,4] [--seeds 89,1,2] [--epochs 5000] [--init stateless]
+usage: python tools/train_folds.py [--folds 0,1,2,3,4] [--seeds 89,1,2] [--epochs 5000] [--init tf27]
                                   [--out FILE]
 """
 import argparse
@@ -34,9 +36,11 @@ N_ENT, N_REL, DIM = 845, 4, 64
 REFERENCE_WEIGHTS_AUC = {0: 0.9072, 1: 0.8841, 2: 0.8832, 3: 0.9148, 4: 0.9068}
 
 
-def run(fold, seed, epochs, init="stateless"):
+def run(fold, seed, epochs, init="tf27"):
     d = np.load(os.path.join(ROOT, "tests", "golden", f"fold{fold}_data.npz"))
-    model = get_IDDGCN_Model(N_ENT, N_REL, DIM, DIM, seed, None, 0, fold, init=init)
+    # the bundled fold-3 weights were trained as the second model of a process (tests/test_tf_random.py)
+    kw = dict(tf_models_before=1, tf_extra_op_seeds=1) if (init == "tf27" and fold == 3 and seed == 89) else {}
+    model = get_IDDGCN_Model(N_ENT, N_REL, DIM, DIM, seed, None, 0, fold, init=init, **kw)
     model.neg_triples = d["X_train_neg"][None]
     model.compile(loss=BinaryCrossentropy(), optimizer=Adam(learning_rate=0.001))
     X = d["X_train"][None]
@@ -63,7 +67,7 @@ def main():
     ap.add_argument("--seeds", default="89,1,2")
     ap.add_argument("--epochs", type=int, default=5000)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--init", default="stateless", choices=["stateless", "independent"],
+    ap.add_argument("--init", default="tf27", choices=["tf27", "independent"],
                     help="weight-initialisation scheme (iddgcn_amd.model.INIT_SCHEMES)")
     a = ap.parse_args()
     runs = []
