@@ -3942,7 +3942,7 @@ bool b3_select(const RowGemmP& p, int& nv, bool& aux, bool& bc) {
 }
 // ~128 row ranges (a multiple of 8) x 2 column halves: one workgroup per CU, every one resident
 #ifndef B3W
-#define B3W 1
+#define B3W 0
 #endif
 void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux, bool bc) {
     const long long nt = ((long long)p.M + rb3::TR - 1) / rb3::TR;
