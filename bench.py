@@ -309,11 +309,21 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         from iddgcn_amd.sampling import negative_samples
         neg = negative_samples(pos[::cfg["neg_every"]], N, 89, device=dev)
     T = len(pos) + len(neg)
-    lo, hi = shard_range(T, rank, world)                  # this rank's contiguous shard (pos ++ neg)
     npos = len(pos)
-    tri = np.concatenate([pos[lo:min(hi, npos)], neg[max(lo - npos, 0):max(hi - npos, 0)]])
-    lab = np.concatenate([np.ones(max(0, min(hi, npos) - lo), np.float32),
-                          np.zeros(max(0, hi - max(lo, npos)), np.float32)])
+    cuts = None
+    if shard == "node" and world > 1:
+        # node-row partitioning: rank k owns a contiguous node range (balanced by tail edges + node work) and the
+        # scored edges whose tail it owns (parallel.NodeShard)
+        from iddgcn_amd.parallel import node_ranges, node_shard_triples
+        cuts = node_ranges(np.bincount(np.concatenate([pos[:, 2], neg[:, 2]]), minlength=N), world)
+        tri, lab = node_shard_triples(np.concatenate([pos, neg]),
+                                      np.concatenate([np.ones(npos, np.float32), np.zeros(len(neg), np.float32)]),
+                                      cuts, rank)
+    else:
+        lo, hi = shard_range(T, rank, world)              # this rank's contiguous shard (pos ++ neg)
+        tri = np.concatenate([pos[lo:min(hi, npos)], neg[max(lo - npos, 0):max(hi - npos, 0)]])
+        lab = np.concatenate([np.ones(max(0, min(hi, npos) - lo), np.float32),
+                              np.zeros(max(0, hi - max(lo, npos)), np.float32)])
     feat = args.features or cfg.get("features", "f32")
     eng = Engine(N, R, D, dev, gemm=gemm, features=feat, planes=not args.no_planes)
     eng.overlap = args.overlap
@@ -323,7 +333,10 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
     init = reference_init(np, N, R, D, 89)
     comm = BucketedAllReduce() if world > 1 else None
-    if shard == "relation" and world > 1:
+    if cuts is not None:
+        from iddgcn_amd.parallel import NodeShard
+        eng.row_shard = NodeShard(cuts)          # node rows split over the ranks, scored edges by tail
+    elif shard == "relation" and world > 1:
         eng.node_shard = RelationShard(R, N)     # SURVEY §8(e) alternative: node tables split by relation
     elif shard == "spmm" and world > 1:
         eng.spmm_shard = RelationShard(R, N)     # row-partitioned SpMMs, node GEMMs replicated
@@ -373,7 +386,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
            "gemm_operands": GEMM_NOTE[gemm] + ("; edge GEMMs bf16 (features=bf16)" if feat == "bf16" else ""),
            "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
                       "scored_edges": T, "scored_edges_per_gpu": ed.T, "feat_dim": D,
-                      "parallelism": f"edge-dp{world}" + ("+relation-sharded-nodes" if eng.node_shard else "")
+                      "parallelism": (f"node-rows{world}" if eng.row_shard else f"edge-dp{world}")
+                      + ("+relation-sharded-nodes" if eng.node_shard else "")
                       + ("+row-partitioned-spmm" if eng.spmm_shard else ""),
                       "gemm": gemm, "features": feat},
            "scored_edges_per_s": T / (elapsed / steps), "loss": loss_val, "steps": steps, "warmup": warmup,
@@ -414,14 +428,15 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--also", nargs="*", default=None,
                     help="further workloads timed in the same run (min(steps, 5) steps, 1 warm-up), reported "
-                         "under 'also': config ids, 'Nr' = config N with relation-sharded node tables, 'Ns' = "
-                         "with row-partitioned SpMMs; default 4 5 (BASELINE configs 4 and 5), plus 3s 4r with "
-                         "more than one GPU; none to skip")
+                         "under 'also': config ids, 'Nn' = config N node-row partitioned, 'Nr' = with "
+                         "relation-sharded node tables, 'Ns' = with row-partitioned SpMMs; default 4 5 (BASELINE "
+                         "configs 4 and 5), plus 4n 5n 4r with more than one GPU; none to skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-planes", action="store_true",
                     help="fp32 tail tables x^1, x^2 instead of the pre-split planes form (A/B)")
-    ap.add_argument("--shard", default="edge", choices=["edge", "relation", "spmm"],
-                    help="multi-GPU: edge partitioning only (default), also relation-sharded node tables, or also "
+    ap.add_argument("--shard", default="edge", choices=["edge", "node", "relation", "spmm"],
+                    help="multi-GPU: edge partitioning only (default), node-row partitioning (node tables split by row "
+                         "range, scored edges by tail: parallel.NodeShard), also relation-sharded node tables, or also "
                          "row-partitioned SpMMs (A_r E all-gathered, dAE reduce-scattered; node GEMMs replicated)")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],
                     help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
@@ -477,14 +492,15 @@ def main():
         result["world"] = world
         result["backend"] = dist.get_backend()
     also = []
-    todo = (["4", "5"] + (["3s", "4r"] if world > 1 else [])) if args.also is None else \
+    todo = (["4", "5"] + (["4n", "5n", "4r"] if world > 1 else [])) if args.also is None else \
         [a for a in args.also if a != "none"]
     for item in todo:
-        cid = int(item.rstrip("rs"))
-        shard = "relation" if item.endswith("r") else ("spmm" if item.endswith("s") else "edge")
+        cid = int(item.rstrip("rsn"))
+        shard = {"r": "relation", "s": "spmm", "n": "node"}.get(item[-1], "edge")
         if cid == args.config and shard == args.shard:
             continue
-        name = CONFIGS[cid]["name"] + {"relation": "+relation-sharded", "spmm": "+row-partitioned-spmm"}.get(shard, "")
+        name = CONFIGS[cid]["name"] + {"relation": "+relation-sharded", "spmm": "+row-partitioned-spmm",
+                                       "node": "+node-rows"}.get(shard, "")
         if world > 1:
             # ranks decide TOGETHER whether the workload fits (a rank that ran out of memory alone would leave the
             # others waiting in a collective), then run it without recovery: any failure ends every rank

@@ -3656,6 +3656,7 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
                                                             const int* __restrict__ hseg_ptr,
                                                             const int* __restrict__ hperm,
                                                             const float* __restrict__ dWedge,
+                                                            const float* __restrict__ ep_in,
                                                             float* __restrict__ dP, long long dp_rel_stride,
                                                             float* __restrict__ dsum, float* __restrict__ dz) {
     constexpr int LPR = D / 4;
@@ -3680,6 +3681,12 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
 #pragma unroll
         for (int r = 0; r < MAX_R; ++r)
             if (r < R) ep[r] += dwe[r];
+    }
+    // node-partitioned steps: the head sums arrive complete from the ranks (iddgcn_head_wsum_f32 + reduce-scatter)
+    if (ep_in && live && sub == 0) {
+#pragma unroll
+        for (int r = 0; r < MAX_R; ++r)
+            if (r < R) ep[r] += ep_in[n * R + r];
     }
     float dw[MAX_R];
 #pragma unroll
@@ -3726,6 +3733,20 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(long long M, int width
     const long long e = x / width;
     const int j = (int)(x % width);
     dst[x] = src[(long long)idx[e] * width + j];
+}
+
+// out[n][r] = sum_{k in [hptr[n], hptr[n+1])} w[hperm[k]][r]: the per-head sums of per-edge narrow rows (the
+// dWedge head sums of a node-partitioned step), one thread per (node, relation), the segment in order
+__global__ __launch_bounds__(256) void head_wsum_kernel(int n_nodes, int R, const int* __restrict__ hptr,
+                                                        const int* __restrict__ hperm, const float* __restrict__ w,
+                                                        float* __restrict__ out) {
+    const long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= (long long)n_nodes * R) return;
+    const long long n = x / R;
+    const int r = (int)(x % R);
+    float s = 0.f;
+    for (int k = hptr[n]; k < hptr[n + 1]; ++k) s += w[(long long)hperm[k] * R + r];
+    out[x] = s;
 }
 
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(int n_slabs, long long n, const float* __restrict__ slab,
@@ -4575,8 +4596,8 @@ int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const in
 
 int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const float* dO, const float* P,
                              long long p_rel_stride, const float* Ssm, const float* W, const int* hseg_ptr,
-                             const int* hperm, const float* dWedge, float* dP, long long dp_rel_stride, float* dsum,
-                             float* dz) {
+                             const int* hperm, const float* dWedge, const float* ep_in, float* dP,
+                             long long dp_rel_stride, float* dsum, float* dz) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
     if (n_nodes < 0 || !dO || !P || !Ssm || !W || !dP || !dz) return IDDGCN_E_BAD_ARG;
@@ -4584,7 +4605,7 @@ int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const floa
     if (n_nodes == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     const unsigned grid = grid_for(n_nodes, d / 4);
-#define HK(DD) hipLaunchKernelGGL(head_bwd_node_kernel<DD>, dim3(grid), dim3(256), 0, st, n_nodes, R, dO, P, p_rel_stride, Ssm, W, hseg_ptr, hperm, dWedge, dP, dp_rel_stride, dsum, dz)
+#define HK(DD) hipLaunchKernelGGL(head_bwd_node_kernel<DD>, dim3(grid), dim3(256), 0, st, n_nodes, R, dO, P, p_rel_stride, Ssm, W, hseg_ptr, hperm, dWedge, ep_in, dP, dp_rel_stride, dsum, dz)
     switch (d) {
         case 32: HK(32); break;
         case 64: HK(64); break;
@@ -4592,6 +4613,17 @@ int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const floa
         default: HK(256); break;
     }
 #undef HK
+    return launch_status();
+}
+
+int iddgcn_head_wsum_f32(void* stream, int n_nodes, int R, const int* hptr, const int* hperm, const float* w,
+                         float* out) {
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (n_nodes < 0 || !hptr || !hperm || !w || !out) return IDDGCN_E_BAD_ARG;
+    if (n_nodes == 0) return 0;
+    const long long total = (long long)n_nodes * R;
+    hipLaunchKernelGGL(head_wsum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       n_nodes, R, hptr, hperm, w, out);
     return launch_status();
 }
 

@@ -337,11 +337,14 @@ class Engine:
         return self._side
 
     node_shard = None      # parallel.RelationShard: per-relation node tables split over the ranks
+    row_shard = None       # parallel.NodeShard: node rows split over the ranks, scored edges by tail (round 4)
     # parallel.RelationShard used for the two SpMMs only (node GEMMs replicated): A_r·E row-partitioned and
     # all-gathered, dAE reduce-scattered to the row owners before a transposed SpMM over their columns
     spmm_shard = None
 
     def forward(self, P, adj, ed, ws, train):
+        if self.row_shard is not None:
+            return self._forward_rows(P, adj, ed, ws, train)
         N, R, D, T = self.N, self.R, self.D, ed.T
         E = P["E"]
         # every GEMM call carries this engine's operand precision: pn for the plain node-level projections, pr for
@@ -417,6 +420,8 @@ class Engine:
         parallel.BucketedAllReduce) gets each contiguous piece of G.buf as soon as it is final: all
         small gradients + the loss after the layer loop, then row chunks of dE as the transposed SpMM
         produces them, so the all-reduce of the large dE overlaps the SpMM of the next chunk."""
+        if self.row_shard is not None:
+            return self._backward_rows(P, G, adj, ed, ws, comm)
         N, R, D = self.N, self.R, self.D
         pk, pn, pr = dict(precision=self.gemm), dict(precision=self.proj_gemm), dict(precision=self.row_gemm)
         dOn, dOn_next = ws.dOn_a, ws.dOn_b      # head seed dO^3, written by distmult_bce_heads
@@ -497,6 +502,126 @@ class Engine:
             # SpMM runs over the entries in its range only, and dE's all-reduce below adds the ranks' parts
             self.spmm_shard.reduce_scatter(ws.dAE.view(R * N, D))
             bptr, bcol, bval = adj.bwd_columns(self.spmm_shard.a, self.spmm_shard.b)
+        chunks = comm.row_chunks(N) if comm is not None else [(0, N)]
+        for n0, n1 in chunks:
+            ops.spmm_csr(bptr[n0:n1 + 1], bcol, bval, ws.dAE.view(R * N, D),
+                         G["E"][n0:n1].view(1, n1 - n0, D), 1, n1 - n0, accumulate=True)
+            if comm is not None:
+                comm.ready(G["E"][n0:n1].reshape(-1))
+
+    # -- node-partitioned step (parallel.NodeShard) -------------------------------
+    def _dm_seed(self, T):
+        if self._pred_seed is None:        # Keras BCE, x 1/num_entities (IDDGCN.py:161-168)
+            return 1.0 / (float(self._t_global or T) * float(self.N)), True
+        return float(self._pred_seed), False
+
+    def _forward_rows(self, P, adj, ed, ws, train):
+        """The forward with the node tables computed for the owned rows [a, b) only (parallel.NodeShard): the
+        rank's scored edges all have their tail there, so the tail chain reads local P / ES1 rows; the edges'
+        heads need W^l (all-gathered, N x R) and DistMult X^3 (all-gathered, N x D)."""
+        N, R, D, T = self.N, self.R, self.D, ed.T
+        sh = self.row_shard
+        a, b = sh.a, sh.b
+        E = P["E"]
+        pn = dict(precision=self.proj_gemm)
+        pr = dict(precision=self.row_gemm)
+        idx = sh.owned_idx(self.device)
+        if b > a:
+            for r in range(R):              # A_r E over the owned rows (IDDGCN.py:69-70)
+                ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + a:r * (N + 1) + b + 1], adj.fwd_col, adj.fwd_val, E,
+                             ws.AE[r][a:b].view(1, b - a, D), 1, b - a)
+            proj = [(ws.AE[r][a:b], P[f"K{l + 1}"][r], ws.P[l, r][a:b], pn) for l in range(NUM_LAYERS)
+                    for r in range(R)]
+            proj.append((E[a:b], P["S1"], ws.ES1[a:b], pn))
+            for i in range(0, len(proj), 16):
+                ops.rowgemm_batched(proj[i:i + 16])
+            ops.alpha_fwd(E[a:b], P["Wa1"], P["ba1"], ws.Ssm[0][a:b], ws.W[0][a:b])
+        sh.all_gather(ws.W[0])
+        ops.gather_rows(ws.W[0], ed.h, ws.Wedge[0])
+        if b > a:
+            ops.combine(ws.ES1, ws.W[0][a:b], ws.P[0], ws.X[0][a:b], y_idx=idx, v_idx=idx)
+        pl = self.use_planes
+        ops.combine(ws.ES1, ws.Wedge[0], ws.P[0], ws.xt[0], y_idx=ed.t, v_idx=ed.t, planes_out=pl)
+        for l in (1, 2):
+            S = P[f"S{l + 1}"]
+            if b > a:
+                ops.alpha_fwd(ws.X[l - 1][a:b], P[f"Wa{l + 1}"], P[f"ba{l + 1}"], ws.Ssm[l][a:b], ws.W[l][a:b])
+            sh.all_gather(ws.W[l])
+            ops.gather_rows(ws.W[l], ed.h, ws.Wedge[l])
+            if b > a:
+                ops.rowgemm(ws.X[l - 1][a:b], S, ws.X[l][a:b], coef=ws.W[l][a:b], V=ws.P[l], v_idx=idx,
+                            v_rel_stride=N * D, act=L.ACT_SIGMOID, **pr)
+            with self._mark("tail_fwd_gemm"):
+                ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
+                            v_rel_stride=N * D, act=L.ACT_SIGMOID,
+                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, **pr)
+        sh.all_gather(ws.X[2])
+        if train:
+            scale, bce = self._dm_seed(T)
+            ops.distmult_bce_heads(ed.hptr, ed.hperm, ws.X[2], ws.xt[2], ed.r, P["rel"], ed.y if bce else None,
+                                   ws.xt[2], ws.dOn_a, ws.drel_slab, ws.loss_slab, scale=scale,
+                                   p_out=ws.p if self._want_p else None, s_out=ws.s if self._want_p else None)
+        else:
+            ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], p_out=ws.p, s_out=ws.s)
+
+    def _backward_rows(self, P, G, adj, ed, ws, comm):
+        """The backward of a node-partitioned step: the head seeds dO^3 and the dWedge head sums are
+        reduce-scattered to the heads' owners, everything node-level runs over the owned rows, the tail
+        segment sums are local; every gradient written is a partial over the rank's rows / edges, summed by
+        ``comm`` (the flat gradient buffer's bucketed all-reduce)."""
+        N, R, D = self.N, self.R, self.D
+        sh = self.row_shard
+        a, b = sh.a, sh.b
+        pk, pn, pr = dict(precision=self.gemm), dict(precision=self.proj_gemm), dict(precision=self.row_gemm)
+        if getattr(ws, "ep", None) is None:
+            ws.ep = torch.empty(N, R, dtype=torch.float32, device=self.device)
+        dOn, dOn_next = ws.dOn_a, ws.dOn_b
+        sh.reduce_scatter(dOn)                   # head seeds dO^3 of the rank's edges -> the heads' owners
+        pl = self.use_planes
+        for l in (2, 1, 0):
+            Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
+            do = ws.xt[l]
+            ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
+                                dsum=ws.dES if l == 0 else None)
+            if l > 0:
+                with self._mark("tail_dS_tn"):
+                    ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)
+                with self._mark("tail_bwd_gemm"):
+                    ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
+                                planes=L.PLANES_AUX if pl else 0, **pr)
+            ops.head_wsum(ed.hptr, ed.hperm, ws.dWedge, ws.ep)
+            sh.reduce_scatter(ws.ep)             # dWedge head sums -> the heads' owners
+            K, dK = P[f"K{l + 1}"], G[f"K{l + 1}"]
+            Xin = ws.X[l - 1] if l > 0 else P["E"]
+            ws.WaT.copy_(P[f"Wa{l + 1}"].t())
+            if b > a:
+                ops.head_bwd_node(dOn[a:b], Pl[:, a:b], ws.Ssm[l][a:b], Wl[a:b], ws.dP[:, a:b], ws.dz[a:b],
+                                  ep=ws.ep[a:b], dsum=ws.dES[a:b] if l == 0 else None)
+                ops.gemm_tn_narrow(Xin[a:b], ws.dz[a:b], G[f"Wa{l + 1}"], G[f"ba{l + 1}"], ws.narrow_slab)
+                tn = [(Xin[a:b], dOn[a:b], G[f"S{l + 1}"], True) if l > 0 else (P["E"][a:b], ws.dES[a:b], G["S1"], False)]
+                tn += [(ws.AE[r][a:b], ws.dP[r][a:b], dK[r], False) for r in range(R)]
+                for i in range(0, len(tn), L.TN_BATCH):
+                    ops.gemm_tn_batched(tn[i:i + L.TN_BATCH], ws.tn_slab, **pk)
+                if l > 0:
+                    ops.rowgemm(dOn[a:b], Sl, dOn_next[a:b], b_trans=True, coef=ws.dz[a:b], V=ws.WaT, v_rel_stride=D,
+                                v_row_stride=0, act=L.ACT_DSIGMOID, aux=Xin[a:b], **pr)
+                else:
+                    ops.rowgemm(ws.dES[a:b], Sl, G["E"][a:b], b_trans=True, coef=ws.dz[a:b], V=ws.WaT,
+                                v_rel_stride=D, v_row_stride=0, **pr)
+                ops.rowgemm_batched([(ws.dP[r][a:b], K[r], ws.dAE[r][a:b],
+                                      dict(b_trans=True, accumulate=(l != 2), **pn)) for r in range(R)])
+            else:                                # an empty range: its partials are zero
+                for k in (f"Wa{l + 1}", f"ba{l + 1}", f"K{l + 1}") + (("S1",) if l == 0 else ()):
+                    G[k].zero_()
+            dOn, dOn_next = dOn_next, dOn
+        ops.reduce_slabs(ws.drel_slab, ws.nb_dm, G["rel"])
+        ops.reduce_slabs(ws.loss_slab, ws.nb_dm, G.loss)
+        if comm is not None:
+            comm.ready(G.buf[N * D:])
+        # dE: the owned rows' direct terms (above), zero elsewhere, + the transposed SpMM of the owned dAE rows
+        G["E"][:a].zero_()
+        G["E"][b:].zero_()
+        bptr, bcol, bval = adj.bwd_node_rows(a, b)
         chunks = comm.row_chunks(N) if comm is not None else [(0, N)]
         for n0, n1 in chunks:
             ops.spmm_csr(bptr[n0:n1 + 1], bcol, bval, ws.dAE.view(R * N, D),

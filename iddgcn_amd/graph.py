@@ -228,6 +228,28 @@ class DeviceAdjacency:
         self._bwd_cols = (key, self.bwd_val, out)
         return out
 
+    def bwd_node_rows(self, a, b):
+        """The merged transposed CSR restricted to the entries whose dAE row is node a <= i < b of ANY relation
+        (column r*N + i): the transposed SpMM of a node-partitioned step (parallel.NodeShard) over the rows its
+        rank owns, every output row's entries in their original order; cached per range."""
+        key = (int(a), int(b))
+        cached = getattr(self, "_bwd_nodes", None)
+        if cached is not None and cached[0] == key and cached[1] is self.bwd_val:
+            return cached[2]
+        N = self.num_entities
+        col = self.bwd_col.long()
+        node = col % N
+        keep = (node >= a) & (node < b)
+        rows = torch.repeat_interleave(torch.arange(N, device=col.device),
+                                       (self.bwd_ptr[1:] - self.bwd_ptr[:-1]).long())
+        counts = torch.bincount(rows[keep], minlength=N)
+        ptr = torch.zeros(N + 1, dtype=torch.int32, device=col.device)
+        ptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+        out = (ptr, self.bwd_col[keep].contiguous(),
+               None if self.bwd_val is None else self.bwd_val[keep].contiguous())
+        self._bwd_nodes = (key, self.bwd_val, out)
+        return out
+
     def to_entry_order(self, csr_vals):
         """Per-entry quantity in forward-CSR order -> list of per-relation tensors in entry order."""
         flat = csr_vals[self.fwd_pos]

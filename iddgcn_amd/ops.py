@@ -373,16 +373,34 @@ def tail_seg_reduce(seg_ptr, h_idx, W, dO, P, dP, dWedge, dsum=None):
                                                _ptr(dWedge)), "tail_seg_reduce")
 
 
-def head_bwd_node(dO, P, Ssm, W, dP, dz, *, hseg_ptr=None, hperm=None, dWedge=None, dsum=None):
+def head_bwd_node(dO, P, Ssm, W, dP, dz, *, hseg_ptr=None, hperm=None, dWedge=None, dsum=None, ep=None):
+    """Head-chain backward of one layer over the rows of dO (include/iddgcn.h iddgcn_head_bwd_node_f32).  P and dP
+    are (R, n, D) views whose rows are contiguous (a row range of the (R, N, D) node tables keeps their relation
+    stride); ``ep``: (n, R) head sums of dWedge computed elsewhere (node-partitioned steps)."""
     R, n_nodes, D = P.shape
     _req(dO, _F32, (n_nodes, D), "dO")
     _req(Ssm, _F32, (n_nodes, R), "Ssm")
     _req(W, _F32, (n_nodes, R), "W")
     _req(dz, _F32, (n_nodes, R), "dz")
     _req(dsum, _F32, (n_nodes, D), "dsum")
-    L.check(L.lib().iddgcn_head_bwd_node_f32(_stream(), n_nodes, D, R, _ptr(dO), _ptr(P), n_nodes * D, _ptr(Ssm),
-                                             _ptr(W), _ptr(hseg_ptr), _ptr(hperm), _ptr(dWedge), _ptr(dP),
-                                             n_nodes * D, _ptr(dsum), _ptr(dz)), "head_bwd_node")
+    _req(ep, _F32, (n_nodes, R), "ep")
+    for t, nm in ((P, "P"), (dP, "dP")):
+        if tuple(t.shape) != (R, n_nodes, D) or t.stride(1) != D or t.stride(2) != 1:
+            raise L.IddgcnError(f"head_bwd_node: {nm} must be (R, n, D) with contiguous rows")
+    L.check(L.lib().iddgcn_head_bwd_node_f32(_stream(), n_nodes, D, R, _ptr(dO), _ptr(P), P.stride(0), _ptr(Ssm),
+                                             _ptr(W), _ptr(hseg_ptr), _ptr(hperm), _ptr(dWedge), _ptr(ep), _ptr(dP),
+                                             dP.stride(0), _ptr(dsum), _ptr(dz)), "head_bwd_node")
+
+
+def head_wsum(hptr, hperm, w, out):
+    """out[n] = sum of w[hperm[k]] over the head segment k in [hptr[n], hptr[n+1]) (iddgcn_head_wsum_f32)."""
+    n_nodes, R = out.shape
+    _req(out, _F32, (n_nodes, R), "out")
+    _req(w, _F32, None, "w")
+    if hptr.numel() != n_nodes + 1:
+        raise L.IddgcnError("head_wsum: hptr must have n + 1 entries")
+    L.check(L.lib().iddgcn_head_wsum_f32(_stream(), n_nodes, R, _ptr(hptr), _ptr(hperm), _ptr(w), _ptr(out)),
+            "head_wsum")
 
 
 def gather_rows(src, idx, dst):

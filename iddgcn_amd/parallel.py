@@ -158,3 +158,108 @@ class RelationShard:
             mine.copy_(out)
         if padded:
             table[self.a:self.b].copy_(full[self.a:self.b])
+
+
+def node_ranges(tail_counts, world_size, node_weight=4.0):
+    """Contiguous node-row ranges [b_k, b_k+1) for a node-partitioned step: balanced by the work a row brings,
+    its scored edges (tail segment length) plus ``node_weight`` edge-equivalents of node-level work (the row's
+    SpMM, projections and head chain, ~4.5 edge GEMM rows at R = 2).  Returns world_size + 1 boundaries."""
+    w = np.asarray(tail_counts, dtype=np.float64) + float(node_weight)
+    c = np.concatenate([[0.0], np.cumsum(w)])
+    cuts = [int(np.searchsorted(c, c[-1] * k / world_size, side="left")) for k in range(world_size + 1)]
+    cuts[0], cuts[-1] = 0, len(w)
+    for k in range(1, world_size + 1):          # non-decreasing (empty ranges allowed on tiny graphs)
+        cuts[k] = max(cuts[k], cuts[k - 1])
+    return cuts
+
+
+class NodeShard:
+    """Node-row partitioning of the step (round 4).
+
+    Rank k owns the node rows [a, b) = [cuts[k], cuts[k+1]) (node_ranges: balanced by tail edges + node work) and
+    takes the scored edges whose TAIL it owns.  Everything a tail needs is then local: its layer-1 ES1 row, its
+    P_r^l rows (A_r E and the projections over the owned rows only), the tail segment sums of the backward (dP,
+    dES).  What crosses ranks, per step (collectives on (N, C) node tables, each rank contributing its rows):
+      forward   all-gather W^l (N x R, 3 per step): the dynamic weights of the edges' HEADS;
+                all-gather X^3 (N x D): DistMult's head rows;
+      backward  reduce-scatter dO^3 (N x D): the head seeds of the rank's edges go to the heads' owners;
+                reduce-scatter the dWedge head sums (N x R, 3 per step);
+                all-reduce of the flat gradient buffer (dE: the transposed SpMM of the owned dAE rows reaches every
+                column; the weight gradients are partial sums over the owned rows / edges).
+    That is 2 N D + 6 N R floats of all-gather / reduce-scatter beside edge partitioning's N D all-reduce, against
+    RelationShard's 6 R N D.  Padded to equal chunks (the ranges differ in length); gloo groups (several ranks
+    sharing a GPU in tests) stage through host memory."""
+
+    def __init__(self, cuts, group=None):
+        self.group = group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.cuts = [int(c) for c in cuts]
+        if len(self.cuts) != self.world + 1:
+            raise ValueError("NodeShard: one range per rank")
+        self.N = self.cuts[-1]
+        self.a, self.b = self.cuts[self.rank], self.cuts[self.rank + 1]
+        self.cmax = max(self.cuts[k + 1] - self.cuts[k] for k in range(self.world))
+        self._gloo = dist.get_backend(group) == "gloo"
+        self._idx = None
+
+    def owned_idx(self, device):
+        """int32 arange(a, b) on the device (row indices of the owned range, for gathered-row kernel forms)."""
+        import torch
+        if self._idx is None or self._idx.device != device:
+            self._idx = torch.arange(self.a, self.b, dtype=torch.int32, device=device)
+        return self._idx
+
+    def _padded(self, table):
+        import torch
+        buf = torch.zeros(self.world * self.cmax, *table.shape[1:], dtype=table.dtype, device=table.device)
+        return buf
+
+    def all_gather(self, table):
+        """table: (N, C) with this rank's rows [a, b) filled -> every row filled, on every rank."""
+        import torch
+        n = self.b - self.a
+        if self._gloo:
+            mine = torch.zeros(self.cmax, *table.shape[1:], dtype=table.dtype)
+            mine[:n] = table[self.a:self.b].cpu()
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(parts, mine, group=self.group)
+            for k in range(self.world):
+                a, b = self.cuts[k], self.cuts[k + 1]
+                if k != self.rank and b > a:
+                    table[a:b].copy_(parts[k][:b - a])
+            return
+        full = self._padded(table)
+        mine = torch.zeros(self.cmax, *table.shape[1:], dtype=table.dtype, device=table.device)
+        mine[:n].copy_(table[self.a:self.b])
+        dist.all_gather_into_tensor(full, mine, group=self.group)
+        for k in range(self.world):
+            a, b = self.cuts[k], self.cuts[k + 1]
+            if k != self.rank and b > a:
+                table[a:b].copy_(full[k * self.cmax:k * self.cmax + b - a])
+
+    def reduce_scatter(self, table):
+        """table: (N, C) partial sums on every rank -> this rank's rows [a, b) hold the sums over the ranks (rank
+        order; the other rows are left as they were)."""
+        import torch
+        n = self.b - self.a
+        if self._gloo:
+            host = table.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+            table[self.a:self.b].copy_(host[self.a:self.b])
+            return
+        full = self._padded(table)
+        for k in range(self.world):
+            a, b = self.cuts[k], self.cuts[k + 1]
+            if b > a:
+                full[k * self.cmax:k * self.cmax + b - a].copy_(table[a:b])
+        out = torch.empty(self.cmax, *table.shape[1:], dtype=table.dtype, device=table.device)
+        dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.group)
+        table[self.a:self.b].copy_(out[:n])
+
+
+def node_shard_triples(triples, labels, cuts, rank):
+    """The scored edges whose tail lies in rank's node range [cuts[rank], cuts[rank+1]) (a NodeShard step), in
+    their original order."""
+    t = np.asarray(triples)[:, 2]
+    keep = (t >= cuts[rank]) & (t < cuts[rank + 1])
+    return np.asarray(triples)[keep], (None if labels is None else np.asarray(labels)[keep])

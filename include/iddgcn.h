@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 7
+#define IDDGCN_ABI_VERSION 8
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -247,13 +247,20 @@ int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const in
 
 /* Node-level (head chain) backward of one layer, node n:
  *   dsum[n] += dO[n]                                   (if dsum)
- *   dW_r     = <dO[n], P[r][n]> + sum_{k in hseg(n)} dWedge[hperm[k]][r]
+ *   dW_r     = <dO[n], P[r][n]> + sum_{k in hseg(n)} dWedge[hperm[k]][r] (+ ep_in[n][r] if ep_in)
  *   ds_r     = dW_r w_r (1-w_r);  dz[n][j] = s_j (ds_j - sum_r ds_r s_r)   (softmax-sigmoid backward)
- *   dP[r][n] += w_r * dO[n]                                                   */
+ *   dP[r][n] += w_r * dO[n]
+ * ep_in (ABI 8): per-node head sums of dWedge computed elsewhere (a node-partitioned step: each rank's
+ * iddgcn_head_wsum_f32 over its edges, summed across the ranks), hseg_ptr NULL then.          */
 int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const float* dO,
                              const float* P, long long p_rel_stride, const float* Ssm, const float* W,
-                             const int* hseg_ptr, const int* hperm, const float* dWedge,
+                             const int* hseg_ptr, const int* hperm, const float* dWedge, const float* ep_in,
                              float* dP, long long dp_rel_stride, float* dsum, float* dz);
+
+/* out[n][r] = sum_{k in [hptr[n], hptr[n+1])} w[hperm[k]][r], in segment order (ABI 8): the head sums of the
+ * per-edge dynamic-weight gradients dWedge (IDDGCN.py:66,75), for a node-partitioned step's reduce-scatter. */
+int iddgcn_head_wsum_f32(void* stream, int n_nodes, int R, const int* hptr, const int* hperm, const float* w,
+                         float* out);
 
 /* dst[e][j] = src[idx[e]][j], j < width: per-edge copies of narrow node tables
  * (the dynamic weights W[h_e] of each layer, IDDGCN.py:66,75, reused by forward and backward). */

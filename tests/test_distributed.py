@@ -143,3 +143,63 @@ def test_relation_shard_collectives_world2_gloo():
     for rank, _, t, u, a, b in res:
         assert np.array_equal(t[:, 0], np.arange(15))
         assert np.all(u[a:b] == 3.0)
+
+
+def test_node_ranges_balance_and_partition():
+    from iddgcn_amd.parallel import node_ranges, node_shard_triples
+    rng = np.random.default_rng(3)
+    counts = np.concatenate([rng.integers(0, 30, 700), rng.integers(50, 150, 200)])     # mutation / drug tails
+    for w in (1, 2, 3, 8):
+        cuts = node_ranges(counts, w, node_weight=4.0)
+        assert cuts[0] == 0 and cuts[-1] == len(counts) and all(a <= b for a, b in zip(cuts, cuts[1:]))
+        work = [counts[a:b].sum() + 4.0 * (b - a) for a, b in zip(cuts, cuts[1:])]
+        assert max(work) <= sum(work) / w + 150 + 4.0             # within one row of the balanced share
+    tri = np.stack([rng.integers(0, 900, 5000), rng.integers(0, 2, 5000), rng.integers(0, 900, 5000)], 1)
+    cuts = node_ranges(np.bincount(tri[:, 2], minlength=900), 3)
+    parts = [node_shard_triples(tri, None, cuts, r)[0] for r in range(3)]
+    assert sum(len(p) for p in parts) == len(tri)
+    for r, p in enumerate(parts):
+        assert np.all((p[:, 2] >= cuts[r]) & (p[:, 2] < cuts[r + 1]))
+
+
+def _node_shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from iddgcn_amd.parallel import NodeShard
+        cuts = [0, 5, 5, 12][:world + 1] if world == 3 else [0, 7, 12]
+        sh = NodeShard(cuts)
+        N, C = cuts[-1], 3
+        # all-gather: each rank fills its rows with rank-specific values
+        tab = torch.full((N, C), -1.0)
+        tab[sh.a:sh.b] = torch.arange(sh.a, sh.b, dtype=torch.float32)[:, None] * 10 + torch.arange(C)
+        sh.all_gather(tab)
+        # reduce-scatter: every rank holds partials (rank + 1) * row index; owners get the sums
+        part = (rank + 1) * torch.arange(N, dtype=torch.float32)[:, None].repeat(1, C)
+        sh.reduce_scatter(part)
+        q.put((rank, tab.numpy(), part[sh.a:sh.b].numpy(), (sh.a, sh.b)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_node_shard_collectives_gloo(world):
+    """NodeShard.all_gather / reduce_scatter on (N, C) tables with UNEQUAL row ranges (one empty at world 3):
+    after the all-gather every rank holds every rank's rows; after the reduce-scatter each owner holds the sums
+    of the ranks' partials for its rows."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_node_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    N = 12
+    want = np.arange(N, dtype=np.float32)[:, None] * 10 + np.arange(3)
+    tot = sum(range(1, world + 1))
+    for rank, tab, mine, (a, b) in res:
+        assert np.array_equal(tab, want)
+        assert np.array_equal(mine, tot * np.arange(a, b, dtype=np.float32)[:, None].repeat(3, 1))

@@ -120,7 +120,7 @@ def test_fit_world2_gloo_one_gpu_equals_single_process(cuda):
         assert np.abs(g0[k] - g).max() <= 2e-4 * np.abs(g).max() + 1e-30, k
 
 
-def _step_worker(rank, world, port, q, mode, N, R, D):
+def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact"):
     """One data-parallel step (forward + backward + bucketed all-reduce, no Adam) on this rank's shard of
     the scored edges, edge-partitioned or with relation-sharded node tables.  "edge_device": the
     bucketed all-reduce on its device branch (asynchronous, in place on the GPU buckets, ordered after
@@ -136,7 +136,12 @@ def _step_worker(rank, world, port, q, mode, N, R, D):
         tri = np.concatenate([pos, neg])
         lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
         lo, hi = shard_range(len(tri), rank, world)
-        eng = Engine(N, R, D, dev)
+        eng = Engine(N, R, D, dev, gemm=gemm)
+        if mode == "node":
+            from iddgcn_amd.parallel import NodeShard, node_ranges, node_shard_triples
+            cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
+            eng.row_shard = NodeShard(cuts)
+            mine, mlab = node_shard_triples(tri, lab, cuts, rank)
         if mode == "relation":
             eng.node_shard = RelationShard(R, N)
         elif mode == "spmm":
@@ -144,7 +149,7 @@ def _step_worker(rank, world, port, q, mode, N, R, D):
         P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
         P.load(_mild(N, R, D, 9))
         adj = eng.adjacency(get_adj_mats(pos, N, R))
-        ed = eng.edges(tri[lo:hi], lab[lo:hi])
+        ed = eng.edges(mine, mlab) if mode == "node" else eng.edges(tri[lo:hi], lab[lo:hi])
         comm = BucketedAllReduce(min_bucket_rows=64, host_staged=False if mode == "edge_device" else None)
         ws = eng.workspace(ed.T, True)
         eng._t_global = len(tri)
@@ -217,3 +222,39 @@ def test_bwd_columns_partition_sums_to_full(cuda):
     assert nnz == adj.bwd_col.numel()
     torch.cuda.synchronize()
     assert (acc - full).abs().max().item() <= 1e-5 * full.abs().max().item()
+
+
+@pytest.mark.parametrize("world,N,R,D,gemm", [(2, 600, 2, 64, "exact"), (3, 601, 3, 256, "exact"),
+                                              (2, 700, 2, 256, "bf16x3"), (3, 650, 2, 256, "split")])
+def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, cuda):
+    """Node-row partitioning (parallel.NodeShard, round 4): rank k owns a contiguous node range (balanced by tail
+    edges + node work), computes the node tables of its rows only, takes the scored edges whose tail it owns;
+    W^l and X^3 are all-gathered, the head seeds dO^3 and the dWedge head sums reduce-scattered, every gradient
+    all-reduced.  world 2 and 3 ranks on one GPU over gloo: the step's loss and every gradient equal the
+    single-process full batch (1e-5 of max|g|), bitwise equal on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pos, neg = synthetic_graph(N, R, 9000, seed=77)
+    tri = np.concatenate([pos, neg])
+    lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+    eng = Engine(N, R, D, cuda, gemm=gemm)
+    P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
+    P.load(_mild(N, R, D, 9))
+    loss, _ = eng.loss_and_grads(P, G, eng.adjacency(get_adj_mats(pos, N, R)), eng.edges(tri, lab))
+    full, full_loss = G.to_numpy(), float(loss.item())
+    del eng, P, G
+    port = _free_port()
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q, "node", N, R, D, gemm)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for o in out[1:]:
+        assert o[1] == out[0][1]
+        assert all(np.array_equal(o[2][k], out[0][2][k]) for k in full)
+    l, g = out[0][1], out[0][2]
+    assert abs(l - full_loss) <= 1e-6 * full_loss
+    for k, v in full.items():
+        assert np.abs(g[k] - v).max() <= 1e-5 * np.abs(v).max() + 1e-30, k
