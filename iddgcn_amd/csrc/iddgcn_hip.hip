@@ -423,22 +423,7 @@ __device__ __forceinline__ void dma_row_1k(const float* src_row, float* lds_row,
 //     MFMAs.  One barrier per tile (A buffers), raw s_barrier so the slab DMA of
 //     the next tile stays in flight across it.
 // ---------------------------------------------------------------------------
-#ifndef V3_STAGGER
-#define V3_STAGGER 1
-#endif
-#ifndef V3_PRIO
-#define V3_PRIO 0
-#endif
 // ablation switches for the GEMM microbenchmark (never set in the product build)
-#ifndef V3_ABL
-#define V3_ABL 0
-#endif
-#ifndef V3_CAP2
-#define V3_CAP2 0
-#endif
-#ifndef V3_COEF16
-#define V3_COEF16 1
-#endif
 namespace r3 {
 constexpr int D = 256, NW = 8, TR = 32;
 constexpr int ROWS_PER_WAVE = TR / NW;                 // A rows each wave stages
@@ -582,24 +567,21 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     static_assert(!C4 || (!X3 && NV == 0 && !AUX && !HAS_COEF), "C4: the f32 plain form (node projections)");
     static_assert(NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
     constexpr bool WIDE = NV > 2;                      // capped slabs, run-time R <= NV
-    // capped V slabs r >= 1 (rows past the cap read from L2): WIDE, and NV = 2 when V3_CAP2 > 0
-    constexpr bool CAPPED = WIDE || (V3_CAP2 > 0 && NV == 2);
+    // capped V slabs r >= 1 (rows past the cap read from L2): WIDE
+    constexpr bool CAPPED = WIDE;
     // the sigma' slab: after the V slabs; BF keeps it out of slab 0, whose fp32 staging of the output
     // would overwrite bf16 aux rows other lanes have not read yet (different row pitches)
     constexpr int AUXS = (BF && NV == 0) ? 1 : NV;
     constexpr int NS = AUX ? AUXS + 1 : NV;
     constexpr int NSL = NS > 1 ? NS : 1;               // slabs per wave (slab 0 also stages C)
     // Slab 0 holds 32 rows (it also stages the C tile); WIDE slabs r >= 1 hold GATHER_CAP rows.
-    constexpr int CAPV = WIDE ? GATHER_CAP : (CAPPED ? V3_CAP2 : 32);
+    constexpr int CAPV = WIDE ? GATHER_CAP : 32;
     constexpr int SLABC = CAPV * 32;
-    // WIDE forward, slot-major V (V3_SLOTV): the tile's distinct V rows as [slot][relation][32 columns] after
+    // WIDE forward, slot-major V: the tile's distinct V rows as [slot][relation][32 columns] after
     // slab 0, so ONE LDS-DMA instruction (64 lanes x 16 B, each lane its own relation row and 16-B group)
     // fetches a distinct row's 32 columns for all R <= 8 relations (two rows at R <= 4) instead of one
     // instruction per relation; CAPN slots in the bytes the capped per-relation slabs used
-#ifndef V3_SLOTV
-#define V3_SLOTV 1
-#endif
-    constexpr bool SLOTV = WIDE && !AUX && V3_SLOTV;
+    constexpr bool SLOTV = WIDE && !AUX;
     constexpr int RPI = WIDE ? 64 / (NV * 8) : 1;      // distinct rows per DMA instruction (SLOTV)
     constexpr int CAPN = WIDE ? ((NSL - 1) * SLABC) / (NV * 32) / RPI * RPI : 0;
     static_assert(!SLOTV || CAPN >= 2, "slot-major V: at least two distinct rows");
@@ -623,7 +605,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     __shared__ __attribute__((aligned(16))) float lds[LDSF];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool late = V3_STAGGER && wave >= 4;         // staggered half
+    const bool late = wave >= 4;         // staggered half
     const int i = lane & 31, h = lane >> 5;
     const int c0 = wave * 32;
     float* bufA = lds;
@@ -682,7 +664,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // [hi plane 512 B | lo plane 512 B] (k-natural order), and records 1/scale per row
     auto convert_rows = [&](int bb) __attribute__((always_inline)) {
         if constexpr (X3 && !BF) {
-            if ((V3_ABL & 16) || (p.planes & IDDGCN_PLANES_A)) {   // rows arrive split (fixed scale)
+            if (p.planes & IDDGCN_PLANES_A) {   // rows arrive split (fixed scale)
                 if (lane < ROWS_PER_WAVE) rowinv[bb * TR + wave * ROWS_PER_WAVE + lane] = PLANE_INV;
                 return;
             }
@@ -742,7 +724,6 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // load is ever left in flight across the pipelined LDS-DMA code (the compiler would otherwise guard
     // its result with a vmcnt(0) that also drains every DMA in flight).
     auto dma_A = [&](long long t, int b) __attribute__((always_inline)) {
-        if (V3_ABL & 64) return;
         int sa[ROWS_PER_WAVE];
         if (p.a_idx) {
             const int v = lane < ROWS_PER_WAVE ? p.a_idx[clampe(t * TR + wave * ROWS_PER_WAVE + lane)] : 0;
@@ -774,8 +755,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     // slot of its row for the epilogue (vslot).
     int* cmpw = idxw + r3::IDX;
     auto dma_slabs = [&](long long t) __attribute__((always_inline)) {
-        if (V3_ABL & 1) return;
-        if (NV > 0 && !(V3_ABL & 256)) {
+        if (NV > 0) {
             int vi = 0;
             bool start = false;
             if (lane < 32) {
@@ -845,7 +825,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                 }
             }
         }
-        if (HAS_COEF && !(V3_ABL & 128) && COEF_WIDE && V3_COEF16 && (R == 4 || R == 8) && !p.coef_idx) {
+        if (HAS_COEF && COEF_WIDE && (R == 4 || R == 8) && !p.coef_idx) {
             // per-edge coefficients (no coef_idx): the tile's 32 x R values are one contiguous block, one
             // 16-B DMA per lane (R = 8: 1 instruction instead of 4, and no per-lane q / R divisions); lanes
             // past the array's end re-read its last 16 B (those rows are past M and never stored)
@@ -854,7 +834,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
             if (off > last) off = last;
             if (lane < 8 * R)
                 __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + off), (lds_vptr)coefw, 16, 0, 0);
-        } else if (HAS_COEF && !(V3_ABL & 128)) {
+        } else if (HAS_COEF) {
             // 32 x R coefficients, 64 per DMA instruction (R <= 2: one instruction)
             for (int k0 = 0; k0 < TR * R; k0 += 64) {
                 const float* g = p.coef;             // lanes past 32*R read a valid dummy
@@ -923,7 +903,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                 if (p.accumulate)
                     v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rc, (i * D + col) * 4, 0, 0));
             }
-            if (NV > 0 && !(V3_ABL & 2)) {
+            if (NV > 0) {
                 // (SLOTV: a slot past CAPN reads slot 0's words, then takes the L2 row below)
                 const int offv = SLOTV ? SLAB + (vslot < CAPN ? vslot : 0) * NV * 32 + 4 * ((2 * j + h) ^ (vslot & 7))
                                        : vslot * 32 + 4 * ((2 * j + h) ^ ((vslot >> 1) & 7));
@@ -953,7 +933,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                     for (int q = 0; q < 4; ++q) v[q] = fmaf(cf[r], s[q], v[q]);
                 }
             }
-            if (p.act == IDDGCN_ACT_SIGMOID && !(V3_ABL & 8)) {
+            if (p.act == IDDGCN_ACT_SIGMOID) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
             } else if (AUX && p.act == IDDGCN_ACT_DSIGMOID) {
@@ -979,10 +959,6 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
         for (int k = 0; k < 4; ++k) {
             const int row = 8 * k + (lane >> 3), cg = lane & 7;
             const f32x4 o = ld4(slabw + row * 32 + 4 * (cg ^ ((row >> 1) & 7)));
-            if (V3_ABL & 4) {
-                asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
-                continue;
-            }
             if constexpr (BF) {
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, f32_to_bf4(o)), rc,
                                                       (row * D + c0 + cg * 4) * 2, 0, 0);
@@ -1109,7 +1085,7 @@ _Pragma("unroll") \
                 ah[0] = __builtin_bit_cast(f16x8, ld4(arow)); \
                 al[0] = __builtin_bit_cast(f16x8, ld4(arow + 16)); \
 _Pragma("unroll") \
-                for (int q = 0; q < ((V3_ABL & 32) ? 0 : D / 16); ++q) { \
+                for (int q = 0; q < D / 16; ++q) { \
                     const int cu = q & 1; \
                     if (q + 1 < D / 16) { \
                         const int qo = 32 * ((q + 1) >> 1) + 8 * ((q + 1) & 1); \
@@ -1159,7 +1135,6 @@ _Pragma("unroll") \
             epilogue(t_end - 1, acc); \
         } \
     }
-    if (V3_PRIO && late) __builtin_amdgcn_s_setprio(1);
     if (late) V3_MAIN_LOOP(true) else V3_MAIN_LOOP(false)
 #undef V3_MAIN_LOOP
 }
@@ -1372,9 +1347,6 @@ __global__ __launch_bounds__(512) void gemm_tn256_dma_kernel(long long M, long l
 // hi*hi + hi*lo + lo*hi with lo = fp16(x*s - hi) (same units; a lo below the fp16 normal range
 // only loses bits below 2^-38 of the block max).
 // ---------------------------------------------------------------------------
-#ifndef TN_ABL
-#define TN_ABL 0            // experiment builds only: 1 skip the B conversion, 2 skip the MFMAs, 4 skip the tile DMA
-#endif
 namespace tn3 {
 constexpr int D = 256, TK = 32, LDR = D + 4, TILE = TK * LDR;
 constexpr float S_INIT = 0x1p126f;                       // pow2_scale(0): "no data yet"
@@ -1443,7 +1415,6 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
     const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
 
     auto stage = [&](long long t, int b) {
-        if (TN_ABL & 4) return;
         float* As = lds + b * BUF;
         float* Bs = As + TILE_A;
 #pragma unroll
@@ -1493,7 +1464,6 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
         *reinterpret_cast<f16x8*>(seg + 64 + 32 * h + 16) = lv[1];
     };
     auto convert = [&](int b) {
-        if (TN_ABL & 1) return;
         if constexpr (!PA) convert_block(lds + b * BUF, sA, true);
         convert_block(lds + b * BUF + TILE_A, sBrun, false);
         if (lane == 0) sBpub[b * 8 + wave] = sBrun;
@@ -1531,7 +1501,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
         const char* Atr = reinterpret_cast<const char*>(lds + b * BUF) + ((8 * h + ((lane >> 2) & 3)) * LDRA) * 4 +
                           128 * wave + 32 * ((lane >> 4) & 1) + 8 * (lane & 3);
 #pragma unroll
-        for (int s = 0; s < ((TN_ABL & 2) ? 0 : TK / 16); ++s) {
+        for (int s = 0; s < TK / 16; ++s) {
             f16x8 ah, al;
             if constexpr (PA) {
                 const char* r0 = Atr + (16 * s) * LDRA * 4;
@@ -1706,27 +1676,13 @@ __device__ __forceinline__ void split3x2(float x0, float x1, unsigned& p0, unsig
     p2 = cvt_pk_bf16(s0, s1);
 }
 __device__ __forceinline__ void split3x4(const f32x4& v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
-#ifndef B3_PAIRSPLIT
-#define B3_PAIRSPLIT 1
-#endif
-    if constexpr (B3_PAIRSPLIT) {
-        unsigned a0, b0, c0, a1, b1, c1;
-        split3x2(v[0], v[1], a0, b0, c0);
-        split3x2(v[2], v[3], a1, b1, c1);
-        const u32x2 a = {a0, a1}, b = {b0, b1}, c = {c0, c1};
-        p0 = __builtin_bit_cast(bf16x4, a);
-        p1 = __builtin_bit_cast(bf16x4, b);
-        p2 = __builtin_bit_cast(bf16x4, c);
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            __bf16 a, b, c;
-            split3(v[q], a, b, c);
-            p0[q] = a;
-            p1[q] = b;
-            p2[q] = c;
-        }
-    }
+    unsigned a0, b0, c0, a1, b1, c1;
+    split3x2(v[0], v[1], a0, b0, c0);
+    split3x2(v[2], v[3], a1, b1, c1);
+    const u32x2 a = {a0, a1}, b = {b0, b1}, c = {c0, c1};
+    p0 = __builtin_bit_cast(bf16x4, a);
+    p1 = __builtin_bit_cast(bf16x4, b);
+    p2 = __builtin_bit_cast(bf16x4, c);
 }
 // a staged fp32 row of 256 values (bytes [0, 1024) of `row`) -> its three bf16 planes in place: plane j at
 // bytes [512 j, 512 j + 512), column k at byte 2k of its plane.  The wave's one ds_read_b128 of the whole row
@@ -1754,12 +1710,6 @@ __device__ __forceinline__ void row_to_planes3(char* row, int lane) {
 //   * epilogue as the v3 kernel: gathered P_r[t] rows (the tile's distinct tails), per-edge coefficients
 //     and sigma' rows (or, accumulating, the old C rows) DMA'd into wave-private slabs ([32][16] fp32, XOR-swizzled 16-B groups); waves 4-7 run
 //     the epilogue of tile t-1 while waves 0-3 run tile t's MFMAs on the same SIMDs; one barrier per tile.
-#ifndef B3_ABL
-#define B3_ABL 0     // experiment builds only: 1 skip the MFMAs, 2 skip the A DMA, 4 skip the conversion, 8 skip stores
-#endif
-#ifndef B3_PF
-#define B3_PF 2      // L2 prefetch of the A tile this many tiles beyond the one being DMA'd (0: none)
-#endif
 // s_waitcnt vmcnt(min(n, 15)) for a run-time, wave-uniform n: every vector-memory op of this wave but the n
 // youngest has completed (LDS-DMA, loads and stores count together, in issue order)
 __device__ __forceinline__ void wait_vm(int n) {
@@ -1777,6 +1727,7 @@ constexpr int PITCH = 1568;                 // A row slot: three 512-B planes + 
 constexpr int ABYTES = TR * PITCH;          // 50,176 B per A buffer (two buffers)
 constexpr int RPW = TR / NW;                // A rows each wave stages and converts
 constexpr int SLAB = TR * CWV;              // floats of a [32 rows][16 columns] slab
+constexpr int PF = 2;                       // L2 prefetch of the A tile this many tiles beyond the one being DMA'd
 }  // namespace rb3
 // float offset of (slot, 16-B column group g) in a [32][16] slab: groups XOR (-(slot / 4)) & 3, so the
 // epilogue's ds_read_b128 (slot l&15 [+16], group l>>4) is conflict-free in each of its four lane groups
@@ -1849,7 +1800,7 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
 #pragma unroll
         for (int j = 0; j < RPW; ++j) {
             const int r = wave * RPW + j;
-            const float* src = p.A + ((B3_ABL & 2) ? (long long)r : clampe(t * TR + r)) * D + lane * 4;
+            const float* src = p.A + clampe(t * TR + r) * D + lane * 4;
             __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(lds + bb * ABYTES + r * PITCH), 16, 0, 0);
         }
         return RPW;
@@ -1857,13 +1808,12 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
     // L2 prefetch of this wave's 4 A rows of tile t: one DMA, a 16-B read per 64 B (16 lanes per row) into a
     // wave-private scratch KiB of LDS that nothing reads; the later A DMA of the tile then hits L2
     auto prefetch = [&](long long t) __attribute__((always_inline)) -> int {
-        if (B3_PF == 0 || (B3_ABL & 2) || t >= t_end) return 0;
+        if (t >= t_end) return 0;
         const float* src = p.A + clampe(t * TR + wave * RPW + (lane >> 4)) * D + (lane & 15) * 16;
         __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)pfw, 16, 0, 0);
         return 1;
     };
     auto convert = [&](int bb) __attribute__((always_inline)) {
-        if (B3_ABL & 4) return;
 #pragma unroll
         for (int j = 0; j < RPW; ++j) row_to_planes3(lds + bb * ABYTES + (wave * RPW + j) * PITCH, lane);
     };
@@ -1963,10 +1913,9 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = v[q] * (x[q] * (1.0f - x[q]));
             }
-            if (B3_ABL & 8) asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
-            else __builtin_amdgcn_raw_buffer_store_b128(v, rc, (row * D + c0 + 4 * g) * 4, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rc, (row * D + c0 + 4 * g) * 4, 0, 0);
         }
-        return (B3_ABL & 8) ? 0 : 2;
+        return 2;
     };
     auto mfma_tile = [&](int bb, f32x4 (&acc)[2]) __attribute__((always_inline)) {
         f32x4 hi0 = {0.f, 0.f, 0.f, 0.f}, lo0 = hi0, hi1 = hi0, lo1 = hi0;
@@ -1988,9 +1937,9 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
                        "i"(64 * (Q) + 16 * PITCH), "i"(64 * (Q) + 16 * PITCH + 512),                      \
                        "i"(64 * (Q) + 16 * PITCH + 1024)                                                 \
                      : "memory")
-        if (!(B3_ABL & 1)) B3_LOADQ(0, 0);
+        B3_LOADQ(0, 0);
 #pragma unroll
-        for (int q = 0; q < ((B3_ABL & 1) ? 0 : 8); ++q) {
+        for (int q = 0; q < 8; ++q) {
             const int S = q & 1;
             if (q + 1 < 8) {
                 switch (q) {      // the offsets are immediates: one asm per k-step
@@ -2041,10 +1990,10 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
     convert(0);
     dma_idx(t_beg + 1);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    for (int k = 1; k <= B3_PF; ++k) prefetch(t_beg + k);
+    for (int k = 1; k <= PF; ++k) prefetch(t_beg + k);
     __syncthreads();
 
-    // per iteration t: A(t+1) DMA, then the L2 prefetch of A(t+1+B3_PF); waves 4-7 run epilogue(t-1) and the slab /
+    // per iteration t: A(t+1) DMA, then the L2 prefetch of A(t+1+PF); waves 4-7 run epilogue(t-1) and the slab /
     // index DMAs of t, t+1 before MFMA(t), waves 0-3 epilogue(t) and those of t+1, t+2 after it
 #define B3_MAIN_LOOP(LATE)                                                                           \
     {                                                                                                \
@@ -2053,7 +2002,7 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
         for (long long t = t_beg; t < t_end; ++t) {                                                  \
             const bool more = t + 1 < t_end;                                                         \
             const int nA = dma_A(t + 1, b ^ 1);                                                      \
-            const int npf = prefetch(t + 1 + B3_PF);                                                 \
+            const int npf = prefetch(t + 1 + PF);                                                 \
             int after_A = npf;                      /* ops issued after A(t+1) */                    \
             if (LATE && t > t_beg) {                                                                 \
                 wait_vm(nA + npf);                  /* slabs(t-1), idx(t) */                         \
@@ -2095,520 +2044,6 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
 #undef B3_MAIN_LOOP
 }
 
-// ---- row GEMM, bf16x3 operands on 32 x 32 x 16 MFMAs (round 4): C = epilogue(A B) over T rows -------------
-// One wave per SIMD (256-thread workgroups), 32 output columns per wave.  The weight's three bf16 planes of
-// those columns are 192 registers per lane, which the 512-entry register file of a lone wave holds beside two
-// accumulator pairs; a workgroup owns one 128-column half, the two halves of a row range run 8 workgroups
-// apart (workgroup b -> XCD b mod 8: the same XCD, so the second read of an A tile is an L2 hit).
-//   * v_mfma_f32_32x32x16_bf16 with the weight planes as operand A (32 columns x 16 k) and the A tile as
-//     operand B (16 k x 32 rows): lane l ends with edge row l&31, columns c0 + 8q + 4(l>>5) + {0..3}, q = 0..3.
-//     The MFMA holds the SIMD's vector issue for 8 of its 32 cycles (the 16x16x32 form of the round-3 kernel:
-//     8 of 16), so 3/4 of the MFMA phase's issue slots are left to the same wave's operand conversion,
-//     epilogue and DMA issue — the round-3 kernel was vector-issue bound (2 waves x (96 MFMA x 8 + 241 VALU x 4)
-//     cycles per SIMD per tile against 3072 MFMA cycles).
-//   * Each wave's fragment reads serve 32 columns: 192 KB of LDS reads per 32-row tile per CU instead of 384.
-//   * A rows (fp32) arrive by LDS-DMA into 1552-B row slots (388 dwords = 4 mod 64 banks: the 16 rows of every
-//     16-lane group of a fragment ds_read_b128 are conflict-free) and each wave converts 8 of the tile's 32 rows
-//     in place to the three planes, one row per k-step in the second half of the MFMA phase.
-//   * Iteration t: the slab DMAs of tile t (the tile's distinct gathered rows, the per-row coefficients, the
-//     sigma' / old-C rows: double-buffered per wave), the index DMA of t+1, the A DMAs of t+1 and an L2
-//     prefetch of A(t+1+PF); the epilogue of t-1 beside k-steps 0..3 of MFMA(t); the conversion of A(t+1)
-//     beside k-steps 8..15.  One barrier per tile.  Every vmcnt wait is an exact compile-time count: the
-//     conversion of row j of A(t+1) waits for everything but the ops issued after it (the younger A rows, the
-//     prefetch, the epilogue's 4 stores), which also covers the slab and index DMAs of the iteration.
-// Epilogue forms (template ACT): 0 none, 1 sigmoid, 2 sigma' (AUX: the aux rows), 3 accumulate (AUX: old C).
-namespace rw3 {
-constexpr int D = 256, NW = 4, TR = 32, CWG = 128, CWV = 32;
-constexpr int PITCH = 1552;                 // A row slot: three 512-B planes + 16 B
-constexpr int ABYTES = TR * PITCH;          // 49,664 B per A buffer (two buffers)
-constexpr int RPW = TR / NW;                // A rows each wave stages and converts
-constexpr int CAP = 16;                     // V-slab slots (distinct gathered rows) per relation; more: from L2
-constexpr int VSLAB = CAP * CWV;            // floats of a V slab [16 slots][32 columns]
-constexpr int XSLAB = TR * CWV;             // floats of an aux slab [32 rows][32 columns]
-constexpr int PF = 2;                       // L2 prefetch distance beyond the tile being DMA'd
-}  // namespace rw3
-// float offset of (slot, 16-B column group g) in a [slots][32] slab: groups XOR ((slot >> 1) & 7), so the
-// epilogue's ds_read_b128 (slot of row l&31, group 2q + (l>>5)) is conflict-free in each 16-lane group for any
-// 16 rows of distinct slot & 15 (and broadcast for equal slots)
-__device__ __forceinline__ int slab32_off(int slot, int g) { return slot * 32 + 4 * (g ^ ((slot >> 1) & 7)); }
-// explicit-address-space loads: an LDS read and a global read that the compiler may not merge into one FLAT load
-// (a FLAT op counts in both vmcnt and lgkmcnt, and its wait drains every DMA in flight)
-__device__ __forceinline__ f32x4 ld4_lds(const float* p) {
-    return *(const __attribute__((address_space(3))) f32x4*)(p);
-}
-__device__ __forceinline__ float ld_lds(const float* p) { return *(const __attribute__((address_space(3))) float*)(p); }
-__device__ __forceinline__ f32x4 ld4_gbl(const float* p) {
-    return *(const __attribute__((address_space(1))) f32x4*)(p);
-}
-// s_waitcnt vmcnt(N) for a compile-time N
-template <int N>
-__device__ __forceinline__ void wait_vm_c() {
-    static_assert(N >= 0 && N <= 63, "vmcnt");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int NV, bool AUX, bool BC, int ACT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void rowgemm256_b3w_kernel(RowGemmP p, int n_ranges) {
-    using namespace rw3;
-    static_assert(NV >= 0 && NV <= 2 && !(NV > 0 && (AUX || BC)), "b3w: gathered forward (NV = R = 1, 2), sigma' / accumulate (AUX), plain");
-    static_assert(!BC || NV == 0, "BC: one broadcast V row per relation (R <= 2), e.g. dz W_a^T");
-    static_assert(AUX == (ACT >= 2), "ACT 2 (sigma') and 3 (accumulate) read the aux slab");
-    // per wave (floats): two slab sets {NV V slabs, the aux slab, coefficients [32][R]}, idx [64], cmp [32],
-    // prefetch landing [256] (never read)
-    constexpr int SET = NV * VSLAB + (AUX ? XSLAB : 0) + 64;
-    constexpr int WF = 2 * SET + 64 + 32 + 256;
-    constexpr int LDSB = 2 * ABYTES + NW * WF * 4;
-    static_assert(LDSB <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(16))) char lds[LDSB];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int e = lane & 31, h = lane >> 5;
-    const int bx = blockIdx.x;
-    const int half = (bx >> 3) & 1;
-    const int range = ((bx >> 4) << 3) | (bx & 7);
-    if (range >= n_ranges) return;
-    const int c0 = half * CWG + wave * CWV;
-    float* wbase = reinterpret_cast<float*>(lds + 2 * ABYTES) + wave * WF;
-    int* idxw = reinterpret_cast<int*>(wbase + 2 * SET);
-    int* cmpw = idxw + 64;
-    float* pfw = reinterpret_cast<float*>(cmpw + 32);
-
-    const long long ntiles = ((long long)p.M + TR - 1) / TR;
-    const long long t_beg = (long long)range * p.tiles_per_block;
-    long long t_end = t_beg + p.tiles_per_block;
-    if (t_end > ntiles) t_end = ntiles;
-    if (t_beg >= t_end) return;
-    const long long Mlast = (long long)p.M - 1;
-    auto clampe = [&](long long x) __attribute__((always_inline)) { return x > Mlast ? Mlast : x; };
-    auto clampt = [&](long long t) __attribute__((always_inline)) { return t < t_end ? t : t_end - 1; };
-
-    // weight planes: k-step s (16 k), lane l: column c0 + (l&31), k = 16 s + 8 (l>>5) + j
-    bf16x8 w0[16], w1[16], w2[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = 16 * s + 8 * h + j;
-            const float wv = p.b_trans ? p.B[(c0 + e) * D + k] : p.B[k * D + c0 + e];
-            __bf16 a, b, c;
-            split3(wv, a, b, c);
-            w0[s][j] = a;
-            w1[s][j] = b;
-            w2[s][j] = c;
-        }
-    // BC: the broadcast V rows (v_row_stride 0: the same R <= 2 rows for every output row), this lane's columns
-    f32x4 vb[2][4];
-    if constexpr (BC) {
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                vb[r][q] = r < p.R ? ld4(p.V + r * p.v_rel_stride + c0 + 8 * q + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-
-    // ---- DMA issue sites (each returns its count of vector-memory ops) ----
-    auto dma_idx = [&](long long t) __attribute__((always_inline)) -> int {
-        if constexpr (NV == 0) {
-            return 0;
-        } else {
-            // identity rows (v_idx NULL): a harmless 4-B read keeps the count compile-time
-            const int* src = p.v_idx ? p.v_idx + clampe(t * TR + e) : reinterpret_cast<const int*>(p.A);
-            __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)idxw, 4, 0, 0);
-            return 1;
-        }
-    };
-    auto dma_A = [&](long long t, int bb) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            const int r = wave * RPW + j;
-            const float* src = p.A + clampe(t * TR + r) * D + lane * 4;
-            __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(lds + bb * ABYTES + r * PITCH), 16, 0, 0);
-        }
-    };
-    auto dma_A1 = [&](long long t, int bb, int j) __attribute__((always_inline)) {
-        const int r = wave * RPW + j;
-        const float* src = p.A + clampe(t * TR + r) * D + lane * 4;
-        __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(lds + bb * ABYTES + r * PITCH), 16, 0, 0);
-    };
-    // L2 prefetch of this wave's 8 A rows of tile t: a 16-B read per 128-B line into a scratch KiB of LDS
-    auto prefetch = [&](long long t) __attribute__((always_inline)) {
-        const float* src = p.A + clampe(clampt(t) * TR + wave * RPW + (lane >> 3)) * D + (lane & 7) * 32;
-        __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)pfw, 16, 0, 0);
-    };
-    // slabs of tile t into set `set`: the tile's distinct V rows (runs of equal v_idx: tail-sorted edges give 1-3
-    // per tile; identity rows give 32) into slots 0..min(u, CAP)-1; the slot and V row of this lane's row e
-    auto dma_slabs = [&](long long t, int set, int& vsl, int& vrow) __attribute__((always_inline)) {
-        float* sb = wbase + set * SET;
-        if constexpr (NV > 0) {
-            int vi = 0;
-            bool start = false;
-            if (lane < 32) {
-                const long long ee = clampe(t * TR + lane);
-                vi = p.v_idx ? ((const __attribute__((address_space(3))) int*)idxw)[lane] : (int)ee;
-                const int prev = p.v_idx ? ((const __attribute__((address_space(3))) int*)idxw)[lane > 0 ? lane - 1 : 0]
-                                         : (int)ee - 1;
-                start = lane == 0 || vi != prev;
-            }
-            const unsigned long long m = __ballot(start);
-            const int u = __popcll(m);
-            vsl = __popcll(m & ((2ull << e) - 1)) - 1;
-            if (start) cmpw[__popcll(m & ((2ull << lane) - 1)) - 1] = vi;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const __attribute__((address_space(3))) int* cmpl = (const __attribute__((address_space(3))) int*)cmpw;
-            vrow = cmpl[vsl];
-            const int un = u < CAP ? u : CAP;
-            for (int kb = 0; kb < un; kb += 8) {
-                const int slot = kb + (lane >> 3);
-                const int g = (lane & 7) ^ ((slot >> 1) & 7);
-                const long long v = cmpl[slot < u ? slot : u - 1];
-#pragma unroll
-                for (int r = 0; r < NV; ++r) {
-                    const float* src = p.V + r * p.v_rel_stride + v * D + c0 + 4 * g;
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(sb + r * VSLAB + kb * 32), 16, 0, 0);
-                }
-            }
-            // 32 x R per-edge coefficients, one 4-B DMA per lane (lanes past 32 R re-read the last value)
-            const long long last = (long long)p.M * NV - 1;
-            long long ci = t * TR * NV + lane;
-            if (ci > last) ci = last;
-            __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + ci), (lds_vptr)(sb + NV * VSLAB), 4, 0, 0);
-        }
-        if constexpr (BC) {
-            const long long last = (long long)p.M * p.R - 1;
-            long long ci = t * TR * p.R + lane;
-            if (ci > last) ci = last;
-            __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + ci), (lds_vptr)(sb + (AUX ? XSLAB : 0)), 4, 0, 0);
-        }
-        if constexpr (AUX) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int slot = 8 * k + (lane >> 3);
-                const int g = (lane & 7) ^ ((slot >> 1) & 7);
-                const float* src = p.aux + clampe(t * TR + slot) * D + c0 + 4 * g;
-                __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(sb + NV * VSLAB + k * 256), 16, 0, 0);
-            }
-        }
-    };
-    // The epilogue of tile t, quarter q (columns c0 + 8q + 4(l>>5) .. +3), in two halves one k-step apart: epi_load
-    // reads the accumulator pair and the LDS operands, epi_fin (a k-step later, the reads landed) combines, applies
-    // the activation and stores.  Rows whose gathered V row is past the slab's CAP slots take epi_fix afterwards.
-    struct EpiIn {
-        f32x4 v, x;
-        f32x4 sv[NV > 0 ? NV : 1];
-        float cf[(NV > 0 || BC) ? 2 : 1];
-    };
-    auto epi_load = [&](int set, int vsl, const f32x16& hi, const f32x16& lo, int q, EpiIn& in)
-        __attribute__((always_inline)) {
-        const float* sb = wbase + set * SET;
-        const int g = 2 * q + h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) in.v[i] = hi[4 * q + i] + lo[4 * q + i];
-        if constexpr (NV > 0) {
-#pragma unroll
-            for (int r = 0; r < NV; ++r) {
-                in.cf[r] = ld_lds(sb + NV * VSLAB + e * NV + r);
-                in.sv[r] = ld4_lds(sb + r * VSLAB + slab32_off(vsl < CAP ? vsl : CAP - 1, g));
-            }
-        }
-        if constexpr (BC) {
-            const float* cb = sb + (AUX ? XSLAB : 0) + e * p.R;
-            in.cf[0] = ld_lds(cb);
-            in.cf[1] = p.R > 1 ? ld_lds(cb + 1) : 0.f;
-        }
-        if constexpr (ACT >= 2) in.x = ld4_lds(sb + NV * VSLAB + slab32_off(e, g));
-    };
-    auto epi_act_store = [&](long long t, int q, f32x4 v, const f32x4& x) __attribute__((always_inline)) {
-        if constexpr (ACT == 1) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = sigmoid_fast(v[i]);
-        } else if constexpr (ACT == 2) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = v[i] * (x[i] * (1.0f - x[i]));
-        } else if constexpr (ACT == 3) {
-            v += x;
-        }
-        const long long row0 = t * TR;
-        const long long left = (long long)p.M - row0;
-        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
-        const __amdgpu_buffer_rsrc_t rc =
-            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(p.C) + row0 * D * 4, (short)0, nbytes, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rc, (e * D + c0 + 8 * q + 4 * h) * 4, 0, 0);
-    };
-    auto epi_fin = [&](long long t, int q, const EpiIn& in) __attribute__((always_inline)) {
-        f32x4 v = in.v;
-        if constexpr (NV > 0) {
-#pragma unroll
-            for (int r = 0; r < NV; ++r)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = fmaf(in.cf[r], in.sv[r][i], v[i]);
-        }
-        if constexpr (BC) {
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = fmaf(in.cf[r], vb[r][q][i], v[i]);
-        }
-        epi_act_store(t, q, v, in.x);
-    };
-    // rows past the CAP slab slots (more than CAP distinct gathered rows in the tile: identity or random rows):
-    // recompute their four quarters with the V rows read from L2 and store again (same lane, same address: the
-    // later store wins).  Tail-sorted edge tiles never take it.
-    auto epi_fix = [&](long long t, int set, int vsl, int vrow, const f32x16& hi, const f32x16& lo)
-        __attribute__((always_inline)) {
-        if constexpr (NV > 0) {
-            if (__ballot(vsl >= CAP) == 0) return;
-            if (vsl >= CAP) {
-                const float* sb = wbase + set * SET;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int g = 2 * q + h;
-                    f32x4 v;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) v[i] = hi[4 * q + i] + lo[4 * q + i];
-#pragma unroll
-                    for (int r = 0; r < NV; ++r) {
-                        const float cf = ld_lds(sb + NV * VSLAB + e * NV + r);
-                        const f32x4 sv = ld4_gbl(p.V + r * p.v_rel_stride + (long long)vrow * D + c0 + 4 * g);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) v[i] = fmaf(cf, sv[i], v[i]);
-                    }
-                    epi_act_store(t, q, v, f32x4{0.f, 0.f, 0.f, 0.f});
-                }
-            }
-        }
-    };
-    // the A-row conversion, split so that the fp32 row is read one k-step before it is converted and written
-    auto conv_read = [&](int bb, int j) __attribute__((always_inline)) -> f32x4 {
-        return ld4_lds(reinterpret_cast<const float*>(lds + bb * ABYTES + (wave * RPW + j) * PITCH) + lane * 4);
-    };
-    auto conv_write = [&](int bb, int j, const f32x4& x) __attribute__((always_inline)) {
-        typedef __attribute__((address_space(3))) bf16x4* lbf4;
-        char* row = lds + bb * ABYTES + (wave * RPW + j) * PITCH;
-        bf16x4 p0, p1, p2;
-        split3x4(x, p0, p1, p2);
-        *(lbf4)(row + lane * 8) = p0;
-        *(lbf4)(row + 512 + lane * 8) = p1;
-        *(lbf4)(row + 1024 + lane * 8) = p2;
-    };
-
-    const unsigned ab0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds + e * PITCH + 16 * h;
-#define W3_LOAD(S, B)                                                                                     \
-    asm volatile("ds_read_b128 %0, %3 offset:%4\n\tds_read_b128 %1, %3 offset:%5\n\tds_read_b128 %2, %3 offset:%6" \
-                 : "=v"(fr[B][0]), "=v"(fr[B][1]), "=v"(fr[B][2])                                          \
-                 : "v"(ab), "i"(32 * (S)), "i"(32 * (S) + 512), "i"(32 * (S) + 1024)                       \
-                 : "memory")
-    constexpr int NIDX = NV > 0 ? 1 : 0;
-
-    // One tile: MFMA(t) on buffer bb into (hi, lo); beside it the epilogue of t-1 (from (phi, plo), slab set bb^1),
-    // the slab DMAs of t (set bb), the index DMA of t+1, the A DMAs of t+1 into buffer bb^1 and their conversion.
-    // Program order of the vector-memory ops: slabs(t) | A(t+1) rows 0-3 [+ store q0] (k-step 0) | rows 4-7 [+ store
-    // q0] (1) | idx(t+1), prefetch, stores q1..q3 (2..4).  Before the conversion reads (k-step 7) every A row must
-    // have landed: only the ops of k-steps 2..4 are surely younger (idx, prefetch, 3 stores), so vmcnt(NIDX + 1 +
-    // 3); that wait also covers slabs(t) and idx(t+1)'s predecessor for the next iteration.
-    auto tile = [&](auto first_c, long long t, int bb, f32x16& hi, f32x16& lo, const f32x16& phi, const f32x16& plo,
-                    int& vsl_cur, int& vrow_cur, int vsl_prev, int vrow_prev) __attribute__((always_inline)) {
-        constexpr bool FIRST = decltype(first_c)::value;
-        constexpr int WAIT_A = NIDX + 1 + (FIRST ? 0 : 3);
-        const int set = bb;
-        dma_slabs(t, set, vsl_cur, vrow_cur);
-        const unsigned ab = ab0 + bb * ABYTES;
-        u32x4 fr[2][3];
-        EpiIn ein = {};
-        f32x4 xr = {0.f, 0.f, 0.f, 0.f};
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        W3_LOAD(0, 0);
-        // conversion state of the A row being converted (read one k-step earlier), in four VALU chunks + writes
-        unsigned cp0a = 0, cp1a = 0, cp2a = 0, cp0b = 0, cp1b = 0, cp2b = 0;
-        float cr0 = 0.f, cr1 = 0.f, cr2 = 0.f, cr3 = 0.f;
-        f32x4 ev = {0.f, 0.f, 0.f, 0.f};
-        // work placed after MFMA m (0..5) of k-step s; every chunk ends in an empty-asm fence on what it produced,
-        // and every MFMA result passes one: the fences are ordered volatile asm, so each chunk stays in its gap
-        auto slot = [&](int s, int m) __attribute__((always_inline)) {
-#ifndef W3_ABL
-#define W3_ABL 0
-#endif
-            if (!(W3_ABL & 4) && s == 0 && m < 4) dma_A1(clampt(t + 1), bb ^ 1, m);
-            if (!(W3_ABL & 4) && s == 1 && m < 4) dma_A1(clampt(t + 1), bb ^ 1, m + 4);
-            if (s == 2 && m == 0) dma_idx(t + 1);
-            if (s == 2 && m == 1) prefetch(t + 1 + PF);
-            if constexpr (!FIRST && !(W3_ABL & 8)) {
-                // epilogue of t-1: quarter q = s - 1 finishes in k-step s (1..4), quarter s is loaded in k-step s (0..3)
-                if (s >= 1 && s <= 4) {
-                    const int q = s - 1;
-                    if (m == 0) {
-                        ev = ein.v;
-                        if constexpr (NV > 0) {
-#pragma unroll
-                            for (int r = 0; r < NV; ++r)
-#pragma unroll
-                                for (int i = 0; i < 4; ++i) ev[i] = fmaf(ein.cf[r], ein.sv[r][i], ev[i]);
-                        }
-                        if constexpr (BC) {
-#pragma unroll
-                            for (int r = 0; r < 2; ++r)
-#pragma unroll
-                                for (int i = 0; i < 4; ++i) ev[i] = fmaf(ein.cf[r], vb[r][q][i], ev[i]);
-                        }
-                        asm volatile("" : "+v"(ev));
-                    } else if (m == 1 || m == 2) {
-#pragma unroll
-                        for (int i = 2 * (m - 1); i < 2 * m; ++i) {
-                            if constexpr (ACT == 1) ev[i] = sigmoid_fast(ev[i]);
-                            else if constexpr (ACT == 2) ev[i] = ev[i] * (ein.x[i] * (1.0f - ein.x[i]));
-                            else if constexpr (ACT == 3) ev[i] += ein.x[i];
-                        }
-                        asm volatile("" : "+v"(ev));
-                    } else if (m == 3) {
-                        const long long row0 = (t - 1) * TR;
-                        const long long left = (long long)p.M - row0;
-                        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
-                        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-                            reinterpret_cast<char*>(p.C) + row0 * D * 4, (short)0, nbytes, 0x00020000);
-                        __builtin_amdgcn_raw_buffer_store_b128(ev, rc, (e * D + c0 + 8 * q + 4 * h) * 4, 0, 0);
-                    }
-                }
-                if (s <= 3 && m == 4) epi_load(bb ^ 1, vsl_prev, phi, plo, s, ein);
-            }
-            if (s == 7 && m == 0) {
-                wait_vm_c<WAIT_A>();
-                xr = conv_read(bb ^ 1, 0);
-            }
-            if (s >= 8 && !(W3_ABL & 2)) {
-                if (m == 0) {          // pair (x0, x1): b0 and the first remainder
-                    cp0a = cvt_pk_bf16(xr[0], xr[1]);
-                    cr0 = xr[0] - __builtin_bit_cast(float, cp0a << 16);
-                    cr1 = xr[1] - __builtin_bit_cast(float, cp0a & 0xffff0000u);
-                    asm volatile("" : "+v"(cp0a), "+v"(cr0), "+v"(cr1));
-                } else if (m == 1) {   // pair (x0, x1): b1, b2
-                    cp1a = cvt_pk_bf16(cr0, cr1);
-                    const float s0 = cr0 - __builtin_bit_cast(float, cp1a << 16);
-                    const float s1 = cr1 - __builtin_bit_cast(float, cp1a & 0xffff0000u);
-                    cp2a = cvt_pk_bf16(s0, s1);
-                    asm volatile("" : "+v"(cp1a), "+v"(cp2a));
-                } else if (m == 2) {   // pair (x2, x3)
-                    cp0b = cvt_pk_bf16(xr[2], xr[3]);
-                    cr2 = xr[2] - __builtin_bit_cast(float, cp0b << 16);
-                    cr3 = xr[3] - __builtin_bit_cast(float, cp0b & 0xffff0000u);
-                    asm volatile("" : "+v"(cp0b), "+v"(cr2), "+v"(cr3));
-                } else if (m == 3) {
-                    cp1b = cvt_pk_bf16(cr2, cr3);
-                    const float s2 = cr2 - __builtin_bit_cast(float, cp1b << 16);
-                    const float s3 = cr3 - __builtin_bit_cast(float, cp1b & 0xffff0000u);
-                    cp2b = cvt_pk_bf16(s2, s3);
-                    asm volatile("" : "+v"(cp1b), "+v"(cp2b));
-                } else if (m == 4) {   // the three planes of row s - 8, then the fp32 read of the next row
-                    typedef __attribute__((address_space(3))) u32x2* lu2;
-                    char* row = lds + (bb ^ 1) * ABYTES + (wave * RPW + (s - 8)) * PITCH + lane * 8;
-                    *(lu2)(row) = u32x2{cp0a, cp0b};
-                    *(lu2)(row + 512) = u32x2{cp1a, cp1b};
-                    *(lu2)(row + 1024) = u32x2{cp2a, cp2b};
-                    if (s < 15) xr = conv_read(bb ^ 1, s - 7);
-                }
-            }
-        };
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const int S = s & 1;
-            if (W3_ABL & 16) asm volatile("" : "+v"(fr[S][0]), "+v"(fr[S][1]), "+v"(fr[S][2])::"memory");
-            else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fr[S][0]), "+v"(fr[S][1]), "+v"(fr[S][2])::"memory");
-            // the LDS values read in the previous k-step and consumed in this one landed with the wait above: the
-            // empty asm "redefines" them, so the compiler sees no pending read (and places no wait) at their use
-            if (s >= 8) asm volatile("" : "+v"(xr));
-            if constexpr (!FIRST) {
-                if (s >= 1 && s <= 4) {
-                    asm volatile("" : "+v"(ein.v), "+v"(ein.x));
-#pragma unroll
-                    for (int r = 0; r < (NV > 0 ? NV : 1); ++r) asm volatile("" : "+v"(ein.sv[r]));
-#pragma unroll
-                    for (int r = 0; r < ((NV > 0 || BC) ? 2 : 1); ++r) asm volatile("" : "+v"(ein.cf[r]));
-                }
-            }
-            if (s + 1 < 16) {
-                switch (s) {
-                    case 0: W3_LOAD(1, 1); break;
-                    case 1: W3_LOAD(2, 0); break;
-                    case 2: W3_LOAD(3, 1); break;
-                    case 3: W3_LOAD(4, 0); break;
-                    case 4: W3_LOAD(5, 1); break;
-                    case 5: W3_LOAD(6, 0); break;
-                    case 6: W3_LOAD(7, 1); break;
-                    case 7: W3_LOAD(8, 0); break;
-                    case 8: W3_LOAD(9, 1); break;
-                    case 9: W3_LOAD(10, 0); break;
-                    case 10: W3_LOAD(11, 1); break;
-                    case 11: W3_LOAD(12, 0); break;
-                    case 12: W3_LOAD(13, 1); break;
-                    case 13: W3_LOAD(14, 0); break;
-                    default: W3_LOAD(15, 1); break;
-                }
-            }
-            const bf16x8 x0 = __builtin_bit_cast(bf16x8, fr[S][0]), x1 = __builtin_bit_cast(bf16x8, fr[S][1]),
-                         x2 = __builtin_bit_cast(bf16x8, fr[S][2]);
-            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[s], x2, s == 0 ? f32x16{} : lo, 0, 0, 0);
-            asm volatile("" : "+a"(lo));
-            slot(s, 0);
-            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2[s], x0, lo, 0, 0, 0);
-            asm volatile("" : "+a"(lo));
-            slot(s, 1);
-            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], x1, lo, 0, 0, 0);
-            asm volatile("" : "+a"(lo));
-            slot(s, 2);
-            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[s], x1, lo, 0, 0, 0);
-            asm volatile("" : "+a"(lo));
-            slot(s, 3);
-            if (!(W3_ABL & 1)) lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], x0, lo, 0, 0, 0);
-            asm volatile("" : "+a"(lo));
-            slot(s, 4);
-            if (!(W3_ABL & 1)) hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0[s], x0, s == 0 ? f32x16{} : hi, 0, 0, 0);
-            asm volatile("" : "+a"(hi));
-            slot(s, 5);
-        }
-        if constexpr (!FIRST) epi_fix(t - 1, bb ^ 1, vsl_prev, vrow_prev, phi, plo);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-
-    // prologue: indices and A of t_beg; A converted
-    dma_idx(t_beg);
-    dma_A(t_beg, 0);
-    for (int k = 1; k <= PF; ++k) prefetch(t_beg + k);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) row_to_planes3(lds + (wave * RPW + j) * PITCH, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    f32x16 hA, lA, hB, lB;
-    int vsA = 0, vrA = 0, vsB = 0, vrB = 0;
-    tile(std::integral_constant<bool, true>{}, t_beg, 0, hA, lA, hB, lB, vsA, vrA, vsB, vrB);
-    long long t = t_beg + 1;
-    for (; t + 1 < t_end; t += 2) {
-        tile(std::integral_constant<bool, false>{}, t, 1, hB, lB, hA, lA, vsB, vrB, vsA, vrA);
-        tile(std::integral_constant<bool, false>{}, t + 1, 0, hA, lA, hB, lB, vsA, vrA, vsB, vrB);
-    }
-    // the last tile's epilogue (its slabs: vmcnt(0)); the MFMA results: the waits below are no MFMA interlock,
-    // the s_nop pad is (32x32x16 result -> VALU read)
-    auto last_epi = [&](long long tl, int set, int vsl, int vrow, const f32x16& hi, const f32x16& lo)
-        __attribute__((always_inline)) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            EpiIn in;
-            epi_load(set, vsl, hi, lo, q, in);
-            epi_fin(tl, q, in);
-        }
-        epi_fix(tl, set, vsl, vrow, hi, lo);
-    };
-    if (t < t_end) {
-        tile(std::integral_constant<bool, false>{}, t, 1, hB, lB, hA, lA, vsB, vrB, vsA, vrA);
-        last_epi(t, 1, vsB, vrB, hB, lB);
-    } else {
-        last_epi(t - 1, (int)((t - 1 - t_beg) & 1), vsA, vrA, hA, lA);
-    }
-#undef W3_LOAD
-}
-
 // ---- TN reduction GEMM, bf16x3 operands: C = A^T B over M rows, partial per workgroup --------------------
 // Wave w owns output rows 32w..32w+31 (columns of A) x all 256 columns (8 accumulator tiles, 128 VGPRs).
 // 16-row tiles of A and B (one v_mfma_f32_32x32x16_bf16 k-step) arrive by LDS-DMA into 1600-B row slots,
@@ -2618,9 +2053,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // MFMAs per (k-step, column tile) into one fp32 accumulator, the smaller products first.  Waves 4-7 convert
 // tile t+1 before their MFMAs of tile t, waves 0-3 after theirs: a SIMD's two waves overlap conversion and
 // MFMA.  One barrier per tile.
-#ifndef TB3_ABL
-#define TB3_ABL 0    // experiment builds only: 2 skip the MFMAs, 4 skip the conversion, 8 skip the DMA
-#endif
 namespace tb3 {
 constexpr int D = 256, TK = 16, PT = 1600, OPB = TK * PT, BUF = 2 * OPB, NBUF = 3;
 }  // namespace tb3
@@ -2659,7 +2091,6 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
             const long long e = r_beg + t * TK + r;
             char* ra = lds + bb * BUF + r * PT;
             if (e < r_end) {
-                if (TB3_ABL & 8) continue;
                 __builtin_amdgcn_global_load_lds((gbl_vptr)(A + e * D + lane * 4), (lds_vptr)ra, 16, 0, 0);
                 __builtin_amdgcn_global_load_lds((gbl_vptr)(B + e * D + lane * 4), (lds_vptr)(ra + OPB), 16, 0, 0);
                 n += 2;
@@ -2671,7 +2102,6 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
         return n;
     };
     auto convert = [&](int bb) __attribute__((always_inline)) {
-        if (TB3_ABL & 4) return;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             char* ra = lds + bb * BUF + (2 * wave + j) * PT;
@@ -2709,14 +2139,12 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
             f32x16 c;
 #pragma unroll
             for (int j = 0; j < 16; ++j) c[j] = 0.f;
-            if (!(TB3_ABL & 2)) {
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
-                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[cj] + c, 0, 0, 0);
-            }
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
+            acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[cj] + c, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
             b0 = n0;
             b1 = n1;
@@ -2908,14 +2336,7 @@ __global__ __launch_bounds__(256) void combine_kernel(int M, const float* __rest
     }
     f32x4 yc[CU_ROWS], pc[RR][CU_ROWS];
     float wc[RR][CU_ROWS];
-#ifndef COMBINE_XCD
-#define COMBINE_XCD 0
-#endif
-    // XCD-aware order: blocks are dealt round-robin over the 8 XCDs, so logical block
-    // (b % 8) * (G / 8) + b / 8 gives each XCD a contiguous run of batches at every step
-    // (the tail rows they gather then live in ONE XCD's L2).
     long long bt = blockIdx.x;
-    if (COMBINE_XCD && (gstride & 7) == 0) bt = (long long)(blockIdx.x & 7) * (gstride >> 3) + (blockIdx.x >> 3);
     CB_LOAD_IDX(bt)
     CB_LOAD_ROWS(yc, pc, wc)
     CB_LOAD_IDX(bt + gstride)
@@ -3185,12 +2606,8 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                                                              float* __restrict__ loss_slab) {
     constexpr int LPR = D / 4;
     constexpr int GROUPS = 256 / LPR;
-#ifndef DM_UW
-#define DM_UW 4
-#endif
-#ifndef DM_SC_MINR
-#define DM_SC_MINR 2      // R = 2 too: 1.96 -> 1.84 ms at config 3 (tools/bench_tailseg.py), bitwise equal
-#endif
+    constexpr int DM_UW = 4;
+    constexpr int DM_SC_MINR = 2;     // R = 2 too: 1.96 -> 1.84 ms at config 3 (tools/bench_tailseg.py), bitwise equal
     // edges per group; the R >= DM_SC_MINR loop (one head per wave, next group prefetched) takes DM_UW
     constexpr int U = (64 / LPR == 1 && RT >= DM_SC_MINR) ? DM_UW : 4;
     __shared__ __attribute__((aligned(16))) float red[GROUPS * RT * D];
@@ -3275,9 +2692,7 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
             auto load_perm = [&](int k) __attribute__((always_inline)) {
                 return (sub < U && k + sub < len) ? perm[beg + k + sub] : -1;
             };
-#ifndef DM_PF2
-#define DM_PF2 1      // two groups in flight at R >= 4: config-5 shape 7.22 -> 6.91 ms; R = 2: +3%, not taken
-#endif
+            // two groups in flight at R >= 4: config-5 shape 7.22 -> 6.91 ms; R = 2: +3%, not taken
             // one group's indices (lane u: edge u), relations, labels and raw tail rows
             struct Grp {
                 int ev, rv;
@@ -3308,8 +2723,8 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                     else b[u] = G.bn[u];
                 }
             };
-            if constexpr (DM_PF2 && RT >= 4) {
-                // two groups in flight (DM_PF2): while group i is computed, the rows of groups i+1 and i+2
+            if constexpr (RT >= 4) {
+                // two groups in flight: while group i is computed, the rows of groups i+1 and i+2
                 // and the perm entries of group i+3 load; the group registers alternate between two sets
                 // (the loop is unrolled by two, so every index into them is static)
                 Grp GA, GB;
@@ -3474,20 +2889,13 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
                                                               float* __restrict__ dsum, float* __restrict__ dWedge) {
     constexpr int LPR = D / 4;
     constexpr int SLOTS = 64 / LPR;                     // edge slots per node (one wave per node)
-#ifndef TS_U
-#define TS_U 4
-#endif
+    constexpr int TS_U = 4;
 // R >= 4 (one node per wave, next group prefetched): 8 edge rows per group, i.e. U x R = 64 coefficients, one
 // per lane.  Rows in flight per wave are what this loop is bound by: at the config-5 shape (R = 8, bf16 rows,
 // degree 50) 4 -> 8 rows per group took a launch from 4.86 to 3.03 ms (tools/bench_tailseg.py)
-#ifndef TS_UW
-#define TS_UW 8
-#endif
+    constexpr int TS_UW = 8;
 // fp32 rows at R <= 2: nontemporal loads (the rows are read once; -2% at config 3, the probe's read-only
 // streams gain 10% from it); the R >= 4 loop with 8 rows in flight is slower with them (3.41 vs 3.03 ms)
-#ifndef TS_NT
-#define TS_NT 1
-#endif
     const long long n = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64;
     const int sub = threadIdx.x % LPR;
     const int slot = (threadIdx.x % 64) / LPR;
@@ -3495,9 +2903,7 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
     int beg = live ? seg_ptr[n] : 0, end = live ? seg_ptr[n + 1] : 0;
     // D = 256 with many relations: one node per wave, its edge rows (and W rows) wave-uniform, the R
     // coefficients of an edge through scalar loads (R = 8: -39%; at R <= 2 the vector loads are faster)
-#ifndef TS_PF_MINR
-#define TS_PF_MINR 4
-#endif
+    constexpr int TS_PF_MINR = 4;
     constexpr bool SCALAR = SLOTS == 1 && R >= TS_PF_MINR;
     constexpr int U = SCALAR ? TS_UW : TS_U;         // edge rows per group
     if constexpr (SCALAR) {
@@ -3521,7 +2927,7 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
             // h_idx == NULL: W is already per edge (W[e][r], gathered once per layer)
             hh[u] = a ? (h_idx ? h_idx[beg + k + u] : beg + k + u) : 0;
             if constexpr (SCALAR) hh[u] = __builtin_amdgcn_readfirstlane(hh[u]);     // scalar W loads
-            if constexpr (TS_NT && !BF)
+            if constexpr (!BF)
                 d[u] = a ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(dO + (long long)(beg + k + u) * D + sub * 4))
                          : f32x4{0.f, 0.f, 0.f, 0.f};
             else
@@ -3935,12 +3341,9 @@ int check_rowgemm(const iddgcn_rowgemm_t& a) {
 // The bf16x3 row GEMM's forms (rowgemm256_b3_kernel<NV, AUX, BC>): plain, C += A B, sigma' backward (AUX),
 // gathered-combine forward with exactly R = NV in {1, 2} per-edge coefficients, broadcast V with R <= 2 row
 // coefficients (BC, plain or sigma'); no a_idx, coef_idx or planes.
-#ifndef B3_DISABLE
-#define B3_DISABLE 0     // experiment builds only: 1 no bf16x3 row GEMM (exact instead), 2 no bf16x3 TN
-#endif
 bool b3_select(const RowGemmP& p, int& nv, bool& aux, bool& bc) {
     bc = false;
-    if ((B3_DISABLE & 1) || p.precision != IDDGCN_GEMM_BF16X3 || p.a_idx || p.planes) return false;
+    if (p.precision != IDDGCN_GEMM_BF16X3 || p.a_idx || p.planes) return false;
     if (p.R > 0 && p.v_row_stride == 0 && !p.v_idx) {
         // broadcast V (one row per relation for every output row: dz W_a^T), plain or with the sigma' factor
         if (p.R > 2 || p.coef_idx || p.accumulate || p.act == IDDGCN_ACT_SIGMOID) return false;
@@ -3962,9 +3365,6 @@ bool b3_select(const RowGemmP& p, int& nv, bool& aux, bool& bc) {
     return true;
 }
 // ~128 row ranges (a multiple of 8) x 2 column halves: one workgroup per CU, every one resident
-#ifndef B3W
-#define B3W 0
-#endif
 void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux, bool bc) {
     const long long nt = ((long long)p.M + rb3::TR - 1) / rb3::TR;
     long long nr = nt < 128 ? nt : 128;
@@ -3973,19 +3373,6 @@ void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux, bool bc) {
     nr = (nr + 7) / 8 * 8;
     const int n_ranges = (int)nr;
     if (p.accumulate) p.aux = p.C;
-    if (B3W) {
-        const dim3 g((unsigned)(2 * nr)), blk(256);
-        const bool sig = p.act == IDDGCN_ACT_SIGMOID;
-#define W3K(NV, AX, BCC, ACT) hipLaunchKernelGGL((rowgemm256_b3w_kernel<NV, AX, BCC, ACT>), g, blk, 0, st, p, n_ranges)
-        if (bc && aux) W3K(0, true, true, 2);
-        else if (bc) W3K(0, false, true, 0);
-        else if (nv == 1) { if (sig) W3K(1, false, false, 1); else W3K(1, false, false, 0); }
-        else if (nv == 2) { if (sig) W3K(2, false, false, 1); else W3K(2, false, false, 0); }
-        else if (aux) { if (p.accumulate) W3K(0, true, false, 3); else W3K(0, true, false, 2); }
-        else { if (sig) W3K(0, false, false, 1); else W3K(0, false, false, 0); }
-#undef W3K
-        return;
-    }
     const dim3 g((unsigned)(2 * nr)), blk(512);
     if (bc && aux) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, true, true>), g, blk, 0, st, p, n_ranges);
     else if (bc) hipLaunchKernelGGL((rowgemm256_b3_kernel<0, false, true>), g, blk, 0, st, p, n_ranges);
@@ -4280,7 +3667,7 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
-    if (d == 256 && precision == IDDGCN_GEMM_BF16X3 && !(B3_DISABLE & 2)) {
+    if (d == 256 && precision == IDDGCN_GEMM_BF16X3) {
         hipLaunchKernelGGL(gemm_tn256_b3_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
     } else if (d == 256 && precision == IDDGCN_GEMM_SPLIT_F16) {
         hipLaunchKernelGGL(gemm_tn256_x3_kernel<>, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab, TnBatch{});
