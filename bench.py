@@ -428,16 +428,18 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
     ap.add_argument("--also", nargs="*", default=None,
                     help="further workloads timed in the same run (min(steps, 5) steps, 1 warm-up), reported "
-                         "under 'also': config ids, 'Nn' = config N node-row partitioned, 'Nr' = with "
-                         "relation-sharded node tables, 'Ns' = with row-partitioned SpMMs; default 4 5 (BASELINE "
-                         "configs 4 and 5), plus 4n 5n 4r with more than one GPU; none to skip")
+                         "under 'also': config ids (with the run's --shard), 'Nn' = config N node-row partitioned, "
+                         "'Ne' = edge-partitioned, 'Nr' = with relation-sharded node tables, 'Ns' = with "
+                         "row-partitioned SpMMs; default 4 5 (BASELINE configs 4 and 5), plus 4e with more than one "
+                         "GPU; none to skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-planes", action="store_true",
                     help="fp32 tail tables x^1, x^2 instead of the pre-split planes form (A/B)")
-    ap.add_argument("--shard", default="edge", choices=["edge", "node", "relation", "spmm"],
-                    help="multi-GPU: edge partitioning only (default), node-row partitioning (node tables split by row "
-                         "range, scored edges by tail: parallel.NodeShard), also relation-sharded node tables, or also "
-                         "row-partitioned SpMMs (A_r E all-gathered, dAE reduce-scattered; node GEMMs replicated)")
+    ap.add_argument("--shard", default=None, choices=["edge", "node", "relation", "spmm"],
+                    help="multi-GPU: node-row partitioning (the default with more than one GPU: node tables split by "
+                         "row range, scored edges by tail, parallel.NodeShard), edge partitioning only (node work "
+                         "replicated), also relation-sharded node tables, or also row-partitioned SpMMs (A_r E "
+                         "all-gathered, dAE reduce-scattered; node GEMMs replicated)")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],
                     help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
     ap.add_argument("--gemm", default="bf16x3", choices=["exact", "bf16x3", "split"],
@@ -450,6 +452,10 @@ def main():
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
+    if args.shard is None:
+        # node-row partitioning beats edge partitioning at every config once there is more than one rank: the node
+        # work is divided instead of replicated (measured per-rank compute, collective volumes)
+        args.shard = "node" if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1 else "edge"
     rc = launch_ranks(args)
     if rc is not None:
         sys.exit(rc)
@@ -492,15 +498,15 @@ def main():
         result["world"] = world
         result["backend"] = dist.get_backend()
     also = []
-    todo = (["4", "5"] + (["4n", "5n", "4r"] if world > 1 else [])) if args.also is None else \
+    todo = (["4", "5"] + (["4e"] if world > 1 else [])) if args.also is None else \
         [a for a in args.also if a != "none"]
     for item in todo:
-        cid = int(item.rstrip("rsn"))
-        shard = {"r": "relation", "s": "spmm", "n": "node"}.get(item[-1], "edge")
+        cid = int(item.rstrip("rsne"))
+        shard = {"r": "relation", "s": "spmm", "n": "node", "e": "edge"}.get(item[-1], args.shard)
         if cid == args.config and shard == args.shard:
             continue
         name = CONFIGS[cid]["name"] + {"relation": "+relation-sharded", "spmm": "+row-partitioned-spmm",
-                                       "node": "+node-rows"}.get(shard, "")
+                                       "node": "+node-rows" if world > 1 else ""}.get(shard, "")
         if world > 1:
             # ranks decide TOGETHER whether the workload fits (a rank that ran out of memory alone would leave the
             # others waiting in a collective), then run it without recovery: any failure ends every rank

@@ -542,6 +542,7 @@ class Engine:
             ops.combine(ws.ES1, ws.W[0][a:b], ws.P[0], ws.X[0][a:b], y_idx=idx, v_idx=idx)
         pl = self.use_planes
         ops.combine(ws.ES1, ws.Wedge[0], ws.P[0], ws.xt[0], y_idx=ed.t, v_idx=ed.t, planes_out=pl)
+        x3 = None
         for l in (1, 2):
             S = P[f"S{l + 1}"]
             if b > a:
@@ -551,11 +552,15 @@ class Engine:
             if b > a:
                 ops.rowgemm(ws.X[l - 1][a:b], S, ws.X[l][a:b], coef=ws.W[l][a:b], V=ws.P[l], v_idx=idx,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID, **pr)
+            if l == 2:
+                # DistMult's head rows X^3 travel while the layer-3 tail GEMM runs (it reads x^2, P^3, Wedge^3 and
+                # writes x^3: nothing of X^3)
+                x3 = sh.all_gather(ws.X[2], async_op=True)
             with self._mark("tail_fwd_gemm"):
                 ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID,
                             planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, **pr)
-        sh.all_gather(ws.X[2])
+        x3.wait()
         if train:
             scale, bce = self._dm_seed(T)
             ops.distmult_bce_heads(ed.hptr, ed.hperm, ws.X[2], ws.xt[2], ed.r, P["rel"], ed.y if bce else None,
@@ -576,7 +581,9 @@ class Engine:
         if getattr(ws, "ep", None) is None:
             ws.ep = torch.empty(N, R, dtype=torch.float32, device=self.device)
         dOn, dOn_next = ws.dOn_a, ws.dOn_b
-        sh.reduce_scatter(dOn)                   # head seeds dO^3 of the rank's edges -> the heads' owners
+        # head seeds dO^3 of the rank's edges -> the heads' owners, travelling while the layer-3 tail side runs (it
+        # reads do^3, x^2, P^3, Wedge^3 and writes dP, dWedge, dS^3, do^2: nothing of dO^3)
+        seeds = sh.reduce_scatter(dOn, async_op=True)
         pl = self.use_planes
         for l in (2, 1, 0):
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
@@ -589,6 +596,7 @@ class Engine:
                 with self._mark("tail_bwd_gemm"):
                     ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
                                 planes=L.PLANES_AUX if pl else 0, **pr)
+            seeds.wait()
             ops.head_wsum(ed.hptr, ed.hperm, ws.dWedge, ws.ep)
             sh.reduce_scatter(ws.ep)             # dWedge head sums -> the heads' owners
             K, dK = P[f"K{l + 1}"], G[f"K{l + 1}"]
@@ -695,10 +703,10 @@ class Engine:
             if getattr(self, "_scratch_grads", None) is None:
                 self._scratch_grads = FlatParams(N, R, D, self.device)
             grads = self._scratch_grads
-        if self.node_shard is not None or self.spmm_shard is not None:
+        if self.node_shard is not None or self.spmm_shard is not None or self.row_shard is not None:
             # a sharded backward leaves only this rank's rows of dAE (or its reduce-scattered range): the
             # SDDMM below needs the full per-rank dAE
-            raise L.IddgcnError("value_grads: not available on an Engine with node_shard / spmm_shard set")
+            raise L.IddgcnError("value_grads: not available on an Engine with node_shard / spmm_shard / row_shard set")
         self._pred_seed, self._want_p = float(scale), True
         try:
             self.forward(params, adj, ed, ws, True)

@@ -190,7 +190,7 @@ class NodeShard:
     RelationShard's 6 R N D.  Padded to equal chunks (the ranges differ in length); gloo groups (several ranks
     sharing a GPU in tests) stage through host memory."""
 
-    def __init__(self, cuts, group=None):
+    def __init__(self, cuts, group=None, staged=None):
         self.group = group
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.cuts = [int(c) for c in cuts]
@@ -199,7 +199,10 @@ class NodeShard:
         self.N = self.cuts[-1]
         self.a, self.b = self.cuts[self.rank], self.cuts[self.rank + 1]
         self.cmax = max(self.cuts[k + 1] - self.cuts[k] for k in range(self.world))
-        self._gloo = dist.get_backend(group) == "gloo"
+        # staged: None = through host memory on a gloo group (several ranks sharing one GPU in tests), the device
+        # collectives on RCCL; False = the device collectives (all_gather_into_tensor / reduce_scatter_tensor) on
+        # any backend, so that gloo tests on CPU tensors run the code path the RCCL ranks take
+        self._gloo = (dist.get_backend(group) == "gloo") if staged is None else bool(staged)
         self._idx = None
 
     def owned_idx(self, device):
@@ -211,11 +214,14 @@ class NodeShard:
 
     def _padded(self, table):
         import torch
-        buf = torch.zeros(self.world * self.cmax, *table.shape[1:], dtype=table.dtype, device=table.device)
-        return buf
+        return torch.empty(self.world * self.cmax, *table.shape[1:], dtype=table.dtype, device=table.device)
 
-    def all_gather(self, table):
-        """table: (N, C) with this rank's rows [a, b) filled -> every row filled, on every rank."""
+    def all_gather(self, table, async_op=False):
+        """table: (N, C) with this rank's rows [a, b) filled -> every row filled, on every rank.  With ``async_op``
+        the collective is only launched (ordered after the work queued so far); the returned handle's ``wait()``
+        completes it (the copy of the other ranks' rows into ``table``, ordered on the current stream).  Until
+        then the kernels queued in between must not read the other ranks' rows of ``table`` nor write any of
+        it."""
         import torch
         n = self.b - self.a
         if self._gloo:
@@ -227,34 +233,68 @@ class NodeShard:
                 a, b = self.cuts[k], self.cuts[k + 1]
                 if k != self.rank and b > a:
                     table[a:b].copy_(parts[k][:b - a])
-            return
+            return _Done()
         full = self._padded(table)
-        mine = torch.zeros(self.cmax, *table.shape[1:], dtype=table.dtype, device=table.device)
+        mine = full[self.rank * self.cmax:(self.rank + 1) * self.cmax]
         mine[:n].copy_(table[self.a:self.b])
-        dist.all_gather_into_tensor(full, mine, group=self.group)
-        for k in range(self.world):
-            a, b = self.cuts[k], self.cuts[k + 1]
-            if k != self.rank and b > a:
-                table[a:b].copy_(full[k * self.cmax:k * self.cmax + b - a])
+        work = dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
 
-    def reduce_scatter(self, table):
+        def finish():
+            work.wait()
+            for k in range(self.world):
+                a, b = self.cuts[k], self.cuts[k + 1]
+                if k != self.rank and b > a:
+                    table[a:b].copy_(full[k * self.cmax:k * self.cmax + b - a])
+        h = _Pending(finish)
+        if not async_op:
+            h.wait()
+        return h
+
+    def reduce_scatter(self, table, async_op=False):
         """table: (N, C) partial sums on every rank -> this rank's rows [a, b) hold the sums over the ranks (rank
-        order; the other rows are left as they were)."""
+        order; the other rows are left as they were).  ``async_op``: as all_gather (until ``wait()``, the kernels
+        queued in between must not touch ``table``)."""
         import torch
         n = self.b - self.a
         if self._gloo:
-            host = table.cpu()
+            host = table.to("cpu", copy=True)    # (a CPU table: .cpu() would alias it)
             dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
             table[self.a:self.b].copy_(host[self.a:self.b])
-            return
+            return _Done()
         full = self._padded(table)
         for k in range(self.world):
             a, b = self.cuts[k], self.cuts[k + 1]
             if b > a:
                 full[k * self.cmax:k * self.cmax + b - a].copy_(table[a:b])
+            if b - a < self.cmax:            # the padding rows take part in the sum: zero them
+                full[k * self.cmax + b - a:(k + 1) * self.cmax].zero_()
         out = torch.empty(self.cmax, *table.shape[1:], dtype=table.dtype, device=table.device)
-        dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.group)
-        table[self.a:self.b].copy_(out[:n])
+        work = dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+        def finish():
+            work.wait()
+            table[self.a:self.b].copy_(out[:n])
+        h = _Pending(finish)
+        if not async_op:
+            h.wait()
+        return h
+
+
+class _Done:
+    def wait(self):
+        pass
+
+
+class _Pending:
+    """Handle of an asynchronous NodeShard collective: wait() once completes it (idempotent)."""
+
+    def __init__(self, fn):
+        self._fn = fn
+
+    def wait(self):
+        if self._fn is not None:
+            fn, self._fn = self._fn, None
+            fn()
 
 
 def node_shard_triples(triples, labels, cuts, rank):

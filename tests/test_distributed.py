@@ -162,35 +162,40 @@ def test_node_ranges_balance_and_partition():
         assert np.all((p[:, 2] >= cuts[r]) & (p[:, 2] < cuts[r + 1]))
 
 
-def _node_shard_worker(rank, world, port, q):
+def _node_shard_worker(rank, world, port, q, staged):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from iddgcn_amd.parallel import NodeShard
         cuts = [0, 5, 5, 12][:world + 1] if world == 3 else [0, 7, 12]
-        sh = NodeShard(cuts)
+        sh = NodeShard(cuts, staged=staged)
         N, C = cuts[-1], 3
-        # all-gather: each rank fills its rows with rank-specific values
+        # all-gather: each rank fills its rows with rank-specific values (asynchronously: the handle completes it)
         tab = torch.full((N, C), -1.0)
         tab[sh.a:sh.b] = torch.arange(sh.a, sh.b, dtype=torch.float32)[:, None] * 10 + torch.arange(C)
-        sh.all_gather(tab)
+        h = sh.all_gather(tab, async_op=True)
+        h.wait()
+        h.wait()                                    # idempotent
         # reduce-scatter: every rank holds partials (rank + 1) * row index; owners get the sums
         part = (rank + 1) * torch.arange(N, dtype=torch.float32)[:, None].repeat(1, C)
         sh.reduce_scatter(part)
-        q.put((rank, tab.numpy(), part[sh.a:sh.b].numpy(), (sh.a, sh.b)))
+        q.put((rank, tab.numpy(), part[sh.a:sh.b].numpy(), (sh.a, sh.b), part.numpy()))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("staged", [None, False])
 @pytest.mark.parametrize("world", [2, 3])
-def test_node_shard_collectives_gloo(world):
+def test_node_shard_collectives_gloo(world, staged):
     """NodeShard.all_gather / reduce_scatter on (N, C) tables with UNEQUAL row ranges (one empty at world 3):
     after the all-gather every rank holds every rank's rows; after the reduce-scatter each owner holds the sums
-    of the ranks' partials for its rows."""
+    of the ranks' partials for its rows and the other rows are untouched.  staged=None: the host-staged gloo
+    branch; staged=False: the device branch the RCCL ranks take (padded all_gather_into_tensor with the rank's
+    chunk aliased in the output, reduce_scatter_tensor with zeroed padding rows), run here on CPU tensors."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_node_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_node_shard_worker, args=(r, world, port, q, staged)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -200,6 +205,9 @@ def test_node_shard_collectives_gloo(world):
     N = 12
     want = np.arange(N, dtype=np.float32)[:, None] * 10 + np.arange(3)
     tot = sum(range(1, world + 1))
-    for rank, tab, mine, (a, b) in res:
+    for rank, tab, mine, (a, b), part in res:
         assert np.array_equal(tab, want)
         assert np.array_equal(mine, tot * np.arange(a, b, dtype=np.float32)[:, None].repeat(3, 1))
+        other = np.ones(N, bool)
+        other[a:b] = False
+        assert np.array_equal(part[other], (rank + 1) * np.arange(N, dtype=np.float32)[other, None].repeat(3, 1))

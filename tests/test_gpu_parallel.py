@@ -137,10 +137,12 @@ def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact"):
         lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
         lo, hi = shard_range(len(tri), rank, world)
         eng = Engine(N, R, D, dev, gemm=gemm)
-        if mode == "node":
+        if mode in ("node", "node_device"):
             from iddgcn_amd.parallel import NodeShard, node_ranges, node_shard_triples
             cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
-            eng.row_shard = NodeShard(cuts)
+            # node_device: the collectives' device branch (padded all_gather_into_tensor / reduce_scatter_tensor on
+            # the GPU tables, asynchronous handles: what the RCCL ranks run), not host-staged
+            eng.row_shard = NodeShard(cuts, staged=False if mode == "node_device" else None)
             mine, mlab = node_shard_triples(tri, lab, cuts, rank)
         if mode == "relation":
             eng.node_shard = RelationShard(R, N)
@@ -149,7 +151,7 @@ def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact"):
         P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
         P.load(_mild(N, R, D, 9))
         adj = eng.adjacency(get_adj_mats(pos, N, R))
-        ed = eng.edges(mine, mlab) if mode == "node" else eng.edges(tri[lo:hi], lab[lo:hi])
+        ed = eng.edges(mine, mlab) if mode.startswith("node") else eng.edges(tri[lo:hi], lab[lo:hi])
         comm = BucketedAllReduce(min_bucket_rows=64, host_staged=False if mode == "edge_device" else None)
         ws = eng.workspace(ed.T, True)
         eng._t_global = len(tri)
@@ -224,14 +226,18 @@ def test_bwd_columns_partition_sums_to_full(cuda):
     assert (acc - full).abs().max().item() <= 1e-5 * full.abs().max().item()
 
 
-@pytest.mark.parametrize("world,N,R,D,gemm", [(2, 600, 2, 64, "exact"), (3, 601, 3, 256, "exact"),
-                                              (2, 700, 2, 256, "bf16x3"), (3, 650, 2, 256, "split")])
-def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, cuda):
+@pytest.mark.parametrize("world,N,R,D,gemm,mode", [(2, 600, 2, 64, "exact", "node"), (3, 601, 3, 256, "exact", "node"),
+                                                   (2, 700, 2, 256, "bf16x3", "node"), (3, 650, 2, 256, "split", "node"),
+                                                   (2, 700, 2, 256, "bf16x3", "node_device"),
+                                                   (3, 601, 3, 256, "exact", "node_device")])
+def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, mode, cuda):
     """Node-row partitioning (parallel.NodeShard, round 4): rank k owns a contiguous node range (balanced by tail
     edges + node work), computes the node tables of its rows only, takes the scored edges whose tail it owns;
     W^l and X^3 are all-gathered, the head seeds dO^3 and the dWedge head sums reduce-scattered, every gradient
     all-reduced.  world 2 and 3 ranks on one GPU over gloo: the step's loss and every gradient equal the
-    single-process full batch (1e-5 of max|g|), bitwise equal on every rank."""
+    single-process full batch (1e-5 of max|g|), bitwise equal on every rank.  mode "node_device": the collectives'
+    device branch with asynchronous handles (X^3 gathered beside the layer-3 tail GEMM, dO^3 reduce-scattered
+    beside the layer-3 tail backward), over gloo on the GPU tables."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     pos, neg = synthetic_graph(N, R, 9000, seed=77)
@@ -244,7 +250,7 @@ def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, cuda):
     full, full_loss = G.to_numpy(), float(loss.item())
     del eng, P, G
     port = _free_port()
-    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q, "node", N, R, D, gemm)) for r in range(world)]
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q, mode, N, R, D, gemm)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])

@@ -10,7 +10,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -k "model or explain or paral
 rc=$?
 tail -3 $OUT/tests.log
 [ $rc -ne 0 ] && exit $rc
-for init in stateless independent; do
+for init in tf27 independent; do
   timeout -k 10 500 python -u tools/train_folds.py --seeds $SEEDS --init $init --out $OUT/train_$init.json > $OUT/train_$init.log 2>&1 || exit $?
   tail -1 $OUT/train_$init.log
 done

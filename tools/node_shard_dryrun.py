@@ -1,0 +1,118 @@
+"""Per-rank compute of a node-row partitioned step (parallel.NodeShard), measured on ONE GPU.
+
+For a BASELINE config and a world size W, each rank k's engine (its node range [cuts[k], cuts[k+1]) from
+parallel.node_ranges, the scored edges whose tail it owns, the full device adjacency) is built and timed on this
+GPU in turn, with the collectives replaced by no-ops (DryShard): the kernels run on the rank's true shapes, so the
+per-rank time is the compute a rank of a W-GPU job does, without communication.  The single-GPU step is timed
+first for reference.  Collective volumes of the real step are reported beside it (bytes per rank), so that
+DESIGN.md's strong-scaling model = max_k compute_k + un-overlapped collectives can be written from measurements.
+(The numbers the kernels produce here are meaningless - other ranks' rows are never filled - only the timing is.)
+
+usage: python tools/node_shard_dryrun.py [config=4] [world=8] [steps=3] [ranks=all|k,k,...]
+"""
+import json
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from bench import CONFIGS, reference_init  # noqa: E402
+from iddgcn_amd.engine import Engine, FlatParams, KerasAdam  # noqa: E402
+from iddgcn_amd.graph import get_adj_mats  # noqa: E402
+from iddgcn_amd.parallel import node_ranges, node_shard_triples  # noqa: E402
+from iddgcn_amd.utils import synthetic_graph  # noqa: E402
+
+
+class DryShard:
+    """parallel.NodeShard's interface with the collectives removed (timing only)."""
+
+    def __init__(self, cuts, rank):
+        self.cuts, self.rank, self.world = [int(c) for c in cuts], rank, len(cuts) - 1
+        self.N = self.cuts[-1]
+        self.a, self.b = self.cuts[rank], self.cuts[rank + 1]
+        self._idx = None
+        self.bytes = 0
+
+    def owned_idx(self, device):
+        if self._idx is None:
+            self._idx = torch.arange(self.a, self.b, dtype=torch.int32, device=device)
+        return self._idx
+
+    def all_gather(self, table):
+        self.bytes += table.numel() * table.element_size() * (self.world - 1) // self.world
+
+    def reduce_scatter(self, table):
+        self.bytes += table.numel() * table.element_size() * (self.world - 1) // self.world
+
+
+def time_steps(eng, P, G, adj, ed, T, steps):
+    opt = KerasAdam(P)
+    eng.train_step(P, G, opt, adj, ed, t_global=T)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.train_step(P, G, opt, adj, ed, t_global=T)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def main():
+    a = sys.argv[1:]
+    cid = int(a[0]) if a else 4
+    world = int(a[1]) if len(a) > 1 else 8
+    steps = int(a[2]) if len(a) > 2 else 3
+    only = None if len(a) < 4 or a[3] == "all" else [int(x) for x in a[3].split(",")]
+    cfg = CONFIGS[cid]
+    N, R, D, M = cfg["N"], cfg["R"], cfg["D"], cfg["M"]
+    feat = cfg.get("features", "f32")
+    gemm = cfg.get("gemm", "bf16x3") if feat == "bf16" else "bf16x3"
+    dev = torch.device("cuda", 0)
+    pos, neg = synthetic_graph(N, R, M, seed=0)
+    if cfg.get("neg_every", 1) > 1:
+        from iddgcn_amd.sampling import negative_samples
+        neg = negative_samples(pos[::cfg["neg_every"]], N, 89, device=dev)
+    tri = np.concatenate([pos, neg])
+    lab = np.concatenate([np.ones(len(pos), np.float32), np.zeros(len(neg), np.float32)])
+    T = len(tri)
+    adj = get_adj_mats(pos, N, R, device=dev)
+    init = reference_init(np, N, R, D, 89)
+    P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
+    P.load(init)
+    out = {"config": cfg["name"], "world": world, "gemm": gemm, "features": feat, "steps": steps}
+    eng = Engine(N, R, D, dev, gemm=gemm, features=feat)
+    ed = eng.edges(tri, lab)
+    out["full_ms"] = time_steps(eng, P, G, adj, ed, T, steps)
+    print(json.dumps({"full_ms": out["full_ms"]}), flush=True)
+    del eng, ed
+    torch.cuda.empty_cache()
+    cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
+    out["cuts"] = cuts
+    ranks = []
+    for k in range(world):
+        if only is not None and k not in only:
+            continue
+        t_k, l_k = node_shard_triples(tri, lab, cuts, k)
+        eng = Engine(N, R, D, dev, gemm=gemm, features=feat)
+        sh = DryShard(cuts, k)
+        eng.row_shard = sh
+        ed = eng.edges(t_k, l_k)
+        P.load(init)
+        ms = time_steps(eng, P, G, adj, ed, T, steps)
+        r = {"rank": k, "rows": cuts[k + 1] - cuts[k], "scored_edges": int(len(t_k)), "ms": ms,
+             "collective_bytes_per_step": sh.bytes // (steps + 1),
+             "dE_allreduce_bytes": 2 * (world - 1) * N * D * 4 // world}
+        ranks.append(r)
+        print(json.dumps(r), flush=True)
+        del eng, ed
+        torch.cuda.empty_cache()
+    out["ranks"] = ranks
+    if ranks:
+        out["max_rank_ms"] = max(r["ms"] for r in ranks)
+        out["compute_speedup"] = out["full_ms"] / out["max_rank_ms"]
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

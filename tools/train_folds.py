@@ -55,7 +55,18 @@ def run(fold, seed, epochs, init="tf27"):
     y = np.concatenate([np.ones(len(d["X_test"])), np.zeros(len(d["neg_X_test"]))])
     p = model.predict(x=[np.arange(N_ENT)[None], Xt[:, :, 0], Xt[:, :, 1], Xt[:, :, 2], adj_eval])[0]
     prec, reca, _ = precision_recall_curve(y, p)
+    # the reference trained its bundled weights from this same start (tf27, seed 89) with the same deterministic
+    # full-batch loop: how far the trained weights land from them, per parameter (max |w - w_ref| / max |w_ref|)
+    wdiff = None
+    if init == "tf27" and seed == 89:
+        model._sync_to_host()
+        ref = np.load(os.path.join(ROOT, "tests", "golden", f"weights_fold{fold}.npz"))
+        mine = model._named()
+        wdiff = {k: float(np.abs(mine[k] - ref[k]).max() / max(np.abs(ref[k]).max(), 1e-30)) for k in ref.files}
+        pr = model.predict(x=[np.arange(N_ENT)[None], Xt[:, :, 0], Xt[:, :, 1], Xt[:, :, 2], adj_eval])[0]
+        assert np.array_equal(pr, p)
     return {"fold": fold, "seed": seed, "init": init, "epochs": epochs, "train_s": train_s,
+            "trained_vs_bundled_weights_rel": wdiff,
             "ms_per_epoch": train_s / epochs * 1e3, "final_loss": hist.history["loss"][-1],
             "roc_auc": float(roc_auc_score(y, p)), "aupr": float(auc(reca, prec)),
             "accuracy": float(((p > 0.5) == (y > 0.5)).mean()), "reference_weights_auc_restated": REFERENCE_WEIGHTS_AUC[fold]}
