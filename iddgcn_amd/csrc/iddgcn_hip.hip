@@ -3052,6 +3052,147 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
 }
 
 // ---------------------------------------------------------------------------
+// tail-side layer backward on MFMAs: R = 8 relations, bf16 edge rows, D = 256 (config 5; round 4).
+// Per tail node t (one wave) and per chunk of 32 of its edges (rows e of do, coefficients W[e][0..7]):
+//   dWedge[e][r] = do[e] . P_r[t]        the chunk (32 x 256, bf16) times P[t]^T (256 x 8, split hi + lo bf16)
+//   dP_r[t]     += sum_e W[e][r] do[e]   W^T (8 x 32, hi + lo) times the chunk (32 x 256)
+//   dsum[t]     += sum_e do[e]           (DSUM, layer 1: a ones row beside W^T)
+// on v_mfma_f32_16x16x32_bf16: the products are exact (bf16 x bf16), accumulation fp32; the fp32 operands P and W
+// enter EXACTLY as three bf16 pieces each (hi + mid + lo = 24 significant bits, as in the bf16x3 GEMMs; the bf16 rows
+// are exact as they are), so the only difference from fp32 arithmetic is the order of the fp32 sums.  The VALU form (tail_seg_reduce_kernel<256, 8, true>) spends ~1100 instructions per 8
+// edges here (two FMA chains per relation and a 64-value butterfly per edge group) and is VALU-bound (11.6 ms per
+// config-5 launch); this one issues ~250 per 32 edges (80 of them MFMAs) and is bound by the rows' bytes.
+//   dWedge product: A = the chunk's rows (lane l: row l&15 of a 16-row block, columns 32 s + 8 (l>>4) .. +7: one
+//     16-B load), B = P[t]'s pieces (lane l: column n = l&15 -> relation n&7; first MFMA: lo for n < 8, none for
+//     n >= 8; second: hi for n < 8, mid for n >= 8, into the same accumulator), so C[e][n] + C[e][n ^ 8] (one DPP row
+//     rotate) is the dot product.
+//   dP product: A = W^T rows (m < 8: relation m; m = 8: ones when DSUM), with the lo, mid and hi pieces in turn into
+//     the same accumulators; B = the chunk transposed (8 consecutive edges of one column per lane),
+//     read with ds_read_b64_tr_b16 from the row-major copy each wave keeps of its chunk in LDS (544-B row pitch, rows
+//     8-15 of every 16 shifted 128 B (tsm_row): the 32 lanes of a transposed read hit distinct banks, the 8 of a row
+//     write up to 2-way).
+// Edges past the segment enter as zero rows with zero coefficients; every node (also an empty one) stores its dP rows.
+namespace tsm {
+constexpr int D = 256, R = 8, CH = 32, PITCH = 544, CHB = CH * PITCH + 256;
+}  // namespace tsm
+// row r's slot: rows 8-15 of every 16 shifted 128 B (bank spread of the transposed reads), and each later 16-row half
+// a further 128 B so that the shifted rows never reach into the next half's first row
+__device__ __forceinline__ int tsm_row(int r) { return r * tsm::PITCH + ((r >> 3) & 1) * 128 + (r >> 4) * 128; }
+
+template <bool DSUM>
+__global__ __launch_bounds__(256) void tail_seg_mfma8_kernel(int n_nodes, const int* __restrict__ seg_ptr,
+                                                             const float* __restrict__ W, const __bf16* __restrict__ dO,
+                                                             const float* __restrict__ P, long long p_rel_stride,
+                                                             float* __restrict__ dP, long long dp_rel_stride,
+                                                             float* __restrict__ dsum, float* __restrict__ dWedge) {
+    using namespace tsm;
+    __shared__ __attribute__((aligned(16))) char lds[4 * CHB];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long n = (long long)blockIdx.x * 4 + wave;
+    if (n >= n_nodes) return;                       // whole waves; the kernel has no barrier
+    char* buf = lds + wave * CHB;
+    const int beg = __builtin_amdgcn_readfirstlane(seg_ptr[n]);
+    const int end = __builtin_amdgcn_readfirstlane(seg_ptr[n + 1]);
+    const int i16 = lane & 15, g = lane >> 4;
+    // B pieces of the dWedge product: k-step s, lane l: P_{(l&15)&7}[t][32 s + 8 g + j] split3; pl: lo (l&15 < 8)
+    // or 0, ph: hi (l&15 < 8) or mid
+    bf16x8 pl[8], ph[8];
+    {
+        const float* pr = P + (long long)(i16 & 7) * p_rel_stride + n * D + 8 * g;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const f32x4 a = ld4(pr + 32 * s), b = ld4(pr + 32 * s + 4);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                __bf16 hi, mid, lo;
+                split3(j < 4 ? a[j] : b[j - 4], hi, mid, lo);
+                ph[s][j] = i16 < 8 ? hi : mid;
+                pl[s][j] = i16 < 8 ? lo : (__bf16)0.0f;
+            }
+        }
+    }
+    f32x4 acc[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    typedef __attribute__((address_space(3))) u32x4* lu4;
+    typedef __attribute__((address_space(3))) v4s16* l4p;
+    // transposed-read address of this lane: rows 8 g + ((l>>2)&3) (+4: second read), columns 4 (l&3) of a block
+    const int tr0 = tsm_row(8 * g + ((lane >> 2) & 3)) + 8 * (lane & 3);
+    const int tr1 = tsm_row(8 * g + 4 + ((lane >> 2) & 3)) + 8 * (lane & 3);
+    for (int c0 = beg; c0 < end; c0 += CH) {
+        const int cnt = end - c0 < CH ? end - c0 : CH;
+        // the chunk's row fragments (block b: rows 16 b + (l&15); zero past the segment)
+        u32x4 fr[2][8];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const bool ok = 16 * b + i16 < cnt;
+            const __bf16* row = dO + (long long)(ok ? c0 + 16 * b + i16 : c0) * D + 8 * g;
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                fr[b][s] = ok ? *reinterpret_cast<const u32x4*>(row + 32 * s) : u32x4{0u, 0u, 0u, 0u};
+        }
+        // W^T rows of the dP product: lane l: row m = l&15, edges 8 g + j of the chunk, split3
+        bf16x8 wh, wm, wl;
+        {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int e = 8 * g + j;
+                float w = 0.f;
+                if (i16 < 8 && e < cnt) w = W[(long long)(c0 + e) * R + i16];
+                __bf16 hi, mid, lo;
+                split3(w, hi, mid, lo);
+                wh[j] = (DSUM && i16 == 8 && e < cnt) ? (__bf16)1.0f : hi;
+                wm[j] = mid;
+                wl[j] = lo;
+            }
+        }
+        // row-major copy of the chunk for the transposed reads
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) *(lu4)(buf + tsm_row(16 * b + i16) + 64 * s + 16 * g) = fr[b][s];
+        // dWedge: two 16-edge blocks x 8 k-steps
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const bf16x8 a = __builtin_bit_cast(bf16x8, fr[b][s]);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pl[s], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ph[s], c, 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = c[i] + dpp<0x128>(c[i]);      // (hi + lo) + the mid column (lane (l&15) ^ 8)
+                const int e = 16 * b + 4 * g + i;
+                if (i16 < 8 && e < cnt) dWedge[(long long)(c0 + e) * R + i16] = v;
+            }
+        }
+        // dP (+ dsum): 16 column blocks, lo, mid and hi pieces of W
+#pragma unroll
+        for (int cb = 0; cb < 16; ++cb) {
+            const v4s16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)(buf + tr0 + 32 * cb));
+            const v4s16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)(buf + tr1 + 32 * cb));
+            const bf16x8 bx = __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bx, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, bx, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bx, acc[cb], 0, 0, 0);
+        }
+    }
+    // lane l holds rows 4 g + i (relations 0-3: g = 0, 4-7: g = 1, dsum: g = 2, i = 0) of columns 16 cb + (l&15)
+#pragma unroll
+    for (int cb = 0; cb < 16; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = 4 * g + i;
+            const long long col = n * D + 16 * cb + i16;
+            if (m < 8) dP[m * dp_rel_stride + col] = acc[cb][i];
+            else if (DSUM && m == 8) dsum[col] = acc[cb][i];
+        }
+}
+
+// ---------------------------------------------------------------------------
 // head-chain node backward (one layer)
 // ---------------------------------------------------------------------------
 template <int D>
@@ -4144,6 +4285,16 @@ int iddgcn_tail_seg_reduce_bf16(void* stream, int n_nodes, int d, int R, const i
     hipStream_t st = (hipStream_t)stream;
     const unsigned grid = grid_for(n_nodes, 64);
     const float* d_o = (const float*)dO;
+    if (R == 8 && !h_idx) {          // per-edge W, 8 relations (config 5): the MFMA form
+        const unsigned g4 = (unsigned)((n_nodes + 3) / 4);
+        if (dsum)
+            hipLaunchKernelGGL((tail_seg_mfma8_kernel<true>), dim3(g4), dim3(256), 0, st, n_nodes, seg_ptr, W,
+                               (const __bf16*)dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge);
+        else
+            hipLaunchKernelGGL((tail_seg_mfma8_kernel<false>), dim3(g4), dim3(256), 0, st, n_nodes, seg_ptr, W,
+                               (const __bf16*)dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge);
+        return launch_status();
+    }
 #define TKB(RR) hipLaunchKernelGGL((tail_seg_reduce_kernel<256, RR, true>), dim3(grid), dim3(256), 0, st, n_nodes, seg_ptr, h_idx, W, d_o, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge)
     switch (R) {
         case 1: TKB(1); break;

@@ -91,13 +91,18 @@ def test_combine_tail_seg_distmult_bf16(R, cuda):
     tl = t.long()
     ref = torch.sigmoid(Y.double()[tl] + sum(W.double()[:, r:r + 1] * P.double()[r][tl] for r in range(R)))
     assert maxrel(out, ref) <= 6e-3
-    # tail-side segmented reduction over bf16 rows == the fp32 kernel on the same (widened) rows
+    # tail-side segmented reduction over bf16 rows == the fp32 kernel on the same (widened) rows: bitwise for the
+    # VALU form (R < 8); R = 8 runs the MFMA form (tail_seg_mfma8_kernel: exact three-piece operands, fp32 sums in
+    # another order), within 1e-5 of max|ref| of it
     tptr = torch.searchsorted(t, torch.arange(N + 1, device=cuda, dtype=torch.int32)).int()
     dP, dWe = torch.empty(R, N, D, device=cuda), torch.empty(M, R, device=cuda)
     ops.tail_seg_reduce(tptr, None, W, out, P, dP, dWe)
     dP32, dWe32 = torch.empty_like(dP), torch.empty_like(dWe)
     ops.tail_seg_reduce(tptr, None, W, out.float(), P, dP32, dWe32)
-    assert torch.equal(dP, dP32) and torch.equal(dWe, dWe32)
+    if R < 8:
+        assert torch.equal(dP, dP32) and torch.equal(dWe, dWe32)
+    else:
+        assert maxrel(dP, dP32.double()) <= 1e-5 and maxrel(dWe, dWe32.double()) <= 1e-5
     # DistMult scores of bf16 tails == the fp32 kernel on the widened rows
     h = torch.randint(0, N, (M,), generator=g).int().to(cuda)
     r = torch.randint(0, R, (M,), generator=g).int().to(cuda)
@@ -135,3 +140,52 @@ def test_bf16_mode_step_tracks_fp32(R, cuda):
     for k, v in g32.items():
         assert np.all(np.isfinite(gb[k])), k
         assert np.abs(gb[k] - v).max() <= 5e-2 * np.abs(v).max() + 1e-30, k
+
+
+@pytest.mark.parametrize("case", ["uniform", "hub", "sparse", "empty", "tiny", "long"])
+@pytest.mark.parametrize("dsum", [False, True])
+def test_tail_seg_mfma8_bf16(case, dsum, cuda):
+    """The R = 8 bf16 tail reduction on MFMAs (tail_seg_mfma8_kernel, config 5's form: per-edge W, bf16 do rows) against
+    float64 index_add references on the same bf16 rows: dP, dWedge and dsum within 1e-5 of max|ref| (the operands
+    W and P enter as exact three-piece bf16 splits, so only the fp32 summation order differs); run twice, bitwise
+    equal.  Cases: runs of tails without edges, a hub tail with a third of the edges, almost every tail without
+    edges, tiny graphs (chunks of 32 edges padded), and segments of 1-200 edges (several chunks, partial last)."""
+    g = torch.Generator().manual_seed(len(case) * 7 + dsum)
+    R = 8
+    N = {"tiny": 5, "empty": 300, "long": 400}.get(case, 1000 + 7)
+    T = {"tiny": 37, "empty": 3, "sparse": 60}.get(case, 30_000)
+    if case == "long":
+        lengths = torch.randint(1, 200, (N,), generator=g)
+        t = torch.repeat_interleave(torch.arange(N), lengths)
+        T = len(t)
+    else:
+        t = torch.randint(0, N, (T,), generator=g)
+        if case == "hub":
+            t[: T // 3] = 517
+        if case == "uniform":
+            t[(t >= 100) & (t < 140)] = 99
+        t = torch.sort(t).values
+    tptr = torch.searchsorted(t, torch.arange(N + 1), right=False).to(torch.int32).to(cuda)
+    W = torch.rand(T, R, generator=g).to(cuda)
+    P = torch.randn(R, N, D, generator=g).to(cuda)
+    dO = bf(torch.randn(T, D, generator=g)).to(cuda)
+    tc = t.to(cuda)
+    outs = []
+    for _ in range(2):
+        dP, dWe = torch.full((R, N, D), 7.0, device=cuda), torch.full((T, R), 7.0, device=cuda)
+        ds = torch.full((N, D), 7.0, device=cuda) if dsum else None
+        ops.tail_seg_reduce(tptr, None, W, dO, P, dP, dWe, dsum=ds)
+        outs.append([dP, dWe] + ([ds] if dsum else []))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    dP, dWe = outs[0][0], outs[0][1]
+    d64, W64, P64 = dO.double(), W.double(), P.double()
+    for r in range(R):
+        ref = torch.zeros(N, D, dtype=torch.float64, device=cuda).index_add_(0, tc, W64[:, r:r + 1] * d64)
+        assert (dP[r].double() - ref).abs().max().item() <= 1e-5 * max(ref.abs().max().item(), 1e-30)
+        if T:
+            refw = (d64 * P64[r][tc]).sum(-1)
+            assert (dWe[:, r].double() - refw).abs().max().item() <= 1e-5 * refw.abs().max().item()
+    if dsum:
+        ref = torch.zeros(N, D, dtype=torch.float64, device=cuda).index_add_(0, tc, d64)
+        assert (outs[0][2].double() - ref).abs().max().item() <= 1e-5 * max(ref.abs().max().item(), 1e-30)
