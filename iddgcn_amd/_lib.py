@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
 GEMM_EXACT_F32, GEMM_SPLIT_F16, GEMM_F32_4CHAIN, GEMM_BF16X3 = 0, 1, 2, 3
@@ -87,6 +87,8 @@ SIGNATURES = {
     "iddgcn_distmult_bce_heads_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, cf, vp, vp, vp, vp, vp, vp,
                                             vp, ci]),
     "iddgcn_tail_seg_reduce_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp, cll, vp, cll, vp, vp]),
+    "iddgcn_tail_seg_reduce_head_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp, cll, vp, vp, vp, vp, vp]),
+    "iddgcn_head_dz_f32": (ci, [vp, ci, ci, vp, vp, vp, vp, vp, vp, vp]),
     # include/iddgcn_graph.h
     "iddgcn_radix_sort_workspace": (cll, [cll, ci]),
     "iddgcn_radix_sort_pairs": (ci, [vp, cll, ci, ci, vp, vp, vp, vp, vp, cll]),

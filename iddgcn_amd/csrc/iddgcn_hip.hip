@@ -2620,6 +2620,15 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
     f32x4 dr[RT];
 #pragma unroll
     for (int r = 0; r < RT; ++r) dr[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // R >= 4 with one head per wave: the per-relation partials of drel live in the block's LDS slab instead of dr[]
+    // (the relation of an edge is wave-uniform, and selecting one of 8 register quads per edge cost ~45 instructions
+    // of branches and moves per edge: config-5 launch 18.3 -> 15.9 ms); same values added in the same order per lane
+    // (the register form's add was contracted into an fma: drel partials within 2e-7)
+    constexpr bool LDS_DR = SLOTS == 1 && RT >= 4 && RT >= DM_SC_MINR;
+    if constexpr (LDS_DR) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r) st4(red + (grp * RT + r) * D + sub * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+    }
     float lacc = 0.f;
     const long long nstride = (long long)gridDim.x * NPB;
     for (long long n0 = (long long)blockIdx.x * NPB; n0 < n_nodes; n0 += nstride) {
@@ -2675,9 +2684,14 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 dx = dx * (b[u] * (1.0f - b[u]));
                 st4e<BF>(do_out, e[u] * D + sub * 4, dx);
                 const f32x4 dre = ds * (a * b[u]);
+                if constexpr (LDS_DR) {
+                    float* dst = red + (grp * RT + rr[u]) * D + sub * 4;     // this lane's own 16 B
+                    st4(dst, ld4(dst) + dre);
+                } else {
 #pragma unroll
-                for (int r = 0; r < RT; ++r)
-                    if (r == rr[u]) dr[r] += dre;
+                    for (int r = 0; r < RT; ++r)
+                        if (r == rr[u]) dr[r] += dre;
+                }
                 acc = fma4(b[u] * ds, rho[u], acc);     // same explicit fma as seg_gather_reduce
             }
         };
@@ -2807,8 +2821,10 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
             for (int q = 0; q < 4; ++q) acc[q] += __shfl_xor(acc[q], LPR * m, 64);
         if (live && slot == 0) st4(dXh + n * D + sub * 4, acc * (a * (1.0f - a)));
     }
+    if constexpr (!LDS_DR) {
 #pragma unroll
-    for (int r = 0; r < RT; ++r) st4(red + (grp * RT + r) * D + sub * 4, dr[r]);
+        for (int r = 0; r < RT; ++r) st4(red + (grp * RT + r) * D + sub * 4, dr[r]);
+    }
     if (sub == 0) lred[grp] = lacc;
     __syncthreads();
     for (int x = threadIdx.x; x < R * D; x += 256) {
@@ -3072,6 +3088,11 @@ __global__ __launch_bounds__(256) void tail_seg_reduce_kernel(int n_nodes, const
 //     8-15 of every 16 shifted 128 B (tsm_row): the 32 lanes of a transposed read hit distinct banks, the 8 of a row
 //     write up to 2-way).
 // Edges past the segment enter as zero rows with zero coefficients; every node (also an empty one) stores its dP rows.
+// HEAD (ABI 9, iddgcn_tail_seg_reduce_head_bf16): the head chain's node terms of the same layer are added before the
+// store, dP[r][n] = tail sum + Wn[n][r] head_dO[n] and dsum[n] = tail sum + head_dO[n], and the node's own part of the
+// dynamic-weight gradient, dwh[n][r] = <head_dO[n], P_r[n]>, is formed from the P pieces already in registers (one
+// 16x16x32 MFMA pair per k-step: rows 0-2 of A = the three bf16 pieces of head_dO[n], so all nine piece products
+// enter), so the rest of the head backward (iddgcn_head_dz_f32) reads neither P nor head_dO again.
 namespace tsm {
 constexpr int D = 256, R = 8, CH = 32, PITCH = 544, CHB = CH * PITCH + 256;
 }  // namespace tsm
@@ -3079,14 +3100,16 @@ constexpr int D = 256, R = 8, CH = 32, PITCH = 544, CHB = CH * PITCH + 256;
 // a further 128 B so that the shifted rows never reach into the next half's first row
 __device__ __forceinline__ int tsm_row(int r) { return r * tsm::PITCH + ((r >> 3) & 1) * 128 + (r >> 4) * 128; }
 
-template <bool DSUM>
+template <bool DSUM, bool HEAD>
 __global__ __launch_bounds__(256) void tail_seg_mfma8_kernel(int n_nodes, const int* __restrict__ seg_ptr,
                                                              const float* __restrict__ W, const __bf16* __restrict__ dO,
                                                              const float* __restrict__ P, long long p_rel_stride,
                                                              float* __restrict__ dP, long long dp_rel_stride,
-                                                             float* __restrict__ dsum, float* __restrict__ dWedge) {
+                                                             float* __restrict__ dsum, float* __restrict__ dWedge,
+                                                             const float* __restrict__ head_dO,
+                                                             const float* __restrict__ Wn, float* __restrict__ dwh) {
     using namespace tsm;
-    __shared__ __attribute__((aligned(16))) char lds[4 * CHB];
+    __shared__ __attribute__((aligned(16))) char lds[4 * CHB + (HEAD ? 4 * 1024 : 0)];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long n = (long long)blockIdx.x * 4 + wave;
@@ -3095,6 +3118,20 @@ __global__ __launch_bounds__(256) void tail_seg_mfma8_kernel(int n_nodes, const 
     const int beg = __builtin_amdgcn_readfirstlane(seg_ptr[n]);
     const int end = __builtin_amdgcn_readfirstlane(seg_ptr[n + 1]);
     const int i16 = lane & 15, g = lane >> 4;
+    // HEAD: the node's head-seed row by one LDS-DMA (1 KiB, kept for dwh below and the store phase; loaded in the store
+    // phase it doubled the launch, held in 16 more VGPRs it took the kernel past 256 registers) and this lane's 4
+    // dynamic weights, issued before the P loads: the wait for those covers them
+    float wn[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (HEAD) {
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(head_dO + n * D + lane * 4), (lds_vptr)(lds + 4 * CHB + wave * 1024),
+                                         16, 0, 0);
+        if (g < 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wn[i] = Wn[n * R + 4 * g + i];
+        }
+    }
+    const __attribute__((address_space(3))) float* hrow =
+        (const __attribute__((address_space(3))) float*)(lds + 4 * CHB + wave * 1024);
     // B pieces of the dWedge product: k-step s, lane l: P_{(l&15)&7}[t][32 s + 8 g + j] split3; pl: lo (l&15 < 8)
     // or 0, ph: hi (l&15 < 8) or mid
     bf16x8 pl[8], ph[8];
@@ -3111,6 +3148,30 @@ __global__ __launch_bounds__(256) void tail_seg_mfma8_kernel(int n_nodes, const 
                 pl[s][j] = i16 < 8 ? lo : (__bf16)0.0f;
             }
         }
+    }
+    if constexpr (HEAD) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the head-seed row's DMA
+        // dwh[n][r] = <head_dO[n], P_r[n]>: A row m < 3 = piece m of head_dO[n] (columns 32 s + 8 g + j), B = the P
+        // pieces (pl: lo | 0, ph: hi | mid), so C[m][r] + C[m][r + 8] summed over m holds all nine piece products
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const f32x4 x0 = *(const __attribute__((address_space(3))) f32x4*)(hrow + 32 * s + 8 * g);
+            const f32x4 x1 = *(const __attribute__((address_space(3))) f32x4*)(hrow + 32 * s + 8 * g + 4);
+            bf16x8 a;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                __bf16 hi, mid, lo;
+                split3(j < 4 ? x0[j] : x1[j - 4], hi, mid, lo);
+                a[j] = i16 == 0 ? hi : i16 == 1 ? mid : i16 == 2 ? lo : (__bf16)0.0f;
+            }
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pl[s], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ph[s], c, 0, 0, 0);
+        }
+        // lanes 0-15 hold C[0..3][l&15]: rows 0-2 are the pieces
+        const float v = (c[0] + c[1]) + c[2];
+        const float tot = v + dpp<0x128>(v);
+        if (lane < 8) dwh[n * R + lane] = tot;
     }
     f32x4 acc[16];
 #pragma unroll
@@ -3182,14 +3243,16 @@ __global__ __launch_bounds__(256) void tail_seg_mfma8_kernel(int n_nodes, const 
     }
     // lane l holds rows 4 g + i (relations 0-3: g = 0, 4-7: g = 1, dsum: g = 2, i = 0) of columns 16 cb + (l&15)
 #pragma unroll
-    for (int cb = 0; cb < 16; ++cb)
+    for (int cb = 0; cb < 16; ++cb) {
+        const long long col = n * D + 16 * cb + i16;
+        const float hd = HEAD ? hrow[16 * cb + i16] : 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int m = 4 * g + i;
-            const long long col = n * D + 16 * cb + i16;
-            if (m < 8) dP[m * dp_rel_stride + col] = acc[cb][i];
-            else if (DSUM && m == 8) dsum[col] = acc[cb][i];
+            if (m < 8) dP[m * dp_rel_stride + col] = HEAD ? fmaf(wn[i], hd, acc[cb][i]) : acc[cb][i];
+            else if (DSUM && m == 8) dsum[col] = HEAD ? acc[cb][i] + hd : acc[cb][i];
         }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -3264,6 +3327,7 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
         for (int r = 0; r < MAX_R; ++r)
             if (r < R) dz[n * R + r] = (dsv[r] - dot) * s[r];
     }
+    if (!dP) return;                 // (ABI 9) the dP term was added by iddgcn_tail_seg_reduce_head_bf16
 #pragma unroll
     for (int r = 0; r < MAX_R; ++r)
         if (r < R) {
@@ -3294,6 +3358,51 @@ __global__ __launch_bounds__(256) void head_wsum_kernel(int n_nodes, int R, cons
     float s = 0.f;
     for (int k = hptr[n]; k < hptr[n + 1]; ++k) s += w[(long long)hperm[k] * R + r];
     out[x] = s;
+}
+
+// The rest of the head backward after iddgcn_tail_seg_reduce_head_bf16, one thread per node: dW_r = dwh[n][r] + the
+// head segment's dWedge rows (in segment order), then the softmax-sigmoid backward of head_bwd_node_kernel -> dz
+__global__ __launch_bounds__(256) void head_dz_kernel(int n_nodes, int R, const float* __restrict__ Ssm,
+                                                      const float* __restrict__ W, const int* __restrict__ hptr,
+                                                      const int* __restrict__ hperm, const float* __restrict__ dWedge,
+                                                      const float* __restrict__ dwh, float* __restrict__ dz) {
+    const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_nodes) return;
+    float dw[MAX_R];
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r) dw[r] = r < R ? dwh[n * R + r] : 0.f;
+    const int beg = hptr[n], end = hptr[n + 1];
+    if (R == 8) {          // the 32-B rows as two 16-B loads (scalar loads: eight transactions per row)
+        for (int k = beg; k < end; ++k) {
+            const float* row = dWedge + (long long)hperm[k] * 8;
+            const f32x4 a = ld4(row), b = ld4(row + 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                dw[r] += a[r];
+                dw[r + 4] += b[r];
+            }
+        }
+    } else {
+        for (int k = beg; k < end; ++k) {
+            const float* row = dWedge + (long long)hperm[k] * R;
+#pragma unroll
+            for (int r = 0; r < MAX_R; ++r)
+                if (r < R) dw[r] += row[r];
+        }
+    }
+    float dsv[MAX_R], sv[MAX_R];
+    float dot = 0.f;
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) {
+            sv[r] = Ssm[n * R + r];
+            const float w = W[n * R + r];
+            dsv[r] = dw[r] * w * (1.0f - w);
+            dot += dsv[r] * sv[r];
+        }
+#pragma unroll
+    for (int r = 0; r < MAX_R; ++r)
+        if (r < R) dz[n * R + r] = (dsv[r] - dot) * sv[r];
 }
 
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(int n_slabs, long long n, const float* __restrict__ slab,
@@ -3617,6 +3726,22 @@ int run_combine_out(void* stream, int M, int d, int R, const float* Y, const int
 inline unsigned grid_for(long long rows, int lpr) {
     const long long threads = rows * lpr;
     return (unsigned)((threads + 255) / 256);
+}
+
+// the config-5 tail reduction on MFMAs (tail_seg_mfma8_kernel), with or without the head chain's node terms
+void launch_tail_mfma8(hipStream_t st, int n_nodes, const int* seg_ptr, const float* W, const void* dO,
+                       const float* P, long long p_rel_stride, float* dP, long long dp_rel_stride, float* dsum,
+                       float* dWedge, const float* head_dO, const float* Wn, float* dwh) {
+    const unsigned g4 = (unsigned)((n_nodes + 3) / 4);
+#define TM8(DS, HD) hipLaunchKernelGGL((tail_seg_mfma8_kernel<DS, HD>), dim3(g4), dim3(256), 0, st, n_nodes, seg_ptr, W, (const __bf16*)dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge, head_dO, Wn, dwh)
+    if (head_dO) {
+        if (dsum) TM8(true, true);
+        else TM8(false, true);
+    } else {
+        if (dsum) TM8(true, false);
+        else TM8(false, false);
+    }
+#undef TM8
 }
 
 }  // namespace
@@ -4128,7 +4253,7 @@ int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const floa
                              long long dp_rel_stride, float* dsum, float* dz) {
     if (!dim_ok(d)) return IDDGCN_E_BAD_DIM;
     if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
-    if (n_nodes < 0 || !dO || !P || !Ssm || !W || !dP || !dz) return IDDGCN_E_BAD_ARG;
+    if (n_nodes < 0 || !dO || !P || !Ssm || !W || !dz) return IDDGCN_E_BAD_ARG;
     if (hseg_ptr && (!hperm || !dWedge)) return IDDGCN_E_BAD_ARG;
     if (n_nodes == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
@@ -4275,6 +4400,30 @@ int iddgcn_distmult_bce_heads_bf16(void* stream, int n_nodes, int d, int R, cons
     return launch_status();
 }
 
+int iddgcn_tail_seg_reduce_head_bf16(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const float* W,
+                                     const void* dO, const float* P, long long p_rel_stride, float* dP,
+                                     long long dp_rel_stride, float* dsum, float* dWedge, const float* head_dO,
+                                     const float* Wn, float* dwh) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (R != 8) return IDDGCN_E_BAD_REL;
+    if (n_nodes < 0 || !seg_ptr || !W || !dO || !P || !dP || !dWedge || !head_dO || !Wn || !dwh)
+        return IDDGCN_E_BAD_ARG;
+    if (n_nodes == 0) return 0;
+    launch_tail_mfma8((hipStream_t)stream, n_nodes, seg_ptr, W, dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge,
+                      head_dO, Wn, dwh);
+    return launch_status();
+}
+
+int iddgcn_head_dz_f32(void* stream, int n_nodes, int R, const float* Ssm, const float* W, const int* hseg_ptr,
+                       const int* hperm, const float* dWedge, const float* dwh, float* dz) {
+    if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
+    if (n_nodes < 0 || !Ssm || !W || !hseg_ptr || !hperm || !dWedge || !dwh || !dz) return IDDGCN_E_BAD_ARG;
+    if (n_nodes == 0) return 0;
+    hipLaunchKernelGGL(head_dz_kernel, dim3((unsigned)((n_nodes + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       n_nodes, R, Ssm, W, hseg_ptr, hperm, dWedge, dwh, dz);
+    return launch_status();
+}
+
 int iddgcn_tail_seg_reduce_bf16(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* h_idx,
                                 const float* W, const void* dO, const float* P, long long p_rel_stride, float* dP,
                                 long long dp_rel_stride, float* dsum, float* dWedge) {
@@ -4286,13 +4435,8 @@ int iddgcn_tail_seg_reduce_bf16(void* stream, int n_nodes, int d, int R, const i
     const unsigned grid = grid_for(n_nodes, 64);
     const float* d_o = (const float*)dO;
     if (R == 8 && !h_idx) {          // per-edge W, 8 relations (config 5): the MFMA form
-        const unsigned g4 = (unsigned)((n_nodes + 3) / 4);
-        if (dsum)
-            hipLaunchKernelGGL((tail_seg_mfma8_kernel<true>), dim3(g4), dim3(256), 0, st, n_nodes, seg_ptr, W,
-                               (const __bf16*)dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge);
-        else
-            hipLaunchKernelGGL((tail_seg_mfma8_kernel<false>), dim3(g4), dim3(256), 0, st, n_nodes, seg_ptr, W,
-                               (const __bf16*)dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge);
+        launch_tail_mfma8(st, n_nodes, seg_ptr, W, dO, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge, nullptr,
+                          nullptr, nullptr);
         return launch_status();
     }
 #define TKB(RR) hipLaunchKernelGGL((tail_seg_reduce_kernel<256, RR, true>), dim3(grid), dim3(256), 0, st, n_nodes, seg_ptr, h_idx, W, d_o, P, p_rel_stride, dP, dp_rel_stride, dsum, dWedge)

@@ -190,6 +190,7 @@ class Workspace:
         self.dAE = e(R, N, D)
         self.dES = e(N, D)
         self.dz = e(N, R)
+        self.dwh = e(N, R)                      # <head seed, P_r> per node (fused R = 8 tail + head backward)
         self.WaT = e(R, D)
         self.drel_slab = e(self.nb_dm * R * D)
         self.loss_slab = e(self.nb_dm)
@@ -437,10 +438,19 @@ class Engine:
             # first waits for everything queued so far (the previous layer's readers of dP), and the
             # main stream waits for it before the head-side work that reads dP, dWedge
             side = self._side_stream() if (self.overlap and l > 0) else None
+            # bf16 edge tables at R = 8, D = 256 (config 5): the tail reduction on MFMAs adds the head chain's node terms
+            # (Wl[n] dO[n] into dP, dO[n] into dES) before its store, so the head backward below skips them
+            fused = self.features == "bf16" and R == 8 and D == 256 and self.node_shard is None
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(side):
-                    ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge)
+                    if fused:
+                        ops.tail_seg_reduce_head(ed.tptr, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge, dOn, Wl, ws.dwh)
+                    else:
+                        ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge)
+            elif fused:
+                ops.tail_seg_reduce_head(ed.tptr, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge, dOn, Wl, ws.dwh,
+                                         dsum=ws.dES if l == 0 else None)
             else:
                 ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
                                     dsum=ws.dES if l == 0 else None)
@@ -454,8 +464,11 @@ class Engine:
             if side is not None:
                 torch.cuda.current_stream().wait_stream(side)
             # head side (node level)
-            ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
-                              dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)
+            if fused:
+                ops.head_dz(ws.Ssm[l], Wl, ed.hptr, ed.hperm, ws.dWedge, ws.dwh, ws.dz)
+            else:
+                ops.head_bwd_node(dOn, Pl, ws.Ssm[l], Wl, ws.dP, ws.dz, hseg_ptr=ed.hptr, hperm=ed.hperm,
+                                  dWedge=ws.dWedge, dsum=ws.dES if l == 0 else None)
             Xin = ws.X[l - 1] if l > 0 else P["E"]
             ws.WaT.copy_(P[f"Wa{l + 1}"].t())
             ops.gemm_tn_narrow(Xin, ws.dz, G[f"Wa{l + 1}"], G[f"ba{l + 1}"], ws.narrow_slab)
@@ -537,27 +550,26 @@ class Engine:
                 ops.rowgemm_batched(proj[i:i + 16])
             ops.alpha_fwd(E[a:b], P["Wa1"], P["ba1"], ws.Ssm[0][a:b], ws.W[0][a:b])
         sh.all_gather(ws.W[0])
-        ops.gather_rows(ws.W[0], ed.h, ws.Wedge[0])
+        # node level first (layers 1-3 over the owned rows, W^l all-gathered as each layer's alpha is known), so
+        # that DistMult's head rows X^3 travel while ALL of the tail side runs (the layer-1 combine, the two tail
+        # GEMMs: they read x^l, P^l, ES1 and the gathered W^l, and write x^l, nothing of X^3)
         if b > a:
             ops.combine(ws.ES1, ws.W[0][a:b], ws.P[0], ws.X[0][a:b], y_idx=idx, v_idx=idx)
-        pl = self.use_planes
-        ops.combine(ws.ES1, ws.Wedge[0], ws.P[0], ws.xt[0], y_idx=ed.t, v_idx=ed.t, planes_out=pl)
-        x3 = None
         for l in (1, 2):
-            S = P[f"S{l + 1}"]
             if b > a:
                 ops.alpha_fwd(ws.X[l - 1][a:b], P[f"Wa{l + 1}"], P[f"ba{l + 1}"], ws.Ssm[l][a:b], ws.W[l][a:b])
             sh.all_gather(ws.W[l])
-            ops.gather_rows(ws.W[l], ed.h, ws.Wedge[l])
             if b > a:
-                ops.rowgemm(ws.X[l - 1][a:b], S, ws.X[l][a:b], coef=ws.W[l][a:b], V=ws.P[l], v_idx=idx,
+                ops.rowgemm(ws.X[l - 1][a:b], P[f"S{l + 1}"], ws.X[l][a:b], coef=ws.W[l][a:b], V=ws.P[l], v_idx=idx,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID, **pr)
-            if l == 2:
-                # DistMult's head rows X^3 travel while the layer-3 tail GEMM runs (it reads x^2, P^3, Wedge^3 and
-                # writes x^3: nothing of X^3)
-                x3 = sh.all_gather(ws.X[2], async_op=True)
+        x3 = sh.all_gather(ws.X[2], async_op=True)
+        pl = self.use_planes
+        ops.gather_rows(ws.W[0], ed.h, ws.Wedge[0])
+        ops.combine(ws.ES1, ws.Wedge[0], ws.P[0], ws.xt[0], y_idx=ed.t, v_idx=ed.t, planes_out=pl)
+        for l in (1, 2):
+            ops.gather_rows(ws.W[l], ed.h, ws.Wedge[l])
             with self._mark("tail_fwd_gemm"):
-                ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
+                ops.rowgemm(ws.xt[l - 1], P[f"S{l + 1}"], ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID,
                             planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, **pr)
         x3.wait()

@@ -358,6 +358,40 @@ def seg_gather_reduce(seg_ptr, rows, out, *, perm=None, coef=None, r_idx=None, r
             "seg_gather_reduce")
 
 
+def tail_seg_reduce_head(seg_ptr, W, dO, P, dP, dWedge, head_dO, Wn, dwh, dsum=None):
+    """tail_seg_reduce with per-edge W on bf16 rows at R = 8, D = 256, fused with the head chain's node terms of the
+    same layer (iddgcn_tail_seg_reduce_head_bf16, ABI 9): dP[r][n] = tail sum + Wn[n][r] head_dO[n], dsum[n] = tail
+    sum + head_dO[n], dwh[n][r] = <head_dO[n], P_r[n]>; the head backward is then head_dz."""
+    R, n_nodes, D = P.shape
+    _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")
+    _req(P, _F32, (R, n_nodes, D), "P")
+    _req(dP, _F32, (R, n_nodes, D), "dP")
+    _req(dsum, _F32, (n_nodes, D), "dsum")
+    _req(head_dO, _F32, (n_nodes, D), "head_dO")
+    _req(Wn, _F32, (n_nodes, R), "Wn")
+    _req(dwh, _F32, (n_nodes, R), "dwh")
+    _req(dO, _BF16, None, "dO")
+    if W.shape[0] != dO.shape[0]:
+        raise L.IddgcnError("tail_seg_reduce_head: per-edge W must have one row per edge")
+    L.check(L.lib().iddgcn_tail_seg_reduce_head_bf16(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(W), _ptr(dO),
+                                                     _ptr(P), n_nodes * D, _ptr(dP), n_nodes * D, _ptr(dsum),
+                                                     _ptr(dWedge), _ptr(head_dO), _ptr(Wn), _ptr(dwh)),
+            "tail_seg_reduce_head")
+
+
+def head_dz(Ssm, W, hseg_ptr, hperm, dWedge, dwh, dz):
+    """The head backward after tail_seg_reduce_head (iddgcn_head_dz_f32, ABI 9): dW_r = dwh[n][r] + the head
+    segment's dWedge rows, then the softmax-sigmoid backward into dz (n, R)."""
+    n_nodes, R = dz.shape
+    for t, nm in ((Ssm, "Ssm"), (W, "W"), (dwh, "dwh"), (dz, "dz")):
+        _req(t, _F32, (n_nodes, R), nm)
+    _req(hseg_ptr, _I32, (n_nodes + 1,), "hseg_ptr")
+    _req(hperm, _I32, None, "hperm")
+    _req(dWedge, _F32, None, "dWedge")
+    L.check(L.lib().iddgcn_head_dz_f32(_stream(), n_nodes, R, _ptr(Ssm), _ptr(W), _ptr(hseg_ptr), _ptr(hperm),
+                                       _ptr(dWedge), _ptr(dwh), _ptr(dz)), "head_dz")
+
+
 def tail_seg_reduce(seg_ptr, h_idx, W, dO, P, dP, dWedge, dsum=None):
     R, n_nodes, D = P.shape
     _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")
@@ -385,11 +419,14 @@ def head_bwd_node(dO, P, Ssm, W, dP, dz, *, hseg_ptr=None, hperm=None, dWedge=No
     _req(dsum, _F32, (n_nodes, D), "dsum")
     _req(ep, _F32, (n_nodes, R), "ep")
     for t, nm in ((P, "P"), (dP, "dP")):
+        if t is None:             # dP None (ABI 9): its head term was added by tail_seg_reduce_head
+            continue
         if tuple(t.shape) != (R, n_nodes, D) or t.stride(1) != D or t.stride(2) != 1:
             raise L.IddgcnError(f"head_bwd_node: {nm} must be (R, n, D) with contiguous rows")
     L.check(L.lib().iddgcn_head_bwd_node_f32(_stream(), n_nodes, D, R, _ptr(dO), _ptr(P), P.stride(0), _ptr(Ssm),
                                              _ptr(W), _ptr(hseg_ptr), _ptr(hperm), _ptr(dWedge), _ptr(ep), _ptr(dP),
-                                             dP.stride(0), _ptr(dsum), _ptr(dz)), "head_bwd_node")
+                                             dP.stride(0) if dP is not None else 0, _ptr(dsum), _ptr(dz)),
+            "head_bwd_node")
 
 
 def head_wsum(hptr, hperm, w, out):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 8
+#define IDDGCN_ABI_VERSION 9
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -249,7 +249,8 @@ int iddgcn_tail_seg_reduce_f32(void* stream, int n_nodes, int d, int R, const in
  *   dsum[n] += dO[n]                                   (if dsum)
  *   dW_r     = <dO[n], P[r][n]> + sum_{k in hseg(n)} dWedge[hperm[k]][r] (+ ep_in[n][r] if ep_in)
  *   ds_r     = dW_r w_r (1-w_r);  dz[n][j] = s_j (ds_j - sum_r ds_r s_r)   (softmax-sigmoid backward)
- *   dP[r][n] += w_r * dO[n]
+ *   dP[r][n] += w_r * dO[n]                             (skipped when dP is NULL, ABI 9: added by
+ *                                                        iddgcn_tail_seg_reduce_head_bf16)
  * ep_in (ABI 8): per-node head sums of dWedge computed elsewhere (a node-partitioned step: each rank's
  * iddgcn_head_wsum_f32 over its edges, summed across the ranks), hseg_ptr NULL then.          */
 int iddgcn_head_bwd_node_f32(void* stream, int n_nodes, int d, int R, const float* dO,
@@ -323,6 +324,26 @@ int iddgcn_distmult_bce_heads_bf16(void* stream, int n_nodes, int d, int R, cons
 int iddgcn_tail_seg_reduce_bf16(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const int* h_idx,
                                 const float* W, const void* dO, const float* P, long long p_rel_stride, float* dP,
                                 long long dp_rel_stride, float* dsum, float* dWedge);
+
+/* ABI 9: iddgcn_tail_seg_reduce_bf16 (per-edge W, R = 8, d = 256 only) fused with the head chain's node terms of the
+ * same layer (IDDGCN.py:66-77 autodiff, node n):
+ *   dP[r][n][:] = sum_{e in seg(n)} W[e][r] dO[e][:]  +  Wn[n][r] * head_dO[n][:]
+ *   dsum[n][:]  = sum_{e in seg(n)} dO[e][:]          +  head_dO[n][:]            (if dsum)
+ *   dWedge      as iddgcn_tail_seg_reduce_bf16
+ *   dwh[n][r]   = <head_dO[n], P[r][n]>                                      (the node's own part of dW_r)
+ * so the head backward is then only iddgcn_head_dz_f32 (the R node tables are written once instead of written, read
+ * and rewritten, and P and head_dO are not read again).  head_dO: the layer's head seed (n_nodes x d fp32), Wn: its
+ * node-level dynamic weights (n_nodes x R), dwh: n_nodes x R output. */
+int iddgcn_tail_seg_reduce_head_bf16(void* stream, int n_nodes, int d, int R, const int* seg_ptr, const float* W,
+                                     const void* dO, const float* P, long long p_rel_stride, float* dP,
+                                     long long dp_rel_stride, float* dsum, float* dWedge, const float* head_dO,
+                                     const float* Wn, float* dwh);
+
+/* ABI 9: the rest of iddgcn_head_bwd_node_f32 after iddgcn_tail_seg_reduce_head_bf16, node n:
+ *   dW_r = dwh[n][r] + sum_{k in hseg(n)} dWedge[hperm[k]][r];  ds_r = dW_r w_r (1-w_r);
+ *   dz[n][j] = s_j (ds_j - sum_r ds_r s_r)                                  (W = Wn, s = Ssm; n_nodes x R each) */
+int iddgcn_head_dz_f32(void* stream, int n_nodes, int R, const float* Ssm, const float* W, const int* hseg_ptr,
+                       const int* hperm, const float* dWedge, const float* dwh, float* dz);
 
 #ifdef __cplusplus
 }

@@ -189,3 +189,42 @@ def test_tail_seg_mfma8_bf16(case, dsum, cuda):
     if dsum:
         ref = torch.zeros(N, D, dtype=torch.float64, device=cuda).index_add_(0, tc, d64)
         assert (outs[0][2].double() - ref).abs().max().item() <= 1e-5 * max(ref.abs().max().item(), 1e-30)
+
+
+@pytest.mark.parametrize("dsum", [False, True])
+def test_tail_seg_reduce_head_fused_equals_two_calls(dsum, cuda):
+    """iddgcn_tail_seg_reduce_head_bf16 (ABI 9: the R = 8 tail reduction that adds the head chain's node terms
+    Wn[n] head_dO[n] to dP and head_dO[n] to dsum before its store, and forms dwh[n] = <head_dO[n], P_r[n]>) followed
+    by head_dz equals tail_seg_reduce + head_bwd_node: dP, dsum, dWedge, dz within 1e-6 of max|ref| (the same terms in
+    other fp32 orders); dwh within 1e-6 of float64."""
+    g = torch.Generator().manual_seed(5 + dsum)
+    R, N, M = 8, 600, 20_000
+    t = tails(M, N, g).to(cuda).int()
+    M = len(t)
+    tptr = torch.searchsorted(t, torch.arange(N + 1, device=cuda, dtype=torch.int32)).int()
+    W = torch.rand(M, R, generator=g).to(cuda)
+    P = torch.randn(R, N, D, generator=g).to(cuda)
+    dO = bf(torch.randn(M, D, generator=g)).to(cuda)
+    hd = torch.randn(N, D, generator=g).to(cuda)
+    Wn = torch.rand(N, R, generator=g).to(cuda)
+    Ssm = torch.rand(N, R, generator=g).to(cuda)
+    h = torch.randint(0, N, (M,), generator=g).to(cuda)
+    hperm = torch.argsort(h, stable=True).int()
+    hptr = torch.searchsorted(h[hperm.long()], torch.arange(N + 1, device=cuda)).int()
+    out = []
+    for fused in (False, True):
+        dP, dWe = torch.empty(R, N, D, device=cuda), torch.empty(M, R, device=cuda)
+        ds = torch.empty(N, D, device=cuda) if dsum else None
+        dz = torch.empty(N, R, device=cuda)
+        if fused:
+            dwh = torch.empty(N, R, device=cuda)
+            ops.tail_seg_reduce_head(tptr, W, dO, P, dP, dWe, hd, Wn, dwh, dsum=ds)
+            ops.head_dz(Ssm, Wn, hptr, hperm, dWe, dwh, dz)
+            ref = torch.einsum("nd,rnd->nr", hd.double(), P.double())
+            assert maxrel(dwh, ref) <= 1e-6
+        else:
+            ops.tail_seg_reduce(tptr, None, W, dO, P, dP, dWe, dsum=ds)
+            ops.head_bwd_node(hd, P, Ssm, Wn, dP, dz, hseg_ptr=hptr, hperm=hperm, dWedge=dWe, dsum=ds)
+        out.append([dP, dWe, dz] + ([ds] if dsum else []))
+    for a, b in zip(*out):
+        assert maxrel(b, a.double()) <= 1e-6

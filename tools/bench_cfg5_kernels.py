@@ -55,10 +55,21 @@ def main():
         "head_bwd_node": (lambda: ops.head_bwd_node(ws.dOn_a, ws.P[1], ws.Ssm[1], ws.W[1], ws.dP, ws.dz,
                                                     hseg_ptr=ed.hptr, hperm=ed.hperm, dWedge=ws.dWedge),
                           lambda: [ws.dP, ws.dz]),
+        "head_bwd_node (no dP)": (lambda: ops.head_bwd_node(ws.dOn_a, ws.P[1], ws.Ssm[1], ws.W[1], None, ws.dz,
+                                                            hseg_ptr=ed.hptr, hperm=ed.hperm, dWedge=ws.dWedge),
+                                  lambda: [ws.dz]),
+        "tail + head (2 passes)": (lambda: (ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[1], do, ws.P[1], ws.dP, ws.dWedge),
+                                            ops.head_bwd_node(ws.dOn_a, ws.P[1], ws.Ssm[1], ws.W[1], ws.dP, ws.dz,
+                                                              hseg_ptr=ed.hptr, hperm=ed.hperm, dWedge=ws.dWedge)),
+                                   lambda: [ws.dP, ws.dz]),
+        "tail+head fused": (lambda: (ops.tail_seg_reduce_head(ed.tptr, ws.Wedge[1], do, ws.P[1], ws.dP, ws.dWedge,
+                                                               ws.dOn_a, ws.W[1], ws.dwh),
+                                     ops.head_dz(ws.Ssm[1], ws.W[1], ed.hptr, ed.hperm, ws.dWedge, ws.dwh, ws.dz)),
+                            lambda: [ws.dP, ws.dz]),
         "distmult_heads": (lambda: ops.distmult_bce_heads(ed.hptr, ed.hperm, ws.X[2], ws.xt[2], ed.r, P["rel"], ed.y,
                                                           ws.xt[0], ws.dOn_b, ws.drel_slab, ws.loss_slab,
                                                           scale=1.0 / (T * N)),
-                           lambda: [ws.xt[0], ws.dOn_b, ws.loss_slab]),
+                           lambda: [ws.xt[0], ws.dOn_b, ws.loss_slab, ws.drel_slab]),
     }
     ref = {}
     for lp in libs:
