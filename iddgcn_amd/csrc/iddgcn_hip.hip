@@ -1541,23 +1541,44 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
     }
 }
 
-// ---------------------------------------------------------------------------
-// TN reduction GEMM, D = 256, bf16 operands (the bf16-feature mode): C = A^T B over bf16 edge tables,
-// same partial-slab contract as the fp32 TN kernels.  Per 32-row tile the 512-B bf16 rows of A and B
-// are DMA'd (32 lanes per row) into 1040-B LDS rows, then wave w transposes column block w of each
-// operand IN PLACE (32 rows x 32 bf16 = 2 KB, wave-private) so that column 32w+i lies k-contiguous in
-// row i's bytes [64w, 64w+64): an MFMA fragment (8 consecutive rows of one column) is one
-// ds_read_b128.  One v_mfma_f32_32x32x16_bf16 per (k-step, column block); fp32 accumulation.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void gemm_tn256_bf16_kernel(long long M, long long rows_per_block,
-                                                              const __bf16* __restrict__ A,
-                                                              const __bf16* __restrict__ B,
-                                                              float* __restrict__ slab) {
-    using namespace tn3;
-    __shared__ __attribute__((aligned(16))) float lds[2 * 2 * TILE];      // [buf][A|B][TK][LDR]
+// s_waitcnt vmcnt(min(n, 15)) for a run-time, wave-uniform n: every vector-memory op of this wave but the n
+// youngest has completed (LDS-DMA, loads and stores count together, in issue order)
+__device__ __forceinline__ void wait_vm(int n) {
+#define WVM(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    switch (n < 15 ? n : 15) {
+        WVM(0) WVM(1) WVM(2) WVM(3) WVM(4) WVM(5) WVM(6) WVM(7)
+        WVM(8) WVM(9) WVM(10) WVM(11) WVM(12) WVM(13) WVM(14)
+        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+#undef WVM
+}
+// TN reduction GEMM over bf16 edge tables, transposed reads (round 4; replaces gemm_tn256_bf16_kernel's in-LDS
+// software transpose: 32 two-byte LDS reads and 8 writes per lane per tile and two barriers).  The 512-B rows of
+// A and B arrive by LDS-DMA (32 lanes per row) into 576-B row slots (144 dwords = 16 mod 64 banks: the 32 lanes of a
+// transposed read, 4 rows x 64 B, are conflict-free), three 32-row buffers deep (four ran slower: 11.55 vs 11.06 ms
+// per config-5 launch, profiles/r04/cfg5/tn_bf16t_ab.txt); the MFMA fragments (8 consecutive
+// rows of one column) come straight from the row-major rows through ds_read_b64_tr_b16.  Wave w owns output rows
+// 32w..32w+31 (columns of A) x all 256 columns (8 accumulator tiles); one v_mfma_f32_32x32x16_bf16 per (k-step,
+// column tile), rows 16s..16s+15 of the tile in k-step s with the same lane k-order as the old kernel, so the
+// partials are bitwise its own.  One barrier per tile.
+namespace tbf {
+constexpr int D = 256, TK = 32, PT = 576, OPB = TK * PT, BUF = 2 * OPB, NBUF = 3, PD = NBUF - 1;
+}  // namespace tbf
+__device__ __forceinline__ bf16x8 tr_frag_bf(const char* p0) {
+    typedef __attribute__((address_space(3))) v4s16* l4p;
+    const v4s16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)p0);
+    const v4s16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)(p0 + 4 * tbf::PT));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+__global__ __launch_bounds__(512) void gemm_tn256_bf16t_kernel(long long M, long long rows_per_block,
+                                                               const __bf16* __restrict__ A,
+                                                               const __bf16* __restrict__ B,
+                                                               float* __restrict__ slab) {
+    using namespace tbf;
+    static_assert(NBUF * BUF <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * BUF];     // [buf][A | B][TK][PT]
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int i = lane & 31, h = lane >> 5;
     f32x16 acc[8];
 #pragma unroll
     for (int cj = 0; cj < 8; ++cj)
@@ -1567,71 +1588,76 @@ __global__ __launch_bounds__(512) void gemm_tn256_bf16_kernel(long long M, long 
     long long r_end = r_beg + rows_per_block;
     if (r_end > M) r_end = M;
     const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
-
-    auto stage = [&](long long t, int b) {          // wave w stages rows 4w..4w+3 of both operands
-        float* As = lds + (b * 2 + 0) * TILE;
-        float* Bs = lds + (b * 2 + 1) * TILE;
+    // rows 4w .. 4w+3 of both operands of tile t into buffer bb, 32 lanes (16 B each) per row, rows past the range
+    // as zeros; returns the LDS-DMA count (wave-uniform)
+    auto stage = [&](long long t, int bb) __attribute__((always_inline)) {
+        int n = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int r = wave * 4 + j;
+            const int r = 4 * wave + j;
             const long long e = r_beg + t * TK + r;
+            char* ra = lds + bb * BUF + r * PT;
             if (e < r_end) {
                 if (lane < 32) {
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)(A + e * D + lane * 8), (lds_vptr)(As + r * LDR), 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)(B + e * D + lane * 8), (lds_vptr)(Bs + r * LDR), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)(A + e * D + lane * 8), (lds_vptr)ra, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)(B + e * D + lane * 8), (lds_vptr)(ra + OPB), 16, 0, 0);
                 }
+                n += 2;
             } else if (lane < 32) {
-                st4(As + r * LDR + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
-                st4(Bs + r * LDR + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                st4(reinterpret_cast<float*>(ra) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                st4(reinterpret_cast<float*>(ra + OPB) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+            }
+        }
+        return n;
+    };
+    auto wait_newest = [&](int n) __attribute__((always_inline)) { wait_vm(n); };
+    // this lane's transposed-read address: rows 8(l>>5) + ((l>>2)&3) (+4: second read), columns
+    // 16((l>>4)&1) + 4(l&3) of a 32-column block
+    const int roff = (8 * (lane >> 5) + ((lane >> 2) & 3)) * PT + 2 * (16 * ((lane >> 4) & 1) + 4 * (lane & 3));
+    auto mfma_tile = [&](int bb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < TK / 16; ++s) {
+            const char* base = lds + bb * BUF + 16 * s * PT + roff;
+            const bf16x8 a = tr_frag_bf(base + 64 * wave);
+            bf16x8 b = tr_frag_bf(base + OPB);
+#pragma unroll
+            for (int cj = 0; cj < 8; ++cj) {
+                bf16x8 nb = b;                              // column tile cj+1's fragment in flight
+                if (cj + 1 < 8) nb = tr_frag_bf(base + OPB + 64 * (cj + 1));
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[cj], 0, 0, 0);
+                b = nb;
             }
         }
     };
-    // transpose column block `wave` of one bf16 tile in place (lane (i, h): column 32w+i, rows 16h..16h+15)
-    auto transpose_block = [&](float* T) {
-        const unsigned short* src = reinterpret_cast<const unsigned short*>(T);
-        s16x4 v[4];
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-            v[r >> 2][r & 3] = (short)src[(16 * h + r) * (LDR * 2) + 32 * wave + i];
-        char* seg = reinterpret_cast<char*>(T + i * LDR) + 64 * wave + 32 * h;
-        *reinterpret_cast<s16x4*>(seg) = v[0];
-        *reinterpret_cast<s16x4*>(seg + 8) = v[1];
-        *reinterpret_cast<s16x4*>(seg + 16) = v[2];
-        *reinterpret_cast<s16x4*>(seg + 24) = v[3];
-    };
-    auto transpose = [&](int b) {
-        transpose_block(lds + (b * 2 + 0) * TILE);
-        transpose_block(lds + (b * 2 + 1) * TILE);
-    };
+    // cnt[k]: the LDS-DMA count of the tile in buffer k (the waits below let the younger tiles' DMAs fly)
+    int cnt[NBUF] = {};
     if (nt > 0) {
-        stage(0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        transpose(0);
+#pragma unroll
+        for (int k = 0; k < PD; ++k) cnt[k] = k < nt ? stage(k, k) : 0;
+        int younger = 0;                            // tile 0 landed: tiles 1 .. PD-1 may still fly
+#pragma unroll
+        for (int k = 1; k < PD; ++k) younger += cnt[k];
+        wait_newest(younger);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();
     }
     int b = 0;
-    for (long long t = 0; t < nt; ++t, b ^= 1) {
-        if (t + 1 < nt) stage(t + 1, b ^ 1);
-        const char* Aseg = reinterpret_cast<const char*>(lds + (b * 2 + 0) * TILE + i * LDR) + 64 * wave;
-        const char* Bseg = reinterpret_cast<const char*>(lds + (b * 2 + 1) * TILE + i * LDR);
+    for (long long t = 0; t < nt; ++t) {
+        const int bn = (b + PD) % NBUF;             // the buffer tile t+PD goes to (read last in iteration t-1)
+        cnt[bn] = t + PD < nt ? stage(t + PD, bn) : 0;
+        mfma_tile(b);
+        // tile t+1 landed: only tiles t+2 .. t+PD may still fly
+        int younger = 0;
 #pragma unroll
-        for (int s = 0; s < TK / 16; ++s) {
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(Aseg + 32 * s + 16 * h);
-#pragma unroll
-            for (int cj = 0; cj < 8; ++cj) {
-                const bf16x8 bf = *reinterpret_cast<const bf16x8*>(Bseg + 64 * cj + 32 * s + 16 * h);
-                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[cj], 0, 0, 0);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t + 1 < nt) {
-            transpose(b ^ 1);
-            __syncthreads();
-        }
+        for (int k = 2; k <= PD; ++k) younger += cnt[(b + k) % NBUF];
+        wait_newest(younger);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        b = (b + 1) % NBUF;
     }
     float* out = slab + (long long)blockIdx.x * D * D;
+    const int i = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int cj = 0; cj < 8; ++cj)
 #pragma unroll
@@ -1710,17 +1736,6 @@ __device__ __forceinline__ void row_to_planes3(char* row, int lane) {
 //   * epilogue as the v3 kernel: gathered P_r[t] rows (the tile's distinct tails), per-edge coefficients
 //     and sigma' rows (or, accumulating, the old C rows) DMA'd into wave-private slabs ([32][16] fp32, XOR-swizzled 16-B groups); waves 4-7 run
 //     the epilogue of tile t-1 while waves 0-3 run tile t's MFMAs on the same SIMDs; one barrier per tile.
-// s_waitcnt vmcnt(min(n, 15)) for a run-time, wave-uniform n: every vector-memory op of this wave but the n
-// youngest has completed (LDS-DMA, loads and stores count together, in issue order)
-__device__ __forceinline__ void wait_vm(int n) {
-#define WVM(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    switch (n < 15 ? n : 15) {
-        WVM(0) WVM(1) WVM(2) WVM(3) WVM(4) WVM(5) WVM(6) WVM(7)
-        WVM(8) WVM(9) WVM(10) WVM(11) WVM(12) WVM(13) WVM(14)
-        default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    }
-#undef WVM
-}
 namespace rb3 {
 constexpr int D = 256, NW = 8, TR = 32, CWG = 128, CWV = 16;
 constexpr int PITCH = 1568;                 // A row slot: three 512-B planes + 32 B
@@ -4347,7 +4362,7 @@ int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const v
     long long rpb = (M + n_blocks - 1) / n_blocks;
     rpb = ((rpb + 31) / 32) * 32;
     if (rpb < 32) rpb = 32;
-    hipLaunchKernelGGL(gemm_tn256_bf16_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb,
+    hipLaunchKernelGGL(gemm_tn256_bf16t_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb,
                        (const __bf16*)A, (const __bf16*)B, slab);
     int rc = launch_status();
     if (rc) return rc;

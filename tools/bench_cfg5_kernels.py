@@ -6,6 +6,7 @@ with the first variant's).  Also prints the tail / head segment-length distribut
 
 usage: python tools/bench_cfg5_kernels.py [lib.so ...]
 """
+import os
 import sys
 
 import numpy as np
@@ -71,6 +72,11 @@ def main():
                                                           scale=1.0 / (T * N)),
                            lambda: [ws.xt[0], ws.dOn_b, ws.loss_slab, ws.drel_slab]),
     }
+    dS = torch.empty(D, D, device=dev)
+    cases["TN bf16 (dS)"] = (lambda: ops.gemm_tn(ws.xt[0], ws.xt[1], dS, ws.tn_slab), lambda: [dS])
+    only = os.environ.get("IDDGCN_CFG5_CASES")      # comma-separated case names (and "fwd") to time; default all
+    if only:
+        cases = {k: v for k, v in cases.items() if k in only.split(",")}
     ref = {}
     for lp in libs:
         if lp:
@@ -90,7 +96,7 @@ def main():
             print(f"{tag:14s} {name:24s} {ms:8.3f} ms  {same}", flush=True)
             del o
     # the forward R = 8 edge GEMM (layer 3: x^2 -> x^3, overwritten in place: timing only, after every comparison)
-    for lp in libs:
+    for lp in (libs if not only or "fwd" in only.split(",") else []):
         if lp:
             L._lib = load_lenient(lp)
         tag = lp.split("/")[-1] if lp else "default"
