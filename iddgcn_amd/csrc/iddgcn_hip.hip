@@ -3351,6 +3351,17 @@ __global__ __launch_bounds__(256) void head_bwd_node_kernel(int n_nodes, int R, 
         }
 }
 
+// dst[e][:] = src[idx[e]][:] for a row width of 4 or 8 floats: one thread per edge, 16-B loads and stores (the
+// per-element form below spent one index load and a 4-B access per float: 1.14 ms per config-5 launch)
+template <int W>
+__global__ __launch_bounds__(256) void gather_rows_vec_kernel(long long M, const float* __restrict__ src,
+                                                              const int* __restrict__ idx, float* __restrict__ dst) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= M) return;
+    const float* s = src + (long long)idx[e] * W;
+#pragma unroll
+    for (int q = 0; q < W; q += 4) st4(dst + e * W + q, ld4(s + q));
+}
 // dst[e][j] = src[idx[e]][j] for a narrow row width (per-edge copies of node tables)
 __global__ __launch_bounds__(256) void gather_rows_kernel(long long M, int width, const float* __restrict__ src,
                                                           const int* __restrict__ idx, float* __restrict__ dst) {
@@ -3375,49 +3386,32 @@ __global__ __launch_bounds__(256) void head_wsum_kernel(int n_nodes, int R, cons
     out[x] = s;
 }
 
-// The rest of the head backward after iddgcn_tail_seg_reduce_head_bf16, one thread per node: dW_r = dwh[n][r] + the
-// head segment's dWedge rows (in segment order), then the softmax-sigmoid backward of head_bwd_node_kernel -> dz
+// The rest of the head backward after iddgcn_tail_seg_reduce_head_bf16: 8 lanes per node, lane r < R owning
+// relation r: dW_r = dwh[n][r] + the head segment's dWedge rows (in segment order; the 8 lanes of a node read one
+// row's R contiguous floats together), then the softmax-sigmoid backward of head_bwd_node_kernel -> dz (the 8-lane
+// dot product by three xor shuffles).  One thread per node with the whole row per thread ran 1.83 ms per config-5
+// launch, latency-bound on its serial row loads.
 __global__ __launch_bounds__(256) void head_dz_kernel(int n_nodes, int R, const float* __restrict__ Ssm,
                                                       const float* __restrict__ W, const int* __restrict__ hptr,
                                                       const int* __restrict__ hperm, const float* __restrict__ dWedge,
                                                       const float* __restrict__ dwh, float* __restrict__ dz) {
-    const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= n_nodes) return;
-    float dw[MAX_R];
-#pragma unroll
-    for (int r = 0; r < MAX_R; ++r) dw[r] = r < R ? dwh[n * R + r] : 0.f;
-    const int beg = hptr[n], end = hptr[n + 1];
-    if (R == 8) {          // the 32-B rows as two 16-B loads (scalar loads: eight transactions per row)
-        for (int k = beg; k < end; ++k) {
-            const float* row = dWedge + (long long)hperm[k] * 8;
-            const f32x4 a = ld4(row), b = ld4(row + 4);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                dw[r] += a[r];
-                dw[r + 4] += b[r];
-            }
-        }
-    } else {
-        for (int k = beg; k < end; ++k) {
-            const float* row = dWedge + (long long)hperm[k] * R;
-#pragma unroll
-            for (int r = 0; r < MAX_R; ++r)
-                if (r < R) dw[r] += row[r];
-        }
-    }
-    float dsv[MAX_R], sv[MAX_R];
-    float dot = 0.f;
-#pragma unroll
-    for (int r = 0; r < MAX_R; ++r)
-        if (r < R) {
-            sv[r] = Ssm[n * R + r];
-            const float w = W[n * R + r];
-            dsv[r] = dw[r] * w * (1.0f - w);
-            dot += dsv[r] * sv[r];
-        }
-#pragma unroll
-    for (int r = 0; r < MAX_R; ++r)
-        if (r < R) dz[n * R + r] = (dsv[r] - dot) * sv[r];
+    const long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long n = x >> 3;
+    const int r = (int)(x & 7);
+    const bool live = n < n_nodes;
+    const bool on = live && r < R;
+    float dw = on ? dwh[n * R + r] : 0.f;
+    const int beg = live ? hptr[n] : 0, end = live ? hptr[n + 1] : 0;
+    for (int k = beg; k < end; ++k)
+        if (on) dw += dWedge[(long long)hperm[k] * R + r];
+    const float sv = on ? Ssm[n * R + r] : 0.f;
+    const float w = on ? W[n * R + r] : 0.f;
+    const float dsv = dw * w * (1.0f - w);
+    float dot = dsv * sv;
+    dot += __shfl_xor(dot, 1, 8);
+    dot += __shfl_xor(dot, 2, 8);
+    dot += __shfl_xor(dot, 4, 8);
+    if (on) dz[n * R + r] = (dsv - dot) * sv;
 }
 
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(int n_slabs, long long n, const float* __restrict__ slab,
@@ -4298,6 +4292,13 @@ int iddgcn_head_wsum_f32(void* stream, int n_nodes, int R, const int* hptr, cons
 int iddgcn_gather_rows_f32(void* stream, long long M, int width, const float* src, const int* idx, float* dst) {
     if (M < 0 || width < 1 || !src || !idx || !dst) return IDDGCN_E_BAD_ARG;
     if (M == 0) return 0;
+    const bool al16 = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+    if (al16 && (width == 4 || width == 8)) {
+        const unsigned g = (unsigned)((M + 255) / 256);
+        if (width == 8) hipLaunchKernelGGL((gather_rows_vec_kernel<8>), dim3(g), dim3(256), 0, (hipStream_t)stream, M, src, idx, dst);
+        else hipLaunchKernelGGL((gather_rows_vec_kernel<4>), dim3(g), dim3(256), 0, (hipStream_t)stream, M, src, idx, dst);
+        return launch_status();
+    }
     const long long n = M * width;
     hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, M,
                        width, src, idx, dst);
@@ -4434,8 +4435,8 @@ int iddgcn_head_dz_f32(void* stream, int n_nodes, int R, const float* Ssm, const
     if (R < 1 || R > MAX_R) return IDDGCN_E_BAD_REL;
     if (n_nodes < 0 || !Ssm || !W || !hseg_ptr || !hperm || !dWedge || !dwh || !dz) return IDDGCN_E_BAD_ARG;
     if (n_nodes == 0) return 0;
-    hipLaunchKernelGGL(head_dz_kernel, dim3((unsigned)((n_nodes + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       n_nodes, R, Ssm, W, hseg_ptr, hperm, dWedge, dwh, dz);
+    hipLaunchKernelGGL(head_dz_kernel, dim3((unsigned)(((long long)n_nodes * 8 + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, n_nodes, R, Ssm, W, hseg_ptr, hperm, dWedge, dwh, dz);
     return launch_status();
 }
 

@@ -72,6 +72,9 @@ def main():
                                                           scale=1.0 / (T * N)),
                            lambda: [ws.xt[0], ws.dOn_b, ws.loss_slab, ws.drel_slab]),
     }
+    cases["gather_rows W[h]"] = (lambda: ops.gather_rows(ws.W[1], ed.h, ws.Wedge[0]), lambda: [ws.Wedge[0]])
+    cases["head_dz"] = (lambda: ops.head_dz(ws.Ssm[1], ws.W[1], ed.hptr, ed.hperm, ws.dWedge, ws.dwh, ws.dz),
+                        lambda: [ws.dz])
     dS = torch.empty(D, D, device=dev)
     cases["TN bf16 (dS)"] = (lambda: ops.gemm_tn(ws.xt[0], ws.xt[1], dS, ws.tn_slab), lambda: [dS])
     only = os.environ.get("IDDGCN_CFG5_CASES")      # comma-separated case names (and "fwd") to time; default all

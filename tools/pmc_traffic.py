@@ -36,7 +36,7 @@ SYMBOLS = {
     # bench's gemm key with `python tools/pmc_traffic.py ... exact synthetic-5 1 profiles/r03 bf16`
     "bf16": {"tail_fwd_gemm": "rowgemm256_v3_kernel<8, false, true, true, false, true, false, false>",
              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, true, false, false>",
-             "tail_dS_tn": "gemm_tn256_bf16_kernel"},
+             "tail_dS_tn": "gemm_tn256_bf16t_kernel"},
 }
 
 
