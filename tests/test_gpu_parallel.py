@@ -120,7 +120,7 @@ def test_fit_world2_gloo_one_gpu_equals_single_process(cuda):
         assert np.abs(g0[k] - g).max() <= 2e-4 * np.abs(g).max() + 1e-30, k
 
 
-def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact"):
+def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact", features="f32"):
     """One data-parallel step (forward + backward + bucketed all-reduce, no Adam) on this rank's shard of
     the scored edges, edge-partitioned or with relation-sharded node tables.  "edge_device": the
     bucketed all-reduce on its device branch (asynchronous, in place on the GPU buckets, ordered after
@@ -136,7 +136,7 @@ def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact"):
         tri = np.concatenate([pos, neg])
         lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
         lo, hi = shard_range(len(tri), rank, world)
-        eng = Engine(N, R, D, dev, gemm=gemm)
+        eng = Engine(N, R, D, dev, gemm=gemm, features=features)
         if mode in ("node", "node_device"):
             from iddgcn_amd.parallel import NodeShard, node_ranges, node_shard_triples
             cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
@@ -226,31 +226,36 @@ def test_bwd_columns_partition_sums_to_full(cuda):
     assert (acc - full).abs().max().item() <= 1e-5 * full.abs().max().item()
 
 
-@pytest.mark.parametrize("world,N,R,D,gemm,mode", [(2, 600, 2, 64, "exact", "node"), (3, 601, 3, 256, "exact", "node"),
-                                                   (2, 700, 2, 256, "bf16x3", "node"), (3, 650, 2, 256, "split", "node"),
-                                                   (2, 700, 2, 256, "bf16x3", "node_device"),
-                                                   (3, 601, 3, 256, "exact", "node_device")])
-def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, mode, cuda):
+@pytest.mark.parametrize("world,N,R,D,gemm,mode,features", [
+    (2, 600, 2, 64, "exact", "node", "f32"), (3, 601, 3, 256, "exact", "node", "f32"),
+    (2, 700, 2, 256, "bf16x3", "node", "f32"), (3, 650, 2, 256, "split", "node", "f32"),
+    (2, 700, 2, 256, "bf16x3", "node_device", "f32"), (3, 601, 3, 256, "exact", "node_device", "f32"),
+    (2, 800, 8, 256, "split", "node_device", "bf16")])
+def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, mode, features, cuda):
     """Node-row partitioning (parallel.NodeShard, round 4): rank k owns a contiguous node range (balanced by tail
     edges + node work), computes the node tables of its rows only, takes the scored edges whose tail it owns;
     W^l and X^3 are all-gathered, the head seeds dO^3 and the dWedge head sums reduce-scattered, every gradient
     all-reduced.  world 2 and 3 ranks on one GPU over gloo: the step's loss and every gradient equal the
     single-process full batch (1e-5 of max|g|), bitwise equal on every rank.  mode "node_device": the collectives'
     device branch with asynchronous handles (X^3 gathered beside the layer-3 tail GEMM, dO^3 reduce-scattered
-    beside the layer-3 tail backward), over gloo on the GPU tables."""
+    beside the layer-3 tail backward), over gloo on the GPU tables.  features "bf16" (config 5's mode: R = 8, bf16
+    edge tables, the MFMA tail reduction): bitwise equal across ranks, and within the bf16 mode's own rounding of the
+    full batch (loss 1e-4 relative, gradients 1e-2 of max|g|: a node-level sum in another order can flip the
+    bf16 rounding of an edge-table element)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     pos, neg = synthetic_graph(N, R, 9000, seed=77)
     tri = np.concatenate([pos, neg])
     lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
-    eng = Engine(N, R, D, cuda, gemm=gemm)
+    eng = Engine(N, R, D, cuda, gemm=gemm, features=features)
     P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
     P.load(_mild(N, R, D, 9))
     loss, _ = eng.loss_and_grads(P, G, eng.adjacency(get_adj_mats(pos, N, R)), eng.edges(tri, lab))
     full, full_loss = G.to_numpy(), float(loss.item())
     del eng, P, G
     port = _free_port()
-    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q, mode, N, R, D, gemm)) for r in range(world)]
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q, mode, N, R, D, gemm, features))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
@@ -261,6 +266,7 @@ def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, mode, cuda):
         assert o[1] == out[0][1]
         assert all(np.array_equal(o[2][k], out[0][2][k]) for k in full)
     l, g = out[0][1], out[0][2]
-    assert abs(l - full_loss) <= 1e-6 * full_loss
+    bl, bg = (1e-4, 1e-2) if features == "bf16" else (1e-6, 1e-5)
+    assert abs(l - full_loss) <= bl * full_loss
     for k, v in full.items():
-        assert np.abs(g[k] - v).max() <= 1e-5 * np.abs(v).max() + 1e-30, k
+        assert np.abs(g[k] - v).max() <= bg * np.abs(v).max() + 1e-30, k
