@@ -285,7 +285,9 @@ struct RowGemmP {
 };
 
 // up to ROWGEMM_BATCH independent row GEMMs of one width in one launch (blockIdx.y = entry): the
-// node-level projections of a step are many tiny launches at the reference's 845 nodes
+// node-level projections of a step are many tiny launches at the reference's 845 nodes.  (25 entries, config 5's
+// whole projection set in one launch, computed entries 16-24 as zeros at N = 1M although a 20k-row 25-entry test
+// passed: 16 kept, cause not found)
 constexpr int ROWGEMM_BATCH = 16;
 struct RowGemmBatch {
     RowGemmP p[ROWGEMM_BATCH];
@@ -3737,6 +3739,304 @@ inline unsigned grid_for(long long rows, int lpr) {
     return (unsigned)((threads + 255) / 256);
 }
 
+// ---------------------------------------------------------------------------
+// Forward edge GEMM of the bf16-feature mode at R = 8 (config 5; round 4, replaces rowgemm256_v3_kernel<8, ..., BF>
+// for this form): x^l[e] = act(x^{l-1}[e] S + sum_r coef[e][r] V_r[v_idx[e]])  (IDDGCN.py:76-77 with the node-level
+// P_r^l = AE_r K_r^l as V), A and C bf16 edge tables, S fp32 as bf16 hi + lo pieces, coef [M][8] fp32 per edge,
+// V = 8 fp32 node tables v_rel_stride apart.  64-row tiles; wave w owns output columns 32w..32w+31.  Both terms run
+// on v_mfma_f32_16x16x32_bf16 with the weight / node-row side as operand A, so lane l ends with edge row l&15 of each
+// 16-row block at 4 consecutive columns: one 8-B bf16 store per 16 x 16 block, no LDS staging of the output.
+//   x S:     k-step q: A = S^T pieces (registers, 128 VGPRs: the wave's 32 columns x 256 k x hi / lo), B = 8
+//            consecutive k of an edge row straight from the LDS-DMA'd A tile (528-B row pitch: conflict-free b128).
+//   combine: the tile's distinct V rows ("slots": runs of equal v_idx; tail-sorted config-5 edges give 1-3 per
+//            64-row tile) are the k axis, k = 8 s + r for slot s < 4 of a block of four: A = V_r[slot s] at the lane's
+//            column (hi / lo), B = coef[e][r] where slot(e) = s, else 0 (hi / lo); three products (hi hi, hi lo,
+//            lo hi) per 16 x 16 block.  Slots 0-3 come by LDS-DMA (one instruction per slot: 8 relations x the wave's
+//            32 columns) a whole MFMA phase ahead; later slots of a tile (short runs, unsorted v_idx) are DMA'd when
+//            their block comes up.  The combine products carry 16 significant bits, as the weights' hi + lo do, 2^8
+//            below the bf16 rounding of the stored output.
+// The v3 epilogue this replaces read 8 KiB of fp32 V slab per edge row from LDS and ran 2048 FMAs per row on the
+// VALU; here the combine is 24 MFMAs per 64 x 32 wave tile plus 16 LDS reads and 48 two-piece splits per lane.
+// Schedule (every wave alike): A(t+2) DMA; wait for tile t-1's slots and A(t+1); epilogue of t-1; prepare t (slots,
+// coefficients, the next v_idx: wave-private, producer = consumer, the wave's own vmcnt); stores of t-1; MFMAs of t;
+// one barrier per tile (A buffers, three deep).  Measured per config-5 launch (tools/fg8_probe.py, one box): v3
+// kernel 24.7 ms; this design at 32-row tiles 20.6 ms with the v3 stagger (waves 4-7 one epilogue behind), 19.7 ms
+// all waves alike; 64-row tiles 18.1 ms; the stagger at 64 rows 20.3 ms (profiles/r04/fg8/).
+namespace fg8 {
+constexpr int D = 256, R = 8, TR = 64, NW = 8, NBUF = 3;
+constexpr int RPW = TR / NW;                             // A rows each wave DMAs per tile
+constexpr int PITCH = 528;                               // bytes per bf16 A row slot (512 + 16)
+constexpr int ABUF = TR * PITCH;                         // 33,792 B per A buffer
+constexpr int CAPS = 4;                                  // slots staged in LDS per tile (one block of the k axis)
+constexpr int SLOTB = 1088;                              // bytes per slot: [8 relations][32 columns] fp32 + 64 pad
+// per wave: v_idx [64], slot -> V row [64], coefficients [64][8], slots
+constexpr int WIDX = 0, WTAIL = 256, WCOEF = 512, WV = WCOEF + TR * R * 4;
+constexpr int WREG = WV + CAPS * SLOTB;                  // 6,912 B per wave
+constexpr int LDSB = NBUF * ABUF + NW * WREG;            // 156,672 B
+static_assert(LDSB <= 160 * 1024, "LDS budget");
+}  // namespace fg8
+
+__global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
+    using namespace fg8;
+    __shared__ __attribute__((aligned(16))) char lds[LDSB];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // per-lane index math inside the tile loop starts from an opaque copy of the lane id, so the compiler recomputes
+    // it (a few VALU ops) instead of hoisting every loop-invariant address and mask out of the loop (hoisted, they
+    // took the kernel past 256 VGPRs and into scratch, whose loads' vmcnt waits drain the DMAs in flight)
+    auto fresh_lane = [&]() __attribute__((always_inline)) {
+        int l = lane;
+        asm volatile("" : "+v"(l));
+        return l;
+    };
+    const int i16 = lane & 15, g = lane >> 4;
+    const int c0 = wave * 32;
+    char* wreg = lds + NBUF * ABUF + wave * WREG;
+    int* idxw = reinterpret_cast<int*>(wreg + WIDX);
+    int* tailw = reinterpret_cast<int*>(wreg + WTAIL);
+    float* coefw = reinterpret_cast<float*>(wreg + WCOEF);
+    char* vsl = wreg + WV;
+    const long long vrs = p.v_rel_stride;
+
+    const long long ntiles = ((long long)p.M + TR - 1) / TR;
+    const long long t_beg = (long long)blockIdx.x * p.tiles_per_block;
+    long long t_end = t_beg + p.tiles_per_block;
+    if (t_end > ntiles) t_end = ntiles;
+    if (t_beg >= t_end) return;                          // whole workgroup: before any barrier
+    const long long Mlast = (long long)p.M - 1;
+    auto clampe = [&](long long e) __attribute__((always_inline)) { return e > Mlast ? Mlast : e; };
+
+    // weights: lane (g, i16), column block cb, k-step q: S[32q + 8g + j][c0 + 16cb + i16], j < 8, as bf16 hi + lo
+    bf16x8 wh[2][8], wl[2][8];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float w = p.B[(32 * q + 8 * g + j) * D + c0 + 16 * cb + i16];
+                const __bf16 hi = (__bf16)w;
+                wh[cb][q][j] = hi;
+                wl[cb][q][j] = (__bf16)(w - (float)hi);
+            }
+
+    // vector-memory ops this wave has issued (wave-uniform): a wait for "op k and everything older" is
+    // s_waitcnt vmcnt(nops - k) (ops complete in issue order; LDS-DMA, loads and stores count alike)
+    int nops = 0;
+    auto dma_A = [&](long long t, int b) __attribute__((always_inline)) {
+        const int lane = fresh_lane();
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int r = wave * RPW + j;
+            const char* gp = reinterpret_cast<const char*>(p.A) + clampe(t * TR + r) * (D * 2) + (lane & 31) * 16;
+            if (lane < 32) __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(lds + b * ABUF + r * PITCH), 16, 0, 0);
+        }
+        nops += RPW;
+    };
+    auto dma_idx = [&](long long t) __attribute__((always_inline)) {
+        const int lane = fresh_lane();
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(p.v_idx + clampe(t * TR + lane)), (lds_vptr)idxw, 4, 0, 0);
+        nops += 1;
+    };
+    // prep(t): idx(t) has landed; find the slots of tile t (runs of equal v_idx; lane = row), DMA its slots < CAPS and
+    // its coefficients, then idx(t + 1) into the idx slot just read
+    unsigned long long msk = 0;                          // run starts of the prepared tile
+    auto prep = [&](long long t) __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int lane = fresh_lane();
+        const int vi = idxw[lane];
+        const int pv = idxw[lane > 0 ? lane - 1 : 0];
+        const bool start = lane == 0 || vi != pv;
+        msk = __ballot(start);
+        const int u = __popcll(msk);
+        if (start) tailw[__popcll(msk & (~0ull >> (63 - lane))) - 1] = vi;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        unsigned long long mm = msk;
+        const int un = u < CAPS ? u : CAPS;
+        const long long loff = (long long)(lane >> 3) * vrs + c0 + 4 * (lane & 7);
+        for (int s = 0; s < un; ++s) {
+            const int ls = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const int tail = __builtin_amdgcn_readlane(vi, ls);
+            __builtin_amdgcn_global_load_lds((gbl_vptr)(p.V + (long long)tail * D + loff), (lds_vptr)(vsl + s * SLOTB),
+                                             16, 0, 0);
+        }
+        nops += un;
+        const long long clast = (long long)p.M * R - 4;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            long long co = t * TR * R + 256 * k + 4 * lane;
+            if (co > clast) co = clast;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)(p.coef + co), (lds_vptr)(coefw + 256 * k), 16, 0, 0);
+        }
+        nops += 2;
+        if (t + 1 < t_end) dma_idx(t + 1);
+    };
+
+    f32x4 acc[4][2];
+    u32x2 outv[4][2];                                    // the finished tile, bf16 packed, until its stores
+    // epi(t): combine (slots and coefficients of the prepared tile), activation, into outv
+    auto epi = [&]() __attribute__((always_inline)) {
+        const int lane = fresh_lane();
+        const int i16 = lane & 15, g = lane >> 4;
+        const int u = __popcll(msk);
+        int slot[4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) slot[rb] = __popcll(msk & (~0ull >> (63 - i16 - 16 * rb))) - 1;
+        for (int b0 = 0; b0 < u; b0 += CAPS) {
+            const int s = b0 + g;
+            if (b0 > 0) {
+                // slots past the staged block (short runs / unsorted v_idx): this block's V rows into the slot
+                // buffers, synchronously (tail-sorted config-5 tiles rarely have more than 4 distinct rows)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const long long loff = (long long)(lane >> 3) * vrs + c0 + 4 * (lane & 7);
+                for (int k = 0; k < CAPS && b0 + k < u; ++k) {
+                    const int tail = __builtin_amdgcn_readfirstlane(tailw[b0 + k]);
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)(p.V + (long long)tail * D + loff),
+                                                     (lds_vptr)(vsl + k * SLOTB), 16, 0, 0);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            // A: V_r[slot s] at the lane's column, r = 0..7, for both column blocks (hi / lo)
+            bf16x8 vh[2], vl[2];
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                const float* vp = reinterpret_cast<const float*>(vsl + g * SLOTB) + 16 * cb + i16;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float x = s < u ? vp[32 * j] : 0.f;
+                    const __bf16 hi = (__bf16)x;
+                    vh[cb][j] = hi;
+                    vl[cb][j] = (__bf16)(x - (float)hi);
+                }
+            }
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb) {
+                // B: the coefficients of the lane's row where its slot is s (hi / lo)
+                const float* cp = coefw + (16 * rb + i16) * 8;
+                const f32x4 lo4 = ld4(cp), hi4 = ld4(cp + 4);
+                bf16x8 ch, cl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float x = slot[rb] == s ? (j < 4 ? lo4[j] : hi4[j - 4]) : 0.f;
+                    const __bf16 hi = (__bf16)x;
+                    ch[j] = hi;
+                    cl[j] = (__bf16)(x - (float)hi);
+                }
+#pragma unroll
+                for (int cb = 0; cb < 2; ++cb) {
+                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], ch, acc[rb][cb], 0, 0, 0);
+                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], cl, acc[rb][cb], 0, 0, 0);
+                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl[cb], ch, acc[rb][cb], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                f32x4 v = acc[rb][cb];
+                if (p.act == IDDGCN_ACT_SIGMOID) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
+                }
+                outv[rb][cb] = __builtin_bit_cast(u32x2, f32_to_bf4(v));
+            }
+    };
+    // the 8 stores of tile t
+    auto store = [&](long long t) __attribute__((always_inline)) {
+        const int lane = fresh_lane();
+        const int i16 = lane & 15, g = lane >> 4;
+        const long long row0 = t * TR;
+        const long long left = (long long)p.M - row0;
+        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 2);
+        const __amdgpu_buffer_rsrc_t rc =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(p.C) + row0 * D * 2, (short)0, nbytes, 0x00020000);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+                __builtin_amdgcn_raw_buffer_store_b64(outv[rb][cb], rc, ((16 * rb + i16) * D + c0 + 16 * cb + 4 * g) * 2,
+                                                      0, 0);
+        nops += 8;
+    };
+    auto mfma_main = [&](int b) __attribute__((always_inline)) {
+        const int lane = fresh_lane();
+        const int i16 = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* ab = lds + b * ABUF + i16 * PITCH + 16 * g;
+        // fragments of k-steps q and q+1 in alternating registers; one k-step per scheduling region (the fully
+        // unrolled loop otherwise hoists all the fragment loads and takes the kernel past 256 VGPRs)
+        bf16x8 x[2][4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) x[0][rb] = *reinterpret_cast<const bf16x8*>(ab + 16 * rb * PITCH);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int cu = q & 1;
+            if (q + 1 < 8) {
+#pragma unroll
+                for (int rb = 0; rb < 4; ++rb)
+                    x[cu ^ 1][rb] = *reinterpret_cast<const bf16x8*>(ab + 16 * rb * PITCH + 64 * (q + 1));
+            }
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                for (int rb = 0; rb < 4; ++rb) {
+                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[cb][q], x[cu][rb], acc[rb][cb], 0, 0, 0);
+                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[cb][q], x[cu][rb], acc[rb][cb], 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    // prologue: idx(t_beg), A(t_beg), A(t_beg + 1) landed, then prepare t_beg
+    dma_idx(t_beg);
+    dma_A(t_beg, 0);
+    if (t_beg + 1 < t_end) dma_A(t_beg + 1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    prep(t_beg);
+    int mark = nops;                                     // the next epilogue's inputs: every op up to mark
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    int b = 0;
+    // every wave: epilogue of t-1, prepare t, stores of t-1, MFMAs of t (a tile's V rows and coefficients are
+    // requested a whole MFMA phase before its epilogue; staggering half the waves, as the v3 kernel does, measured
+    // slower here: 20.6 vs 19.7 ms per config-5 launch)
+    for (long long t = t_beg; t < t_end; ++t) {
+        // A(t+2) into the buffer of tile t-1 (every wave's MFMAs on it ended before the last barrier)
+        if (t + 2 < t_end) dma_A(t + 2, b == 0 ? 2 : b - 1);
+        if (t > t_beg) {
+            wait_vm(nops - mark);            // prep(t-1) and A(t+1), with everything older
+            epi();
+            prep(t);
+            mark = nops;
+            store(t - 1);
+        } else {
+            mark = nops;                     // (t_beg: the next wait must also cover A(t_beg + 2))
+        }
+        mfma_main(b);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        b = b == 2 ? 0 : b + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    epi();
+    store(t_end - 1);
+}
+
+// config-5 forward form (R = 8, per-edge coefficients, gathered V rows, bf16 A / C): one persistent workgroup per CU
+void launch_fwd_gather8(hipStream_t st, RowGemmP p) {
+    const long long ntiles = ((long long)p.M + fg8::TR - 1) / fg8::TR;
+    long long nb = ntiles < 256 ? ntiles : 256;
+    p.tiles_per_block = (int)((ntiles + nb - 1) / nb);
+    nb = (ntiles + p.tiles_per_block - 1) / p.tiles_per_block;
+    hipLaunchKernelGGL(fwd_gather8_bf16_kernel, dim3((unsigned)nb), dim3(512), 0, st, p);
+}
+
 // the config-5 tail reduction on MFMAs (tail_seg_mfma8_kernel), with or without the head chain's node terms
 void launch_tail_mfma8(hipStream_t st, int n_nodes, const int* seg_ptr, const float* W, const void* dO,
                        const float* P, long long p_rel_stride, float* dP, long long dp_rel_stride, float* dsum,
@@ -4345,6 +4645,12 @@ int iddgcn_rowgemm_bf16(void* stream, const iddgcn_rowgemm_t* a) {
     if (a->planes) return IDDGCN_E_BAD_ARG;
     RowGemmP p = to_p(*a);
     p.accumulate = 0;
+    auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    if (a->R == 8 && a->v_idx && !a->coef_idx && !a->a_idx && !a->b_trans && !dsig && al16(a->A) && al16(a->C) &&
+        al16(a->coef) && al16(a->V) && (a->v_rel_stride & 3) == 0) {
+        launch_fwd_gather8((hipStream_t)stream, p);
+        return launch_status();
+    }
     V3Sel sel;
     sel.nv = a->R == 0 ? 0 : a->R == 1 ? 1 : a->R == 2 ? 2 : a->R <= 4 ? 4 : 8;
     sel.aux = dsig;

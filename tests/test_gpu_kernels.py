@@ -860,6 +860,30 @@ def test_rowgemm256_batched_one_launch_bitwise(gm, cuda):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("gm", ["exact", "split"])
+def test_rowgemm256_batched_full_projection_set(gm, cuda):
+    """A full batch of L.ROWGEMM_BATCH = 16 entries laid out like the forward projections (entry l*R + r reads A_r,
+    R = 5, three layers, plus one extra entry): one launch, bitwise equal to one call per entry; one entry more
+    is refused."""
+    g = torch.Generator().manual_seed(9)
+    D, R, M = 256, 5, 20_011
+    A = [torch.randn(M, D, generator=g).to(cuda) for _ in range(R)] + [torch.randn(M, D, generator=g).to(cuda)]
+    calls = [(A[r], (torch.randn(D, D, generator=g) / 16).to(cuda)) for _ in range(3) for r in range(R)]
+    calls.append((A[R], (torch.randn(D, D, generator=g) / 16).to(cuda)))
+    assert len(calls) == L.ROWGEMM_BATCH
+    single = []
+    for a, b in calls:
+        C = torch.empty(M, D, device=cuda)
+        ops.rowgemm(a, b, C, precision=gm)
+        single.append(C)
+    outs = [torch.full((M, D), float("nan"), device=cuda) for _ in calls]
+    ops.rowgemm_batched([(a, b, C, dict(precision=gm)) for (a, b), C in zip(calls, outs)])
+    for x, y in zip(single, outs):
+        assert torch.equal(x, y)
+    with pytest.raises(L.IddgcnError):
+        ops.rowgemm_batched([(a, b, C, dict(precision=gm)) for (a, b), C in zip(calls + calls[:1], outs + outs[:1])])
+
+
 @pytest.mark.parametrize("R", [1, 2, 4, 8])
 @pytest.mark.parametrize("case", ["uniform", "hub", "sparse", "empty", "tiny"])
 @pytest.mark.parametrize("dsum", [False, True])
