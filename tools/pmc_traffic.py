@@ -34,7 +34,7 @@ SYMBOLS = {
               "tail_dS_tn": "gemm_tn256_dma_kernel"},
     # the bf16-feature mode (config 5: R = 8 gathered relations, bf16 edge tables); recorded under the
     # bench's gemm key with `python tools/pmc_traffic.py ... exact synthetic-5 1 profiles/r03 bf16`
-    "bf16": {"tail_fwd_gemm": "rowgemm256_v3_kernel<8, false, true, true, false, true, false, false>",
+    "bf16": {"tail_fwd_gemm": "fwd_gather8_bf16_kernel",
              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, true, false, false>",
              "tail_dS_tn": "gemm_tn256_bf16t_kernel"},
 }
