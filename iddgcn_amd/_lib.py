@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
 ABI_VERSION = 9
-ROWGEMM_BATCH = 16          # IDDGCN_ROWGEMM_BATCH: entries per iddgcn_rowgemm_batched_f32 call
+ROWGEMM_BATCH = 25          # IDDGCN_ROWGEMM_BATCH: entries per iddgcn_rowgemm_batched_f32 call
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
 GEMM_EXACT_F32, GEMM_SPLIT_F16, GEMM_F32_4CHAIN, GEMM_BF16X3 = 0, 1, 2, 3

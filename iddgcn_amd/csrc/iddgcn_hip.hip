@@ -285,10 +285,11 @@ struct RowGemmP {
 };
 
 // up to ROWGEMM_BATCH independent row GEMMs of one width in one launch (blockIdx.y = entry): the
-// node-level projections of a step are many tiny launches at the reference's 845 nodes.  (25 entries, config 5's
-// whole projection set in one launch, computed entries 16-24 as zeros at N = 1M although a 20k-row 25-entry test
-// passed: 16 kept, cause not found)
-constexpr int ROWGEMM_BATCH = 16;
+// node-level projections of a step are many tiny launches at the reference's 845 nodes.  25 = 3R + 1 at R = 8:
+// config 5's whole forward projection set (three layers per AE_r, plus E S^1) in one launch, so the three
+// entries reading the same AE_r run concurrently (entries r, r + R, r + 2R land on one XCD when R * per is a
+// multiple of 8) and AE_r comes from HBM once instead of twice (25 x 136 B of kernel arguments)
+constexpr int ROWGEMM_BATCH = 25;
 struct RowGemmBatch {
     RowGemmP p[ROWGEMM_BATCH];
 };

@@ -375,8 +375,9 @@ class Engine:
                              ws.AE[r][n0:n1].view(1, n1 - n0, D), 1, n1 - n0)
                 proj += [(ws.AE[r][n0:n1], P[f"K{l + 1}"][r], ws.P[l, r][n0:n1], pn) for l in range(NUM_LAYERS)]
         proj.append((E, P["S1"], ws.ES1, pn))
-        for i in range(0, len(proj), L.ROWGEMM_BATCH):
-            ops.rowgemm_batched(proj[i:i + 16])
+        nb = L.ROWGEMM_BATCH
+        for i in range(0, len(proj), nb):
+            ops.rowgemm_batched(proj[i:i + nb])
         if sh is not None:
             for l in range(NUM_LAYERS):
                 sh.all_gather(ws.P[l].view(R * N, D))
@@ -546,8 +547,9 @@ class Engine:
             proj = [(ws.AE[r][a:b], P[f"K{l + 1}"][r], ws.P[l, r][a:b], pn) for l in range(NUM_LAYERS)
                     for r in range(R)]
             proj.append((E[a:b], P["S1"], ws.ES1[a:b], pn))
-            for i in range(0, len(proj), L.ROWGEMM_BATCH):
-                ops.rowgemm_batched(proj[i:i + 16])
+            nb = L.ROWGEMM_BATCH
+            for i in range(0, len(proj), nb):
+                ops.rowgemm_batched(proj[i:i + nb])
             ops.alpha_fwd(E[a:b], P["Wa1"], P["ba1"], ws.Ssm[0][a:b], ws.W[0][a:b])
         sh.all_gather(ws.W[0])
         # node level first (layers 1-3 over the owned rows, W^l all-gathered as each layer's alpha is known), so

@@ -116,7 +116,7 @@ def rowgemm_kernel_id(A, B, C, **kw):
 
 def rowgemm_batched(calls):
     """Independent row GEMMs of one width in one launch (iddgcn_rowgemm_batched_f32).  calls: list of
-    (A, B, C, kwargs) as for rowgemm; at most L.ROWGEMM_BATCH (16)."""
+    (A, B, C, kwargs) as for rowgemm; at most L.ROWGEMM_BATCH (25)."""
     if not calls:
         return
     arr = (L.RowGemmArgs * len(calls))(*[_rowgemm_args(A, B, C, **kw) for A, B, C, kw in calls])

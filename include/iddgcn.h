@@ -271,10 +271,10 @@ int iddgcn_gather_rows_f32(void* stream, long long M, int width, const float* sr
 int iddgcn_reduce_slabs_f32(void* stream, int n_slabs, long long n, const float* slab,
                             float* out, int accumulate, float scale);
 
-/* Up to 16 (IDDGCN_ROWGEMM_BATCH) independent iddgcn_rowgemm_f32 calls of one width D (e.g. the per-relation, per-layer
+/* Up to 25 (IDDGCN_ROWGEMM_BATCH) independent iddgcn_rowgemm_f32 calls of one width D (e.g. the per-relation, per-layer
  * node projections A_r·E·K_r of IDDGCN.py:71-77) in ONE launch (blockIdx.y = entry); at D = 256 when
  * every entry maps to the same v3 variant (iddgcn_rowgemm_kernel_id), else one launch per entry. */
-#define IDDGCN_ROWGEMM_BATCH 16
+#define IDDGCN_ROWGEMM_BATCH 25
 int iddgcn_rowgemm_batched_f32(void* stream, const iddgcn_rowgemm_t* args, int n);
 
 /* Keras-2.7 Adam, one tensor (IDDGCN.py:174,392).  sparse_form=0: TF ApplyAdam

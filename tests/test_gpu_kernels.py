@@ -862,11 +862,12 @@ def test_rowgemm256_batched_one_launch_bitwise(gm, cuda):
 
 @pytest.mark.parametrize("gm", ["exact", "split"])
 def test_rowgemm256_batched_full_projection_set(gm, cuda):
-    """A full batch of L.ROWGEMM_BATCH = 16 entries laid out like the forward projections (entry l*R + r reads A_r,
-    R = 5, three layers, plus one extra entry): one launch, bitwise equal to one call per entry; one entry more
-    is refused."""
+    """A full batch of L.ROWGEMM_BATCH = 25 entries laid out like config 5's forward projections (entry l*R + r
+    reads A_r, R = 8, three layers, plus one extra entry): one launch, bitwise equal to one call per entry; one
+    entry more is refused.  (The engine-level check is tests/test_gpu_config5.py: its layer-3 tables come from
+    entries 16-23.)"""
     g = torch.Generator().manual_seed(9)
-    D, R, M = 256, 5, 20_011
+    D, R, M = 256, 8, 20_011
     A = [torch.randn(M, D, generator=g).to(cuda) for _ in range(R)] + [torch.randn(M, D, generator=g).to(cuda)]
     calls = [(A[r], (torch.randn(D, D, generator=g) / 16).to(cuda)) for _ in range(3) for r in range(R)]
     calls.append((A[R], (torch.randn(D, D, generator=g) / 16).to(cuda)))
@@ -995,3 +996,31 @@ def test_rowgemm_f32_4chain_accumulation(D, cuda):
         with pytest.raises(L.IddgcnError):
             ops.rowgemm(A.float(), B.float(), torch.empty(M, D, device=cuda), precision="exact4", act=L.ACT_DSIGMOID,
                         aux=torch.rand(M, D, device=cuda))
+
+
+@pytest.mark.parametrize("R", [2, 5, 8])
+def test_engine_projection_batches_cover_every_entry(R, cuda, monkeypatch):
+    """The engine's forward hands every node-level projection (3R + 1 of them) to rowgemm_batched in chunks of at
+    most L.ROWGEMM_BATCH, each exactly once (a chunk sliced shorter than its stride once left config 5's layer-3
+    tables uncomputed)."""
+    from iddgcn_amd.engine import Engine, FlatParams
+    from iddgcn_amd.graph import get_adj_mats
+    from iddgcn_amd.utils import synthetic_graph
+    N, D = 300, 256
+    pos, neg = synthetic_graph(N, R, 3000, seed=R)
+    eng = Engine(N, R, D, cuda, features="bf16" if R == 8 else "f32")
+    P = FlatParams(N, R, D, cuda)
+    rng = np.random.default_rng(R)
+    P.load({name: rng.standard_normal(shape).astype(np.float32) * 0.05 for name, shape, _ in P.layout})
+    seen = []
+    orig = ops.rowgemm_batched
+
+    def spy(calls):
+        assert len(calls) <= L.ROWGEMM_BATCH
+        seen.extend(C.data_ptr() for _, _, C, _ in calls)
+        return orig(calls)
+
+    monkeypatch.setattr(ops, "rowgemm_batched", spy)
+    eng.predict(P, eng.adjacency(get_adj_mats(pos, N, R)), eng.edges(np.concatenate([pos, neg]),
+                                                                     np.zeros(len(pos) + len(neg))))
+    assert len(seen) == 3 * R + 1 and len(set(seen)) == 3 * R + 1
