@@ -83,6 +83,27 @@ def test_fwd_gather8_bf16(case, cuda):
     assert C[M:].isnan().all()                 # nothing past row M is written
 
 
+def test_fwd_gather8_bf16_offsets_past_2e32(cuda):
+    """fwd_gather8_bf16_kernel addresses relation r's node row as r·v_rel_stride + row·D in 64 bits: with N = 2.5M
+    ((R-1)·N·D = 4.5e9 elements > 2^32) rows gathered from the top of the table, the same bar as above."""
+    g = torch.Generator(device=cuda).manual_seed(31)
+    R, N, M = 8, 2_500_000, 4096
+    assert (R - 1) * N * D > 2 ** 32
+    P = torch.randn(R, N, D, device=cuda, generator=g)
+    t = (N - 1 - torch.sort(torch.randint(0, 600, (M,), device=cuda, generator=g), descending=True)[0]).int()
+    A = bf(torch.rand(M, D, device=cuda, generator=g))
+    S = torch.randn(D, D, device=cuda, generator=g) / 16
+    W = torch.rand(M, R, device=cuda, generator=g)
+    ref = torch.sigmoid(A.double() @ S.double() + sum(W[:, r:r + 1].double() * P[r][t.long()].double()
+                                                      for r in range(R)))
+    C = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
+    ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)
+    del P
+    torch.cuda.empty_cache()
+    err = (C.double() - ref).abs()
+    assert (err <= 2 ** -8 * ref.abs() + 1e-5 * ref.abs().max()).all(), err.max().item()
+
+
 def test_rowgemm_bf16_backward_dsigmoid(cuda):
     g = torch.Generator().manual_seed(7)
     M = 30_001
