@@ -98,9 +98,41 @@ class KerasAdam:
     def apply(self, params, grads):
         self.iterations += 1
         alpha = self.alpha_at(self.iterations)
+        self._apply_range(params, grads, 0, params.flat.numel(), alpha)
+
+    def _apply_range(self, params, grads, lo, hi, alpha):
+        """The update of flat elements [lo, hi) (sparse form below params.n_sparse, dense above); the update is
+        elementwise, so any partition of the buffer gives bitwise the whole-buffer result."""
         ns = params.n_sparse
-        ops.adam(params.flat[:ns], self.m[:ns], self.v[:ns], grads.flat[:ns], alpha, self.b1, self.b2, self.eps, 1)
-        ops.adam(params.flat[ns:], self.m[ns:], self.v[ns:], grads.flat[ns:], alpha, self.b1, self.b2, self.eps, 0)
+        for a, b, sparse in ((lo, min(hi, ns), 1), (max(lo, ns), hi, 0)):
+            if a < b:
+                ops.adam(params.flat[a:b], self.m[a:b], self.v[a:b], grads.flat[a:b], alpha, self.b1, self.b2,
+                         self.eps, sparse)
+
+    def apply_overlapped(self, params, grads, comm):
+        """apply() after a data-parallel backward, bucket by bucket: each all-reduced bucket of ``grads.buf``
+        (parallel.BucketedAllReduce.finish_each, in hand-over order) gets its parameters' update as soon as its
+        sum has landed, so the update of the small weights and of dE's first row chunks runs while the later
+        chunks are still on the wire; the elements no bucket covered are updated after the last."""
+        self.iterations += 1
+        alpha = self.alpha_at(self.iterations)
+        n, base = params.flat.numel(), grads.buf.data_ptr()
+        done = []
+
+        def on_bucket(view):
+            off = (view.data_ptr() - base) // view.element_size()
+            if view.dtype != grads.buf.dtype or not 0 <= off < n:
+                return
+            hi = min(off + view.numel(), n)
+            self._apply_range(params, grads, off, hi, alpha)
+            done.append((off, hi))
+
+        comm.finish_each(on_bucket)
+        pos = 0
+        for a, b in sorted(done) + [(n, n)]:
+            if a > pos:
+                self._apply_range(params, grads, pos, a, alpha)
+            pos = max(pos, b)
 
 
     def apply_table(self, params, grads, alpha_table, step):
@@ -660,9 +692,12 @@ class Engine:
         self._t_global = t_global
         self.forward(params, adj, ed, ws, True)
         self.backward(params, grads, adj, ed, ws, comm)
-        if comm is not None:
-            comm.finish()
-        opt.apply(params, grads)
+        if comm is not None and hasattr(comm, "finish_each") and hasattr(opt, "apply_overlapped"):
+            opt.apply_overlapped(params, grads, comm)
+        else:
+            if comm is not None:
+                comm.finish()
+            opt.apply(params, grads)
         return grads.loss
 
     def predict(self, params, adj, ed, logits=False):

@@ -68,13 +68,23 @@ class BucketedAllReduce:
             host = view.cpu()
             dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
             view.copy_(host)
+            self._works.append((None, view))
             return
-        self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        self._works.append((dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True), view))
 
     def finish(self):
+        self.finish_each(None)
+
+    def finish_each(self, fn):
+        """Wait for the buckets in the order they were handed over; after each, ``fn(view)`` (if given) with the
+        bucket now summed — work queued there on the current stream overlaps the later buckets' all-reduces
+        (the engine's Adam over each bucket's parameter range)."""
         works, self._works = self._works, []
-        for w in works:
-            w.wait()
+        for w, view in works:
+            if w is not None:
+                w.wait()
+            if fn is not None:
+                fn(view)
 
     def __call__(self, buf):
         """Whole-buffer form (one bucket)."""

@@ -211,3 +211,47 @@ def test_node_shard_collectives_gloo(world, staged):
         other = np.ones(N, bool)
         other[a:b] = False
         assert np.array_equal(part[other], (rank + 1) * np.arange(N, dtype=np.float32)[other, None].repeat(3, 1))
+
+
+def _finish_each_worker(rank, world, port, q, host_staged):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        buf = torch.arange(40, dtype=torch.float32) * (rank + 1)
+        comm = BucketedAllReduce(host_staged=host_staged)
+        pieces = [(30, 40), (0, 10), (10, 20), (20, 30)]      # hand-over order: small part first, then row chunks
+        for a, b in pieces:
+            comm.ready(buf[a:b])
+        seen = []
+
+        def fn(view):
+            off = (view.data_ptr() - buf.data_ptr()) // 4
+            seen.append((off, off + view.numel(), view.clone().numpy()))
+
+        comm.finish_each(fn)
+        q.put((rank, seen, buf.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("host_staged", [None, False])
+def test_bucketed_finish_each_in_order_after_each_sum(host_staged):
+    """BucketedAllReduce.finish_each (the hook the overlapped Adam update rides on): the callback sees every bucket
+    once, in hand-over order, each already summed over the ranks (gloo world 2 on CPU tensors; host_staged=False:
+    the asynchronous in-place branch the RCCL ranks take)."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_finish_each_worker, args=(r, 2, port, q, host_staged)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = np.arange(40, dtype=np.float32) * 3
+    for _, seen, buf in res:
+        assert [(a, b) for a, b, _ in seen] == [(30, 40), (0, 10), (10, 20), (20, 30)]
+        for a, b, v in seen:
+            assert np.array_equal(v, want[a:b])
+        assert np.array_equal(buf, want)

@@ -270,3 +270,70 @@ def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, mode, feature
     assert abs(l - full_loss) <= bl * full_loss
     for k, v in full.items():
         assert np.abs(g[k] - v).max() <= bg * np.abs(v).max() + 1e-30, k
+
+
+def _adam_worker(rank, world, port, q, mode):
+    """One data-parallel training step through Engine.train_step (Adam applied bucket by bucket as the all-reduced
+    buckets land: KerasAdam.apply_overlapped) and the same step with the whole all-reduce waited for first and one
+    KerasAdam.apply: parameters and moments bitwise equal."""
+    import torch.distributed as dist
+    from iddgcn_amd.engine import KerasAdam
+    from iddgcn_amd.parallel import BucketedAllReduce, NodeShard, node_ranges, node_shard_triples
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        N, R, D = 700, 2, 256
+        pos, neg = synthetic_graph(N, R, 9000, seed=77)
+        tri = np.concatenate([pos, neg])
+        lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+        eng = Engine(N, R, D, dev, gemm="bf16x3")
+        if mode == "node_device":
+            cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
+            eng.row_shard = NodeShard(cuts, staged=False)
+            mine, mlab = node_shard_triples(tri, lab, cuts, rank)
+        else:
+            lo, hi = shard_range(len(tri), rank, world)
+            mine, mlab = tri[lo:hi], lab[lo:hi]
+        adj = eng.adjacency(get_adj_mats(pos, N, R))
+        ed = eng.edges(mine, mlab)
+        out = []
+        for overlapped in (True, False):
+            P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
+            P.load(_mild(N, R, D, 9))
+            opt = KerasAdam(P)
+            comm = BucketedAllReduce(min_bucket_rows=64, host_staged=False)
+            if overlapped:
+                eng.train_step(P, G, opt, adj, ed, t_global=len(tri), comm=comm)
+            else:
+                ws = eng.workspace(ed.T, True)
+                eng._t_global = len(tri)
+                eng.forward(P, adj, ed, ws, True)
+                eng.backward(P, G, adj, ed, ws, comm)
+                comm.finish()
+                opt.apply(P, G)
+            torch.cuda.synchronize()
+            out.append((P.buf.cpu().numpy(), opt.m.cpu().numpy(), opt.v.cpu().numpy()))
+        q.put((rank, all(np.array_equal(a, b) for a, b in zip(out[0], out[1])), out[0][0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["edge_device", "node_device"])
+def test_overlapped_adam_equals_adam_after_allreduce(mode, cuda):
+    """Engine.train_step with a BucketedAllReduce updates each bucket's parameters as soon as that bucket's sum
+    lands (the small weights, then dE's row chunks) — bitwise the step that waits for the whole all-reduce and
+    then runs one Adam update; the ranks' parameters bitwise equal.  2 ranks on one GPU over gloo, device branch."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_adam_worker, args=(r, 2, port, q, mode)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0][1] and out[1][1]
+    assert np.array_equal(out[0][2], out[1][2])
