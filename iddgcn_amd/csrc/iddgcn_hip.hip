@@ -3758,9 +3758,11 @@ inline unsigned grid_for(long long rows, int lpr) {
 //            below the bf16 rounding of the stored output.
 // The v3 epilogue this replaces read 8 KiB of fp32 V slab per edge row from LDS and ran 2048 FMAs per row on the
 // VALU; here the combine is 24 MFMAs per 64 x 32 wave tile plus 16 LDS reads and 48 two-piece splits per lane.
-// Schedule (every wave alike): A(t+2) DMA; wait for tile t-1's slots and A(t+1); epilogue of t-1; prepare t (slots,
-// coefficients, the next v_idx: wave-private, producer = consumer, the wave's own vmcnt); stores of t-1; MFMAs of t;
-// one barrier per tile (A buffers, three deep).  Measured per config-5 launch (tools/fg8_probe.py, one box): v3
+// Schedule (every wave alike): A(t+2) DMA; wait for tile t-1's slots and A(t+1); combine of t-1 (into a second
+// accumulator set); prepare t (slots, coefficients, the next v_idx: wave-private, producer = consumer, the wave's own
+// vmcnt); MFMAs of t with t-1's activation, conversion and stores issued one 16 x 16 block per k-step between them
+// (18.5-18.6 vs 18.7-18.8 ms, bitwise the same; profiles/r04/fg8/probe_overlap_ab.log); one barrier per tile
+// (A buffers, three deep).  Measured per config-5 launch (tools/fg8_probe.py, one box): v3
 // kernel 24.7 ms; this design at 32-row tiles 20.6 ms with the v3 stagger (waves 4-7 one epilogue behind), 19.7 ms
 // all waves alike; 64-row tiles 18.1 ms; the stagger at 64 rows 20.3 ms (profiles/r04/fg8/).
 namespace fg8 {
@@ -3874,10 +3876,10 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
         if (t + 1 < t_end) dma_idx(t + 1);
     };
 
-    f32x4 acc[4][2];
-    u32x2 outv[4][2];                                    // the finished tile, bf16 packed, until its stores
-    // epi(t): combine (slots and coefficients of the prepared tile), activation, into outv
-    auto epi = [&]() __attribute__((always_inline)) {
+    f32x4 acc[4][2];                                     // the tile in the x S MFMAs
+    f32x4 accP[4][2];                                    // the previous tile: combine, activation, stores
+    // combine(): the prepared tile's V term (slots and coefficients in the wave's LDS) into accP
+    auto combine = [&]() __attribute__((always_inline)) {
         const int lane = fresh_lane();
         const int i16 = lane & 15, g = lane >> 4;
         const int u = __popcll(msk);
@@ -3926,42 +3928,33 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
                 }
 #pragma unroll
                 for (int cb = 0; cb < 2; ++cb) {
-                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], ch, acc[rb][cb], 0, 0, 0);
-                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], cl, acc[rb][cb], 0, 0, 0);
-                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl[cb], ch, acc[rb][cb], 0, 0, 0);
+                    accP[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], ch, accP[rb][cb], 0, 0, 0);
+                    accP[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], cl, accP[rb][cb], 0, 0, 0);
+                    accP[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl[cb], ch, accP[rb][cb], 0, 0, 0);
                 }
             }
         }
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int cb = 0; cb < 2; ++cb) {
-                f32x4 v = acc[rb][cb];
-                if (p.act == IDDGCN_ACT_SIGMOID) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = sigmoid_fast(v[q]);
-                }
-                outv[rb][cb] = __builtin_bit_cast(u32x2, f32_to_bf4(v));
-            }
     };
-    // the 8 stores of tile t
-    auto store = [&](long long t) __attribute__((always_inline)) {
+    // finish(t, q): block q = (rb, cb) of the previous tile t: activation, bf16, one 8-B store per lane
+    auto finish = [&](long long t, int q) __attribute__((always_inline)) {
         const int lane = fresh_lane();
         const int i16 = lane & 15, g = lane >> 4;
+        const int rb = q >> 1, cb = q & 1;
         const long long row0 = t * TR;
         const long long left = (long long)p.M - row0;
         const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 2);
         const __amdgpu_buffer_rsrc_t rc =
             __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(p.C) + row0 * D * 2, (short)0, nbytes, 0x00020000);
+        f32x4 v = accP[rb][cb];
+        if (p.act == IDDGCN_ACT_SIGMOID) {
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-            for (int cb = 0; cb < 2; ++cb)
-                __builtin_amdgcn_raw_buffer_store_b64(outv[rb][cb], rc, ((16 * rb + i16) * D + c0 + 16 * cb + 4 * g) * 2,
-                                                      0, 0);
-        nops += 8;
+            for (int e = 0; e < 4; ++e) v[e] = sigmoid_fast(v[e]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, f32_to_bf4(v)), rc,
+                                              ((16 * rb + i16) * D + c0 + 16 * cb + 4 * g) * 2, 0, 0);
+        nops += 1;
     };
-    auto mfma_main = [&](int b) __attribute__((always_inline)) {
+    auto mfma_main = [&](int b, long long tprev) __attribute__((always_inline)) {
         const int lane = fresh_lane();
         const int i16 = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -3989,6 +3982,8 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
                     acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[cb][q], x[cu][rb], acc[rb][cb], 0, 0, 0);
                     acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[cb][q], x[cu][rb], acc[rb][cb], 0, 0, 0);
                 }
+            // the previous tile's block q: its VALU and store issue in the shadow of this k-step's MFMAs
+            if (tprev >= 0) finish(tprev, q);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -4003,30 +3998,34 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     int b = 0;
-    // every wave: epilogue of t-1, prepare t, stores of t-1, MFMAs of t (a tile's V rows and coefficients are
-    // requested a whole MFMA phase before its epilogue; staggering half the waves, as the v3 kernel does, measured
-    // slower here: 20.6 vs 19.7 ms per config-5 launch)
+    // every wave: combine of t-1, prepare t, MFMAs of t with t-1's activation and stores interleaved (a tile's V rows
+    // and coefficients are requested a whole MFMA phase before its combine; staggering half the waves, as the v3
+    // kernel does, measured slower here: 20.6 vs 19.7 ms per config-5 launch at 32-row tiles, 20.3 vs 18.1 at 64)
     for (long long t = t_beg; t < t_end; ++t) {
         // A(t+2) into the buffer of tile t-1 (every wave's MFMAs on it ended before the last barrier)
         if (t + 2 < t_end) dma_A(t + 2, b == 0 ? 2 : b - 1);
         if (t > t_beg) {
             wait_vm(nops - mark);            // prep(t-1) and A(t+1), with everything older
-            epi();
+            combine();
             prep(t);
             mark = nops;
-            store(t - 1);
         } else {
             mark = nops;                     // (t_beg: the next wait must also cover A(t_beg + 2))
         }
-        mfma_main(b);
+        mfma_main(b, t > t_beg ? t - 1 : -1);
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) accP[rb][cb] = acc[rb][cb];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         b = b == 2 ? 0 : b + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    epi();
-    store(t_end - 1);
+    combine();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) finish(t_end - 1, q);
 }
 
 // config-5 forward form (R = 8, per-edge coefficients, gathered V rows, bf16 A / C): one persistent workgroup per CU
