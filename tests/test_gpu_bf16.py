@@ -83,6 +83,30 @@ def test_fwd_gather8_bf16(case, cuda):
     assert C[M:].isnan().all()                 # nothing past row M is written
 
 
+def test_fwd_gather8_unaligned_coef_takes_v3_path(cuda):
+    """iddgcn_rowgemm_bf16 sends the R = 8 forward to fwd_gather8_bf16_kernel only with 16-B aligned A, C, coef and V
+    (its DMAs move 16-B pieces); a coefficient table 4 B off alignment takes the v3 kernel: same bar against fp64,
+    and within one bf16 ulp of the MFMA-combine result."""
+    g = torch.Generator().manual_seed(12)
+    N, M, R = 3000, 20_011, 8
+    A = bf(torch.rand(M, D, generator=g)).to(cuda)
+    S = (torch.randn(D, D, generator=g) / 16).to(cuda)
+    W = torch.rand(M, R, generator=g).to(cuda)
+    Wu = torch.empty(M * R + 1, device=cuda)[1:].view(M, R)
+    Wu.copy_(W)
+    P = torch.randn(R, N, D, generator=g).to(cuda)
+    t = tails(M, N, g).to(cuda).int()
+    ref = torch.sigmoid(A.double() @ S.double() + sum(W.double()[:, r:r + 1] * P.double()[r][t.long()] for r in range(R)))
+    outs = []
+    for coef in (W, Wu):
+        C = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
+        ops.rowgemm(A, S, C, coef=coef, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID)
+        err = (C.double() - ref).abs()
+        assert (err <= 2 ** -8 * ref.abs() + 1e-5 * ref.abs().max()).all(), err.max().item()
+        outs.append(C.double())
+    assert (outs[0] - outs[1]).abs().max().item() <= 2 ** -8
+
+
 def test_fwd_gather8_bf16_offsets_past_2e32(cuda):
     """fwd_gather8_bf16_kernel addresses relation r's node row as r·v_rel_stride + row·D in 64 bits: with N = 2.5M
     ((R-1)·N·D = 4.5e9 elements > 2^32) rows gathered from the top of the table, the same bar as above."""
