@@ -205,6 +205,26 @@ def cpu_model():
     return "unknown"
 
 
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 (cpu.max) or v1 (cfs quota / period) CPU controller, rounded up; None if
+    unlimited or unreadable."""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else max(1, math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return None if q <= 0 else max(1, math.ceil(q / p))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(cfg, frac=0.05, min_steps=3, budget_s=60.0):
     """The reference formulation on the host cores (one full step: pos + neg forward, autograd backward,
     Keras Adam), on a bounded sample of the same workload: the same N, D, R and a `frac` share of its
@@ -219,6 +239,14 @@ def cpu_baseline(cfg, frac=0.05, min_steps=3, budget_s=60.0):
     from oracle.ref_utils import get_adj_coo
     from iddgcn_amd.utils import synthetic_graph
     N, R, D = cfg["N"], cfg["R"], cfg["D"]
+    # every core this process may run on (torch.set_num_threads(os.cpu_count())), bounded by what the
+    # lease grants: the affinity mask and the cgroup CPU quota (the GPU box shows the whole host's CPUs in both
+    # os.cpu_count() and the mask, and grants a 16-CPU share), all counts on the record
+    affinity = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    usable = min(affinity, quota) if quota else affinity
+    threads_before = torch.get_num_threads()
+    torch.set_num_threads(usable)
     threads = torch.get_num_threads()
 
     def make(M_s):
@@ -247,14 +275,18 @@ def cpu_baseline(cfg, frac=0.05, min_steps=3, budget_s=60.0):
         if len(times) >= min_steps and (len(times) >= 5 or sum(times) + times[-1] > budget_s):
             break
     t = statistics.median(times)
+    torch.set_num_threads(threads_before)
     return {"value": M_s / t, "unit": "adjacency edges/s", "cores": threads, "kind": "port",
-            "host_cpu_count": os.cpu_count(), "cpu_model": cpu_model(),
+            "host_cpu_count": os.cpu_count(), "cpus_in_affinity_mask": affinity,
+            "cgroup_cpu_quota": quota,
+            "torch_threads_default": threads_before, "cpu_model": cpu_model(),
             "fraction_of_workload": M_s / cfg["M"], "step_s": times,
             "scored_edges_per_s": 2 * M_s / t,
             "sample": (f"oracle/ref_model.py reference formulation (torch-CPU fp32: per-edge GEMMs, A_r.E per layer, "
                        f"Keras BCE, autograd backward, Keras Adam), N={N} D={D} R={R}, {M_s} of the workload's "
                        f"{cfg['M']} adjacency edges ({100 * M_s / cfg['M']:.0f}%) + {M_s} negatives; median of "
-                       f"{len(times)} steps after a warm-up step, {t:.2f} s/step, {threads} torch threads on a "
+                       f"{len(times)} steps after a warm-up step, {t:.2f} s/step, {threads} torch threads "
+                       f"(torch.set_num_threads: {affinity} CPUs in the affinity mask, cgroup quota {quota} CPUs) on a "
                        f"{os.cpu_count()}-CPU host ({cpu_model()})")}
 
 
@@ -280,6 +312,21 @@ def step_roofline(N, R, D, T, M, gemm, features, ms_per_step):
                                  "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS},
             "mode": {"gemm": gemm, "features": features, "mfma_products_per_flop": hw, "peak_TFLOPs": peak,
                      "t_mfma_ms": t_mode, "t_roof_ms": t_mode + t_hbm, "frac": (t_mode + t_hbm) / ms_per_step}}
+
+
+def rank_consistency(buf):
+    """After the timed steps: the largest |params - rank 0's params| over all ranks (0.0 when every rank holds
+    bitwise the same parameters, as the replicated Adam on all-reduced gradients must).  ``buf``: the rank's flat
+    parameter buffer (FlatParams.buf) on its GPU."""
+    import torch.distributed as dist
+    ref = buf.clone()
+    dist.broadcast(ref, 0)
+    d = (buf - ref).abs().max().reshape(1)
+    if dist.get_backend() != "nccl":
+        d = d.cpu()
+    dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    del ref
+    return float(d.item())
 
 
 def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=True, shard=None, steps=None,
@@ -367,20 +414,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         probe_out, eng.probe = eng.probe, None
         return elapsed, float(loss.item()) / T, probe_out
 
-    def rank_consistency():
-        """After the timed steps: the largest |params - rank 0's params| over all ranks (0.0 when every rank
-        holds bitwise the same parameters, as the replicated Adam on all-reduced gradients must)."""
-        ref = P.buf.clone()
-        dist.broadcast(ref, 0)
-        d = (P.buf - ref).abs().max().reshape(1)
-        if dist.get_backend() != "nccl":
-            d = d.cpu()
-        dist.all_reduce(d, op=dist.ReduceOp.MAX)
-        del ref
-        return float(d.item())
-
     elapsed, loss_val, probe = timed_run(gemm, probe_kernels)
-    consist = rank_consistency() if world > 1 else None
+    consist = rank_consistency(P.buf) if world > 1 else None
     out = {"value": M / (elapsed / steps), "ms_per_step": elapsed / steps * 1e3,
            "scaling": cfg["scaling"], "dtype": DTYPE_BF16 if feat == "bf16" else DTYPE[gemm],
            "gemm_operands": GEMM_NOTE[gemm] + ("; edge GEMMs bf16 (features=bf16)" if feat == "bf16" else ""),

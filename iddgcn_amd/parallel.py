@@ -1,6 +1,8 @@
 """Data parallelism for the full-batch step (one process per GPU, RCCL over xGMI).
 
-Edge partitioning (the default): the scored edges of a full-batch step are
+Two partitions of the step.  Node-row partitioning (NodeShard below, bench.py's default with more
+than one GPU) splits the node rows and takes the scored edges by tail.  Edge partitioning (``--shard edge``; the
+default of IDDGCN_Model.fit's multi-rank branch): the scored edges of a full-batch step are
 independent given the node tables, so each rank takes a contiguous slice of them; the graph (CSR
 of every A_r) and all parameters are replicated.  Every gradient of the step is a sum over scored
 edges, so the per-rank gradients — already normalised by the GLOBAL edge count — are summed by an

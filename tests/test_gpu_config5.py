@@ -74,9 +74,13 @@ def test_config5_device_negatives_bit_exact(cfg5):
     assert np.array_equal(neg[:, 0], rh) and np.array_equal(neg[:, 1], rr) and np.array_equal(neg[:, 2], rt)
 
 
-def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, cuda):
+@pytest.mark.parametrize("gemm", ["exact", "split"])
+def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, gemm, cuda):
+    """``gemm``: the node-level GEMMs' operand precision; "split" (split-fp16 node projections) is the mode
+    bench.py times for config 5 (CONFIGS[5]["gemm"])."""
     params = mild_params()
     eng, ed, sample = cfg5["eng"], cfg5["ed"], cfg5["sample"]
+    eng.gemm = gemm
     P = FlatParams(N, R, D, cuda)
     P.load(params)
     p, s = eng.predict(P, cfg5["adj"], ed, logits=True)
@@ -92,6 +96,7 @@ def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, cuda):
     assert torch.equal(xt3, xt3.to(torch.bfloat16).float())
     del P
     eng.release()
+    eng.gemm = "exact"
 
 
 def test_config5_step_finite_and_deterministic(cfg5, cuda):
@@ -123,5 +128,7 @@ def test_config5_step_grads_vs_oracle_sample(cfg5, features, cuda):
                             saturating=False, what="config 5 f32")
         eng.release()
     else:
-        check_sampled_grads(cfg5["eng"], cfg5["adj"], mild_params(3), cfg5["pos"], tri_s, lab_s, ("exact",), cuda,
-                            saturating=False, what="config 5 bf16", bar=5e-2, loss_bar=2e-2, p_bar=2e-2)
+        # both node-GEMM operand modes: "split" is what bench.py times for config 5
+        check_sampled_grads(cfg5["eng"], cfg5["adj"], mild_params(3), cfg5["pos"], tri_s, lab_s, ("exact", "split"),
+                            cuda, saturating=False, what="config 5 bf16", bar=5e-2, loss_bar=2e-2, p_bar=2e-2)
+        cfg5["eng"].gemm = "exact"

@@ -230,7 +230,8 @@ def test_bwd_columns_partition_sums_to_full(cuda):
     (2, 600, 2, 64, "exact", "node", "f32"), (3, 601, 3, 256, "exact", "node", "f32"),
     (2, 700, 2, 256, "bf16x3", "node", "f32"), (3, 650, 2, 256, "split", "node", "f32"),
     (2, 700, 2, 256, "bf16x3", "node_device", "f32"), (3, 601, 3, 256, "exact", "node_device", "f32"),
-    (2, 800, 8, 256, "split", "node_device", "bf16")])
+    (2, 800, 8, 256, "split", "node_device", "bf16"), (2, 800, 8, 256, "exact", "node_device", "f32"),
+    (3, 800, 8, 256, "bf16x3", "node", "f32")])
 def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, mode, features, cuda):
     """Node-row partitioning (parallel.NodeShard, round 4): rank k owns a contiguous node range (balanced by tail
     edges + node work), computes the node tables of its rows only, takes the scored edges whose tail it owns;
@@ -241,7 +242,9 @@ def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, mode, feature
     beside the layer-3 tail backward), over gloo on the GPU tables.  features "bf16" (config 5's mode: R = 8, bf16
     edge tables, the MFMA tail reduction): bitwise equal across ranks, and within the bf16 mode's own rounding of the
     full batch (loss 1e-4 relative, gradients 1e-2 of max|g|: a node-level sum in another order can flip the
-    bf16 rounding of an edge-table element)."""
+    bf16 rounding of an edge-table element).  R = 8 with fp32 edge tables at the 1e-5 bar: the reduce-scattered
+    dWedge head sums and the head seeds of every relation (a missing or doubled small term, which the bf16 bar and
+    rank-to-rank equality would not see)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     pos, neg = synthetic_graph(N, R, 9000, seed=77)

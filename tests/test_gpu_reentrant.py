@@ -82,16 +82,20 @@ def test_two_engines_two_modes_two_streams_bitwise(cuda):
             assert torch.equal(a, b), mode
 
 
-@pytest.mark.parametrize("gemm", ["exact", "bf16x3"])
-def test_overlap_backward_bitwise_eager_and_graphed(gemm, cuda):
-    N, R, D = 4000, 2, 256
+@pytest.mark.parametrize("gemm,R,features", [("exact", 2, "f32"), ("bf16x3", 2, "f32"), ("split", 8, "bf16")])
+def test_overlap_backward_bitwise_eager_and_graphed(gemm, R, features, cuda):
+    """Engine.overlap: the layer-2/3 tail reductions on a side stream (fork after everything queued, join before the
+    head side).  R = 8 with bf16 edge tables (config 5's mode) forks the fused tail + head-term reduction
+    (tail_seg_reduce_head: dP, dWedge and the per-node <dO, P_r> into dwh, read by head_dz after the join): bitwise the
+    single-stream step, eager and HIP-graph replayed."""
+    N, D = 4000, 256
     pos, neg = synthetic_graph(N, R, 40_000, seed=17)
     tri = np.concatenate([pos, neg])
     lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
     params = _params(N, R, D, 5)
 
     def four_steps(overlap, graphed):
-        eng = Engine(N, R, D, cuda, gemm=gemm)
+        eng = Engine(N, R, D, cuda, gemm=gemm, features=features)
         eng.overlap = overlap
         P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
         P.load(params)
