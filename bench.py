@@ -361,8 +361,9 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     if shard == "node" and world > 1:
         # node-row partitioning: rank k owns a contiguous node range (balanced by tail edges + node work) and the
         # scored edges whose tail it owns (parallel.NodeShard)
-        from iddgcn_amd.parallel import node_ranges, node_shard_triples
-        cuts = node_ranges(np.bincount(np.concatenate([pos[:, 2], neg[:, 2]]), minlength=N), world)
+        from iddgcn_amd.parallel import node_ranges, node_row_weight, node_shard_triples
+        cuts = node_ranges(np.bincount(np.concatenate([pos[:, 2], neg[:, 2]]), minlength=N), world,
+                           node_weight=node_row_weight(R, args.features or cfg.get("features", "f32")))
         tri, lab = node_shard_triples(np.concatenate([pos, neg]),
                                       np.concatenate([np.ones(npos, np.float32), np.zeros(len(neg), np.float32)]),
                                       cuts, rank)

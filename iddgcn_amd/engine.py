@@ -631,11 +631,23 @@ class Engine:
         # reads do^3, x^2, P^3, Wedge^3 and writes dP, dWedge, dS^3, do^2: nothing of dO^3)
         seeds = sh.reduce_scatter(dOn, async_op=True)
         pl = self.use_planes
+        # the tail segments of the rank's edges are the owned rows' (edges are taken by tail): the tail reductions
+        # run over [a, b) only, their dP / dES rows are the owned ones
+        tptr = ed.tptr[a:b + 1]
+        # bf16 edge tables at R = 8, D = 256 (config 5): layers 2 and 1 take the fused tail + head-term reduction (their
+        # head seeds dO[a:b] are final: the node level of the layer above), then head_dz over the owned rows with the
+        # reduce-scattered dWedge head sums; layer 3's head seeds are still on the wire during its tail reduction
+        fuse = self.features == "bf16" and R == 8 and D == 256
         for l in (2, 1, 0):
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
             do = ws.xt[l]
-            ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
-                                dsum=ws.dES if l == 0 else None)
+            fused = fuse and l < 2
+            if b > a and fused:
+                ops.tail_seg_reduce_head(tptr, ws.Wedge[l], do, Pl[:, a:b], ws.dP[:, a:b], ws.dWedge, dOn[a:b],
+                                         Wl[a:b], ws.dwh[a:b], dsum=ws.dES[a:b] if l == 0 else None)
+            elif b > a:
+                ops.tail_seg_reduce(tptr, None, ws.Wedge[l], do, Pl[:, a:b], ws.dP[:, a:b], ws.dWedge,
+                                    dsum=ws.dES[a:b] if l == 0 else None)
             if l > 0:
                 with self._mark("tail_dS_tn"):
                     ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)
@@ -649,8 +661,12 @@ class Engine:
             Xin = ws.X[l - 1] if l > 0 else P["E"]
             ws.WaT.copy_(P[f"Wa{l + 1}"].t())
             if b > a:
-                ops.head_bwd_node(dOn[a:b], Pl[:, a:b], ws.Ssm[l][a:b], Wl[a:b], ws.dP[:, a:b], ws.dz[a:b],
-                                  ep=ws.ep[a:b], dsum=ws.dES[a:b] if l == 0 else None)
+                if fused:       # dW = dwh + the head sums: head_dz over one-entry "segments" n -> ep[a + n]
+                    ops.head_dz(ws.Ssm[l][a:b], Wl[a:b], sh.owned_ptr(self.device), sh.owned_idx(self.device), ws.ep,
+                                ws.dwh[a:b], ws.dz[a:b])
+                else:
+                    ops.head_bwd_node(dOn[a:b], Pl[:, a:b], ws.Ssm[l][a:b], Wl[a:b], ws.dP[:, a:b], ws.dz[a:b],
+                                      ep=ws.ep[a:b], dsum=ws.dES[a:b] if l == 0 else None)
                 ops.gemm_tn_narrow(Xin[a:b], ws.dz[a:b], G[f"Wa{l + 1}"], G[f"ba{l + 1}"], ws.narrow_slab)
                 tn = [(Xin[a:b], dOn[a:b], G[f"S{l + 1}"], True) if l > 0 else (P["E"][a:b], ws.dES[a:b], G["S1"], False)]
                 tn += [(ws.AE[r][a:b], ws.dP[r][a:b], dK[r], False) for r in range(R)]

@@ -358,14 +358,27 @@ def seg_gather_reduce(seg_ptr, rows, out, *, perm=None, coef=None, r_idx=None, r
             "seg_gather_reduce")
 
 
+def _req_rel_rows(t, shape, name):
+    """An (R, n, D) fp32 GPU view whose rows are contiguous (a node-row range of an (R, N, D) table keeps its
+    relation stride); returns that stride (elements)."""
+    if t is None:
+        return 0
+    if not t.is_cuda or t.dtype != _F32:
+        raise L.IddgcnError(f"{name} must be an fp32 GPU tensor (no CPU fallback)")
+    if tuple(t.shape) != tuple(shape) or t.stride(1) != shape[2] or t.stride(2) != 1:
+        raise L.IddgcnError(f"{name} must be {tuple(shape)} with contiguous rows")
+    return t.stride(0)
+
+
 def tail_seg_reduce_head(seg_ptr, W, dO, P, dP, dWedge, head_dO, Wn, dwh, dsum=None):
     """tail_seg_reduce with per-edge W on bf16 rows at R = 8, D = 256, fused with the head chain's node terms of the
     same layer (iddgcn_tail_seg_reduce_head_bf16, ABI 9): dP[r][n] = tail sum + Wn[n][r] head_dO[n], dsum[n] = tail
-    sum + head_dO[n], dwh[n][r] = <head_dO[n], P_r[n]>; the head backward is then head_dz."""
+    sum + head_dO[n], dwh[n][r] = <head_dO[n], P_r[n]>; the head backward is then head_dz.  P, dP: (R, n, D) views
+    with contiguous rows (a node-row range: seg_ptr the matching slice of the tail pointers, absolute edge offsets)."""
     R, n_nodes, D = P.shape
     _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")
-    _req(P, _F32, (R, n_nodes, D), "P")
-    _req(dP, _F32, (R, n_nodes, D), "dP")
+    ps = _req_rel_rows(P, (R, n_nodes, D), "P")
+    dps = _req_rel_rows(dP, (R, n_nodes, D), "dP")
     _req(dsum, _F32, (n_nodes, D), "dsum")
     _req(head_dO, _F32, (n_nodes, D), "head_dO")
     _req(Wn, _F32, (n_nodes, R), "Wn")
@@ -374,7 +387,7 @@ def tail_seg_reduce_head(seg_ptr, W, dO, P, dP, dWedge, head_dO, Wn, dwh, dsum=N
     if W.shape[0] != dO.shape[0]:
         raise L.IddgcnError("tail_seg_reduce_head: per-edge W must have one row per edge")
     L.check(L.lib().iddgcn_tail_seg_reduce_head_bf16(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(W), _ptr(dO),
-                                                     _ptr(P), n_nodes * D, _ptr(dP), n_nodes * D, _ptr(dsum),
+                                                     _ptr(P), ps, _ptr(dP), dps, _ptr(dsum),
                                                      _ptr(dWedge), _ptr(head_dO), _ptr(Wn), _ptr(dwh)),
             "tail_seg_reduce_head")
 
@@ -393,17 +406,20 @@ def head_dz(Ssm, W, hseg_ptr, hperm, dWedge, dwh, dz):
 
 
 def tail_seg_reduce(seg_ptr, h_idx, W, dO, P, dP, dWedge, dsum=None):
+    """Tail segment sums of a layer's backward (include/iddgcn.h iddgcn_tail_seg_reduce_*): dP[r][n] = sum over the
+    tail segment of n of W[e][r] dO[e], dWedge[e][r] = <dO[e], P_r[t_e]> (and dsum[n] = sum of dO[e]).  P, dP: (R, n,
+    D) views with contiguous rows (a node-row range: seg_ptr the matching slice of the tail pointers)."""
     R, n_nodes, D = P.shape
     _req(seg_ptr, _I32, (n_nodes + 1,), "seg_ptr")
-    _req(P, _F32, (R, n_nodes, D), "P")
-    _req(dP, _F32, (R, n_nodes, D), "dP")
+    ps = _req_rel_rows(P, (R, n_nodes, D), "P")
+    dps = _req_rel_rows(dP, (R, n_nodes, D), "dP")
     _req(dsum, _F32, (n_nodes, D), "dsum")
     if h_idx is None and W.shape[0] != dO.shape[0]:
         raise L.IddgcnError("tail_seg_reduce: per-edge W must have one row per edge")
     _req(dO, _BF16 if dO.dtype == _BF16 else _F32, None, "dO")
     fn = L.lib().iddgcn_tail_seg_reduce_bf16 if dO.dtype == _BF16 else L.lib().iddgcn_tail_seg_reduce_f32
     L.check(fn(_stream(), n_nodes, D, R, _ptr(seg_ptr), _ptr(h_idx), _ptr(W),
-                                               _ptr(dO), _ptr(P), n_nodes * D, _ptr(dP), n_nodes * D, _ptr(dsum),
+                                               _ptr(dO), _ptr(P), ps, _ptr(dP), dps, _ptr(dsum),
                                                _ptr(dWedge)), "tail_seg_reduce")
 
 

@@ -172,10 +172,25 @@ class RelationShard:
             table[self.a:self.b].copy_(full[self.a:self.b])
 
 
+def node_row_weight(R, features="f32"):
+    """Node-level work of one node row in edge-equivalents (scored edges' work), for node_ranges.
+
+    In D x D GEMM rows: a scored edge costs the tail chain's 6 (2 forward, 2 sigma' backward, 2 dS TN), a node row
+    9R + 8 (3R + 1 projections, 3R dAE and 3R dK rows, the head chain's 2 forward, 2 backward and 2 dS TN rows, dE's
+    1; the SpMM rows and the head / tail reductions scale alike).  The bf16-feature mode halves the edge tables' bytes
+    and runs the edge GEMMs at 2 bf16 MFMAs per k-step while the node tables stay fp32: a node row weighs twice as
+    many edges.  Calibrated on the single-GPU kernel profiles: R = 2 fp32 (config 4) 4.3, the round-4 constant 4 gave
+    per-rank steps within 3% (profiles/r04/dryrun_cfg4.jsonl); R = 8 bf16 (config 5) 26.7 against 26 from the
+    node-level vs edge-level kernel times (profiles/r04/kernel_stats_cfg5_r04z4.txt: 79 ms per 1M rows, 151 ms per
+    50M scored edges)."""
+    return (9.0 * R + 8.0) / 6.0 * (2.0 if features == "bf16" else 1.0)
+
+
 def node_ranges(tail_counts, world_size, node_weight=4.0):
     """Contiguous node-row ranges [b_k, b_k+1) for a node-partitioned step: balanced by the work a row brings,
     its scored edges (tail segment length) plus ``node_weight`` edge-equivalents of node-level work (the row's
-    SpMM, projections and head chain, ~4.5 edge GEMM rows at R = 2).  Returns world_size + 1 boundaries."""
+    SpMM, projections and head chain: node_row_weight(R, features); 4 ~ R = 2).  Returns world_size + 1
+    boundaries."""
     w = np.asarray(tail_counts, dtype=np.float64) + float(node_weight)
     c = np.concatenate([[0.0], np.cumsum(w)])
     cuts = [int(np.searchsorted(c, c[-1] * k / world_size, side="left")) for k in range(world_size + 1)]
@@ -216,6 +231,7 @@ class NodeShard:
         # any backend, so that gloo tests on CPU tensors run the code path the RCCL ranks take
         self._gloo = (dist.get_backend(group) == "gloo") if staged is None else bool(staged)
         self._idx = None
+        self._ptr = None
 
     def owned_idx(self, device):
         """int32 arange(a, b) on the device (row indices of the owned range, for gathered-row kernel forms)."""
@@ -223,6 +239,14 @@ class NodeShard:
         if self._idx is None or self._idx.device != device:
             self._idx = torch.arange(self.a, self.b, dtype=torch.int32, device=device)
         return self._idx
+
+    def owned_ptr(self, device):
+        """int32 arange(0, b - a + 1) on the device: one-entry segments over the owned rows (head_dz reading the
+        reduce-scattered head sums ep[a + n] through owned_idx)."""
+        import torch
+        if self._ptr is None or self._ptr.device != device:
+            self._ptr = torch.arange(0, self.b - self.a + 1, dtype=torch.int32, device=device)
+        return self._ptr
 
     def _padded(self, table):
         import torch

@@ -8,7 +8,8 @@ first for reference.  Collective volumes of the real step are reported beside it
 DESIGN.md's strong-scaling model = max_k compute_k + un-overlapped collectives can be written from measurements.
 (The numbers the kernels produce here are meaningless - other ranks' rows are never filled - only the timing is.)
 
-usage: python tools/node_shard_dryrun.py [config=4] [world=8] [steps=3] [ranks=all|k,k,...]
+usage: python tools/node_shard_dryrun.py [config=4] [world=8] [steps=3] [ranks=all|none|k,k,...] [node_weight]
+  (ranks "none": the single-GPU step only; a rank list skips it; node_weight: default parallel.node_row_weight)
 """
 import json
 import sys
@@ -21,8 +22,13 @@ sys.path.insert(0, ".")
 from bench import CONFIGS, reference_init  # noqa: E402
 from iddgcn_amd.engine import Engine, FlatParams, KerasAdam  # noqa: E402
 from iddgcn_amd.graph import get_adj_mats  # noqa: E402
-from iddgcn_amd.parallel import node_ranges, node_shard_triples  # noqa: E402
+from iddgcn_amd.parallel import node_ranges, node_row_weight, node_shard_triples  # noqa: E402
 from iddgcn_amd.utils import synthetic_graph  # noqa: E402
+
+
+class _Done:
+    def wait(self):
+        pass
 
 
 class DryShard:
@@ -40,11 +46,18 @@ class DryShard:
             self._idx = torch.arange(self.a, self.b, dtype=torch.int32, device=device)
         return self._idx
 
-    def all_gather(self, table):
-        self.bytes += table.numel() * table.element_size() * (self.world - 1) // self.world
+    def owned_ptr(self, device):
+        if getattr(self, "_ptr", None) is None:
+            self._ptr = torch.arange(0, self.b - self.a + 1, dtype=torch.int32, device=device)
+        return self._ptr
 
-    def reduce_scatter(self, table):
+    def all_gather(self, table, async_op=False):
         self.bytes += table.numel() * table.element_size() * (self.world - 1) // self.world
+        return _Done()
+
+    def reduce_scatter(self, table, async_op=False):
+        self.bytes += table.numel() * table.element_size() * (self.world - 1) // self.world
+        return _Done()
 
 
 def time_steps(eng, P, G, adj, ed, T, steps):
@@ -63,7 +76,7 @@ def main():
     cid = int(a[0]) if a else 4
     world = int(a[1]) if len(a) > 1 else 8
     steps = int(a[2]) if len(a) > 2 else 3
-    only = None if len(a) < 4 or a[3] == "all" else [int(x) for x in a[3].split(",")]
+    only = None if len(a) < 4 or a[3] == "all" else ([] if a[3] == "none" else [int(x) for x in a[3].split(",")])
     cfg = CONFIGS[cid]
     N, R, D, M = cfg["N"], cfg["R"], cfg["D"], cfg["M"]
     feat = cfg.get("features", "f32")
@@ -83,11 +96,14 @@ def main():
     out = {"config": cfg["name"], "world": world, "gemm": gemm, "features": feat, "steps": steps}
     eng = Engine(N, R, D, dev, gemm=gemm, features=feat)
     ed = eng.edges(tri, lab)
-    out["full_ms"] = time_steps(eng, P, G, adj, ed, T, steps)
-    print(json.dumps({"full_ms": out["full_ms"]}), flush=True)
+    if only is None or a[3] == "none":
+        out["full_ms"] = time_steps(eng, P, G, adj, ed, T, steps)
+        print(json.dumps({"full_ms": out["full_ms"]}), flush=True)
     del eng, ed
     torch.cuda.empty_cache()
-    cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
+    nw = float(a[4]) if len(a) > 4 else node_row_weight(R, feat)
+    out["node_weight"] = nw
+    cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world, node_weight=nw)
     out["cuts"] = cuts
     ranks = []
     for k in range(world):
@@ -110,7 +126,8 @@ def main():
     out["ranks"] = ranks
     if ranks:
         out["max_rank_ms"] = max(r["ms"] for r in ranks)
-        out["compute_speedup"] = out["full_ms"] / out["max_rank_ms"]
+        if "full_ms" in out:
+            out["compute_speedup"] = out["full_ms"] / out["max_rank_ms"]
     print(json.dumps(out), flush=True)
 
 
