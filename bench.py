@@ -396,6 +396,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         opt = KerasAdam(P)
         for _ in range(warmup):
             eng.train_step(P, G, opt, adj, ed, t_global=T, comm=comm)
+        eng.finish_pending()
         torch.cuda.synchronize()
         eng.probe = {} if probe else None
         if world > 1:
@@ -404,6 +405,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         t0 = time.perf_counter()
         for _ in range(steps):
             loss = eng.train_step(P, G, opt, adj, ed, t_global=T, comm=comm)
+        eng.finish_pending()               # node rows: the last step's all-gather of E (its work, inside the timing)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -432,10 +434,13 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     if world > 1:
         out["ranks_consistent"] = consist == 0.0
         out["params_max_abs_diff_vs_rank0"] = consist
-        # the RCCL-only branches (BucketedAllReduce's asynchronous in-place buckets, RelationShard's collectives, this
-        # consistency check and the secondary workloads' fit vote) have run over gloo only: every builder box has one
-        # GPU
-        out["rccl_paths_verified_before_this_run"] = False
+        # the RCCL calls of the multi-rank branches (NodeShard's padded all_gather / reduce_scatter incl. the node-row
+        # E ownership, BucketedAllReduce's asynchronous in-place buckets, RelationShard's collectives, this consistency
+        # check) have executed on RCCL at world size 1 on a builder box (tests/test_gpu_rccl.py: bitwise the gloo and
+        # the communicator-free steps; profiles/r05/gpu_tests_r05b.txt) and over gloo at world 2-3; never with more
+        # than one GPU before a multi-GPU driver run (every builder box has one GPU)
+        out["rccl_paths_verified_before_this_run"] = {"rccl_world1_on_one_gpu": True, "gloo_world2_3": True,
+                                                      "rccl_multi_gpu": False}
     if other_mode and feat == "f32":
         mode2 = "exact" if gemm != "exact" else "bf16x3"
         el2, loss2, _ = timed_run(mode2, False)

@@ -135,6 +135,27 @@ class KerasAdam:
             pos = max(pos, b)
 
 
+    def apply_owned(self, params, grads, comm, rs_e, e_lo, e_hi):
+        """apply() after a node-partitioned backward whose dE was reduce-scattered to the row owners
+        (Engine._backward_rows with e_owner; round 5): the small gradients' buckets (everything past E, all-reduced)
+        are updated as their sums land, then this rank's E rows — flat elements [e_lo, e_hi) — once ``rs_e`` (the
+        reduce-scatter handle) completes.  The other E rows and their moments are left to their owners (the
+        caller all-gathers E); the update being elementwise, the owners' rows together are the whole update."""
+        self.iterations += 1
+        alpha = self.alpha_at(self.iterations)
+        n, base = params.flat.numel(), grads.buf.data_ptr()
+        n_e = params["E"].numel()
+
+        def on_bucket(view):
+            off = (view.data_ptr() - base) // view.element_size()
+            if view.dtype == grads.buf.dtype and n_e <= off < n:
+                self._apply_range(params, grads, off, min(off + view.numel(), n), alpha)
+
+        comm.finish_each(on_bucket)
+        rs_e.wait()
+        if e_hi > e_lo:
+            self._apply_range(params, grads, e_lo, e_hi, alpha)
+
     def apply_table(self, params, grads, alpha_table, step):
         """apply() with alpha = alpha_table[step] read on the device (HIP-graph replay); the caller
         advances ``step`` and, after the replays, ``iterations``."""
@@ -304,13 +325,24 @@ class Engine:
             return "exact4"
         return "exact4" if self._gemm == "exact" else self._gemm
 
+    _row_gemm = None
+
     @property
     def row_gemm(self):
         """Precision of the other row GEMMs (the tail / head chains and their backward): the engine's ``gemm``,
         except at D < 256 in the exact mode, where the register-staged kernel takes "exact4" for every form (the
         four-chain accumulation costs nothing there and keeps the trained-weight logits of the reference's
-        64-wide model further inside the 1e-4 bar)."""
+        64-wide model further inside the 1e-4 bar).  Settable (None = this default), as ``proj_gemm`` is: a second
+        summation order for the training-drift measurement (tools/fold_order_sensitivity.py)."""
+        if self._row_gemm is not None:
+            return self._row_gemm
         return "exact4" if (self._gemm in ("exact", "bf16x3") and self.D < 256) else self._gemm
+
+    @row_gemm.setter
+    def row_gemm(self, mode):
+        if mode is not None and mode not in PROJ_MODES:
+            raise L.IddgcnError(f"row_gemm must be None or one of {sorted(PROJ_MODES)}")
+        self._row_gemm = mode
 
     @proj_gemm.setter
     def proj_gemm(self, mode):
@@ -449,13 +481,14 @@ class Engine:
     _pred_seed = None      # None: BCE seed; a float: gradient of pred_seed * sum_e p_e
 
     # -- backward -----------------------------------------------------------
-    def backward(self, P, G, adj, ed, ws, comm=None):
+    def backward(self, P, G, adj, ed, ws, comm=None, e_owner=False):
         """Gradients of the step into G (and the loss sum into G.loss).  ``comm`` (data parallel,
         parallel.BucketedAllReduce) gets each contiguous piece of G.buf as soon as it is final: all
         small gradients + the loss after the layer loop, then row chunks of dE as the transposed SpMM
-        produces them, so the all-reduce of the large dE overlaps the SpMM of the next chunk."""
+        produces them, so the all-reduce of the large dE overlaps the SpMM of the next chunk.  ``e_owner``
+        (node-partitioned steps only): dE is reduce-scattered to the row owners instead (returns the handle)."""
         if self.row_shard is not None:
-            return self._backward_rows(P, G, adj, ed, ws, comm)
+            return self._backward_rows(P, G, adj, ed, ws, comm, e_owner)
         N, R, D = self.N, self.R, self.D
         pk, pn, pr = dict(precision=self.gemm), dict(precision=self.proj_gemm), dict(precision=self.row_gemm)
         dOn, dOn_next = ws.dOn_a, ws.dOn_b      # head seed dO^3, written by distmult_bce_heads
@@ -561,10 +594,20 @@ class Engine:
             return 1.0 / (float(self._t_global or T) * float(self.N)), True
         return float(self._pred_seed), False
 
+    _e_pending = None      # the asynchronous all-gather of E after an owner-row Adam (node-partitioned train_step)
+
+    def finish_pending(self):
+        """Complete the all-gather of E a node-partitioned train_step left in flight (the next forward does it
+        itself, after its owner-local work): every rank's E whole again."""
+        pend, self._e_pending = self._e_pending, None
+        if pend is not None:
+            pend.wait()
+
     def _forward_rows(self, P, adj, ed, ws, train):
         """The forward with the node tables computed for the owned rows [a, b) only (parallel.NodeShard): the
         rank's scored edges all have their tail there, so the tail chain reads local P / ES1 rows; the edges'
-        heads need W^l (all-gathered, N x R) and DistMult X^3 (all-gathered, N x D)."""
+        heads need W^l (all-gathered, N x R) and DistMult X^3 (all-gathered, N x D).  E S^1 and the layer-1 alpha
+        read the owned E rows only: they run first, beside a pending all-gather of E (train_step's owner Adam)."""
         N, R, D, T = self.N, self.R, self.D, ed.T
         sh = self.row_shard
         a, b = sh.a, sh.b
@@ -573,16 +616,18 @@ class Engine:
         pr = dict(precision=self.row_gemm)
         idx = sh.owned_idx(self.device)
         if b > a:
+            ops.rowgemm(E[a:b], P["S1"], ws.ES1[a:b], **pn)
+            ops.alpha_fwd(E[a:b], P["Wa1"], P["ba1"], ws.Ssm[0][a:b], ws.W[0][a:b])
+        self.finish_pending()
+        if b > a:
             for r in range(R):              # A_r E over the owned rows (IDDGCN.py:69-70)
                 ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + a:r * (N + 1) + b + 1], adj.fwd_col, adj.fwd_val, E,
                              ws.AE[r][a:b].view(1, b - a, D), 1, b - a)
             proj = [(ws.AE[r][a:b], P[f"K{l + 1}"][r], ws.P[l, r][a:b], pn) for l in range(NUM_LAYERS)
                     for r in range(R)]
-            proj.append((E[a:b], P["S1"], ws.ES1[a:b], pn))
             nb = L.ROWGEMM_BATCH
             for i in range(0, len(proj), nb):
                 ops.rowgemm_batched(proj[i:i + nb])
-            ops.alpha_fwd(E[a:b], P["Wa1"], P["ba1"], ws.Ssm[0][a:b], ws.W[0][a:b])
         sh.all_gather(ws.W[0])
         # node level first (layers 1-3 over the owned rows, W^l all-gathered as each layer's alpha is known), so
         # that DistMult's head rows X^3 travel while ALL of the tail side runs (the layer-1 combine, the two tail
@@ -615,11 +660,13 @@ class Engine:
         else:
             ops.distmult_bce(ws.X[2], ed.h, ws.xt[2], ed.r, P["rel"], p_out=ws.p, s_out=ws.s)
 
-    def _backward_rows(self, P, G, adj, ed, ws, comm):
+    def _backward_rows(self, P, G, adj, ed, ws, comm, e_owner=False):
         """The backward of a node-partitioned step: the head seeds dO^3 and the dWedge head sums are
         reduce-scattered to the heads' owners, everything node-level runs over the owned rows, the tail
         segment sums are local; every gradient written is a partial over the rank's rows / edges, summed by
-        ``comm`` (the flat gradient buffer's bucketed all-reduce)."""
+        ``comm`` (the flat gradient buffer's bucketed all-reduce).  ``e_owner``: dE is not all-reduced but
+        reduce-scattered to the row owners (asynchronously; the handle is returned, and G["E"][a:b] holds the sums
+        once it is waited for), for the owners' Adam (KerasAdam.apply_owned) and an all-gather of E."""
         N, R, D = self.N, self.R, self.D
         sh = self.row_shard
         a, b = sh.a, sh.b
@@ -692,6 +739,9 @@ class Engine:
         G["E"][:a].zero_()
         G["E"][b:].zero_()
         bptr, bcol, bval = adj.bwd_node_rows(a, b)
+        if e_owner:
+            ops.spmm_csr(bptr, bcol, bval, ws.dAE.view(R * N, D), G["E"].view(1, N, D), 1, N, accumulate=True)
+            return sh.reduce_scatter(G["E"], async_op=True)
         chunks = comm.row_chunks(N) if comm is not None else [(0, N)]
         for n0, n1 in chunks:
             ops.spmm_csr(bptr[n0:n1 + 1], bcol, bval, ws.dAE.view(R * N, D),
@@ -707,6 +757,16 @@ class Engine:
         ws = self.workspace(ed.T, True)
         self._t_global = t_global
         self.forward(params, adj, ed, ws, True)
+        sh = self.row_shard
+        if sh is not None and getattr(sh, "owner_e", False) and comm is not None:
+            # node-partitioned step, E owned by rows (round 5): dE reduce-scattered to the owners, Adam over the owned
+            # E rows only, E all-gathered asynchronously — the next forward runs its owner-local work (E S^1 and the
+            # layer-1 alpha of the owned rows) before it waits (finish_pending)
+            rs = self.backward(params, grads, adj, ed, ws, comm, e_owner=True)
+            D = self.D
+            opt.apply_owned(params, grads, comm, rs, sh.a * D, sh.b * D)
+            self._e_pending = sh.all_gather(params["E"], async_op=True)
+            return grads.loss
         self.backward(params, grads, adj, ed, ws, comm)
         if comm is not None and hasattr(comm, "finish_each") and hasattr(opt, "apply_overlapped"):
             opt.apply_overlapped(params, grads, comm)

@@ -2,8 +2,8 @@
 
 Two partitions of the step.  Node-row partitioning (NodeShard below, bench.py's default with more
 than one GPU) splits the node rows and takes the scored edges by tail.  Edge partitioning (``--shard edge``; the
-default of IDDGCN_Model.fit's multi-rank branch): the scored edges of a full-batch step are
-independent given the node tables, so each rank takes a contiguous slice of them; the graph (CSR
+default of IDDGCN_Model.fit's multi-rank branch; described in the rest of this paragraph): the scored edges of a
+full-batch step are independent given the node tables, so each rank takes a contiguous slice of them; the graph (CSR
 of every A_r) and all parameters are replicated.  Every gradient of the step is a sum over scored
 edges, so the per-rank gradients — already normalised by the GLOBAL edge count — are summed by an
 all-reduce of the flat gradient buffer IN PLACE (FlatParams.buf = [E | rel | layer params | loss]),
@@ -211,14 +211,21 @@ class NodeShard:
                 all-gather X^3 (N x D): DistMult's head rows;
       backward  reduce-scatter dO^3 (N x D): the head seeds of the rank's edges go to the heads' owners;
                 reduce-scatter the dWedge head sums (N x R, 3 per step);
-                all-reduce of the flat gradient buffer (dE: the transposed SpMM of the owned dAE rows reaches every
-                column; the weight gradients are partial sums over the owned rows / edges).
+                all-reduce of the flat gradient buffer past E (the weight gradients are partial sums over the owned
+                rows / edges);
+                dE (the transposed SpMM of the owned dAE rows reaches every column): with ``owner_e`` (default)
+                reduce-scattered to the row owners, who alone run Adam over their E rows (1/p of the largest
+                update), then E all-gathered, asynchronously, beside the next forward's owner-local start (E S^1 and
+                the layer-1 alpha of the owned rows); without it, all-reduced with the rest of the buffer.
     That is 2 N D + 6 N R floats of all-gather / reduce-scatter beside edge partitioning's N D all-reduce, against
     RelationShard's 6 R N D.  Padded to equal chunks (the ranges differ in length); gloo groups (several ranks
     sharing a GPU in tests) stage through host memory."""
 
-    def __init__(self, cuts, group=None, staged=None):
+    def __init__(self, cuts, group=None, staged=None, owner_e=True):
         self.group = group
+        # owner_e (round 5): Engine.train_step reduce-scatters dE to the row owners, runs Adam over the owned E rows only
+        # and all-gathers E (instead of all-reducing dE and updating every row on every rank)
+        self.owner_e = bool(owner_e)
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.cuts = [int(c) for c in cuts]
         if len(self.cuts) != self.world + 1:

@@ -294,7 +294,7 @@ def _adam_worker(rank, world, port, q, mode):
         eng = Engine(N, R, D, dev, gemm="bf16x3")
         if mode == "node_device":
             cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
-            eng.row_shard = NodeShard(cuts, staged=False)
+            eng.row_shard = NodeShard(cuts, staged=False, owner_e=False)     # (owner_e: test_node_sharded_owner_e_adam)
             mine, mlab = node_shard_triples(tri, lab, cuts, rank)
         else:
             lo, hi = shard_range(len(tri), rank, world)
@@ -340,3 +340,89 @@ def test_overlapped_adam_equals_adam_after_allreduce(mode, cuda):
         assert p.exitcode == 0
     assert out[0][1] and out[1][1]
     assert np.array_equal(out[0][2], out[1][2])
+
+
+def _owner_worker(rank, world, port, q, staged, N, R, D, gemm):
+    """Two node-partitioned training steps (Engine.train_step) with E owned by rows (NodeShard owner_e: dE
+    reduce-scattered to the row owners, Adam over the owned E rows, E all-gathered) and with the all-reduce of the
+    whole gradient buffer (owner_e False): parameters, moments and the owned rows' dE of each."""
+    import torch.distributed as dist
+    from iddgcn_amd.engine import KerasAdam
+    from iddgcn_amd.parallel import BucketedAllReduce, NodeShard, node_ranges, node_shard_triples
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        pos, neg = synthetic_graph(N, R, 9000, seed=77)
+        tri = np.concatenate([pos, neg])
+        lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+        cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
+        mine, mlab = node_shard_triples(tri, lab, cuts, rank)
+        eng = Engine(N, R, D, dev, gemm=gemm)
+        adj = eng.adjacency(get_adj_mats(pos, N, R))
+        ed = eng.edges(mine, mlab)
+        a, b = cuts[rank], cuts[rank + 1]
+        res = {}
+        for owner in (True, False):
+            eng.row_shard = NodeShard(cuts, staged=staged, owner_e=owner)
+            P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
+            P.load(_mild(N, R, D, 9))
+            opt = KerasAdam(P)
+            comm = BucketedAllReduce(min_bucket_rows=64, host_staged=staged)
+            dE0 = None
+            for _ in range(2):
+                eng.train_step(P, G, opt, adj, ed, t_global=len(tri), comm=comm)
+                if dE0 is None:
+                    dE0 = G["E"][a:b].cpu().numpy()        # the first step's summed dE rows (at the initial weights)
+            eng.finish_pending()
+            torch.cuda.synchronize()
+            res[owner] = (P.buf.cpu().numpy(), opt.m[a * D:b * D].cpu().numpy(), opt.v[a * D:b * D].cpu().numpy(), dE0)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,staged", [(2, None), (2, False), (3, False)])
+def test_node_sharded_owner_e_adam(world, staged, cuda):
+    """Round 5: a node-partitioned step reduce-scatters dE to the row owners, each rank runs
+    Keras Adam over its own E rows only and E is all-gathered asynchronously (completed by the next forward, after
+    its owner-local E S^1 and layer-1 alpha).  world 2 / 3 ranks on one GPU over gloo, host-staged (None) and device
+    (False) collectives, two training steps: every rank's parameters bitwise equal; the owned rows' dE of the last
+    step... (see below); the first step's dE of the owned rows, assembled over the ranks, equal to the single-process
+    full batch's dE (1e-5 of max|g|); against the same sharded step with dE all-reduced (owner_e False): the weights past E bitwise, E and the
+    owned rows' Adam moments bitwise at world 2 (a + b is a + b in either collective) and within 1e-6 of max|E| at
+    world 3 (the reduce-scatter may add the three partials in another order than the all-reduce)."""
+    N, R, D, gemm = 700, 2, 256, "bf16x3"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, q, staged, N, R, D, gemm)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, res in out[1:]:
+        assert np.array_equal(res[True][0], out[0][1][True][0])
+    nE = N * D
+    for _, res in out:
+        own, ar = res[True], res[False]
+        assert np.array_equal(own[0][nE:], ar[0][nE:])
+        if world == 2:
+            assert all(np.array_equal(x, y) for x, y in zip(own, ar))
+        else:
+            assert np.abs(own[0][:nE] - ar[0][:nE]).max() <= 1e-6 * np.abs(ar[0][:nE]).max()
+    # the first step's dE, owned rows assembled, against the full batch at the same (initial) parameters
+    pos, neg = synthetic_graph(N, R, 9000, seed=77)
+    tri = np.concatenate([pos, neg])
+    lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+    eng = Engine(N, R, D, cuda, gemm=gemm)
+    P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
+    P.load(_mild(N, R, D, 9))
+    adj, ed = eng.adjacency(get_adj_mats(pos, N, R)), eng.edges(tri, lab)
+    eng.loss_and_grads(P, G, adj, ed)
+    full = G["E"].cpu().numpy()
+    dE = np.concatenate([res[True][3] for _, res in out])
+    assert np.abs(dE - full).max() <= 1e-5 * np.abs(full).max()

@@ -7,7 +7,9 @@ calls through RCCL on the box's GPU:
   * ``NodeShard(staged=False)``: padded ``all_gather_into_tensor`` (W^l, X^3 asynchronously) and
     ``reduce_scatter_tensor`` (dO^3 asynchronously, the dWedge head sums);
   * ``BucketedAllReduce``'s device branch: asynchronous in-place ``all_reduce`` of the flat gradient buffer's buckets,
-    with ``KerasAdam.apply_overlapped`` updating each bucket as its sum lands (Engine.train_step);
+    with ``KerasAdam.apply_overlapped`` updating each bucket as its sum lands (Engine.train_step, edge partitioning);
+  * the node-row step's E ownership (round 5, NodeShard owner_e): dE ``reduce_scatter_tensor`` to the row owners,
+    ``KerasAdam.apply_owned``, then the asynchronous ``all_gather_into_tensor`` of E (Engine.finish_pending);
   * ``RelationShard``'s ``all_gather_into_tensor`` / ``reduce_scatter_tensor`` (``--shard relation``);
   * bench.py's ``rank_consistency`` (broadcast + MAX all-reduce on the device).
 
@@ -86,6 +88,7 @@ def _child(port, q, N, R, D, gemm, features):
             P.load(_mild(N, R, D, 9))
             opt = KerasAdam(P)
             loss = eng.train_step(P, G, opt, adj, ed, t_global=len(tri), comm=comm)
+            eng.finish_pending()        # node rows (owner_e): the all-gather of E the step left in flight
             torch.cuda.synchronize()
             return float(loss.item()), G.buf.cpu().numpy(), P.buf.cpu().numpy(), P.buf
 

@@ -2,7 +2,8 @@
 
 For a BASELINE config and a world size W, each rank k's engine (its node range [cuts[k], cuts[k+1]) from
 parallel.node_ranges, the scored edges whose tail it owns, the full device adjacency) is built and timed on this
-GPU in turn, with the collectives replaced by no-ops (DryShard): the kernels run on the rank's true shapes, so the
+GPU in turn, with the collectives replaced by no-ops (DryShard, DryComm: the rank's Adam included, over the owned E
+rows and the all-reduced small weights as in the real step): the kernels run on the rank's true shapes, so the
 per-rank time is the compute a rank of a W-GPU job does, without communication.  The single-GPU step is timed
 first for reference.  Collective volumes of the real step are reported beside it (bytes per rank), so that
 DESIGN.md's strong-scaling model = max_k compute_k + un-overlapped collectives can be written from measurements.
@@ -40,6 +41,7 @@ class DryShard:
         self.a, self.b = self.cuts[rank], self.cuts[rank + 1]
         self._idx = None
         self.bytes = 0
+        self.owner_e = True         # the node-row step's E ownership (round 5): dE reduce-scattered, Adam over owned rows
 
     def owned_idx(self, device):
         if self._idx is None:
@@ -60,13 +62,37 @@ class DryShard:
         return _Done()
 
 
-def time_steps(eng, P, G, adj, ed, T, steps):
+class DryComm:
+    """parallel.BucketedAllReduce's interface without the all-reduce: the buckets' Adam runs as in a rank's step."""
+
+    def __init__(self, sh):
+        self.sh, self._views = sh, []
+
+    def row_chunks(self, n_rows):
+        return [(0, n_rows)]
+
+    def ready(self, view):
+        self.sh.bytes += 2 * view.numel() * view.element_size() * (self.sh.world - 1) // self.sh.world
+        self._views.append(view)
+
+    def finish_each(self, fn):
+        views, self._views = self._views, []
+        for v in views:
+            if fn is not None:
+                fn(v)
+
+    def finish(self):
+        self.finish_each(None)
+
+
+def time_steps(eng, P, G, adj, ed, T, steps, comm=None):
     opt = KerasAdam(P)
-    eng.train_step(P, G, opt, adj, ed, t_global=T)
+    eng.train_step(P, G, opt, adj, ed, t_global=T, comm=comm)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        eng.train_step(P, G, opt, adj, ed, t_global=T)
+        eng.train_step(P, G, opt, adj, ed, t_global=T, comm=comm)
+    eng.finish_pending()
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / steps * 1e3
 
@@ -115,10 +141,10 @@ def main():
         eng.row_shard = sh
         ed = eng.edges(t_k, l_k)
         P.load(init)
-        ms = time_steps(eng, P, G, adj, ed, T, steps)
+        ms = time_steps(eng, P, G, adj, ed, T, steps, comm=DryComm(sh))
         r = {"rank": k, "rows": cuts[k + 1] - cuts[k], "scored_edges": int(len(t_k)), "ms": ms,
              "collective_bytes_per_step": sh.bytes // (steps + 1),
-             "dE_allreduce_bytes": 2 * (world - 1) * N * D * 4 // world}
+             "of_which_dE_reduce_scatter_and_E_all_gather": 2 * (world - 1) * N * D * 4 // world}
         ranks.append(r)
         print(json.dumps(r), flush=True)
         del eng, ed

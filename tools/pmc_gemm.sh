@@ -10,7 +10,7 @@ P2="SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_I
 for c in "$@"; do
   for p in 1 2; do
     if [ $p = 1 ]; then CTR=$P1; else CTR=$P2; fi
-    timeout -s KILL 90 rocprofv3 --pmc $CTR -d "$OUT/${c}_$p" -o run --output-format csv -- python3 tools/gemm_probe.py $c $MODE 3 > "$OUT/${c}_$p.log" 2>&1 || { echo "pass $c/$p failed"; exit 1; }
+    timeout -s KILL 90 rocprofv3 --pmc $CTR -d "$OUT/${c}_$p" -o run --output-format csv -- python3 tools/gemm_probe.py ${c%%_*} $MODE 3 > "$OUT/${c}_$p.log" 2>&1 || { echo "pass $c/$p failed"; exit 1; }
   done
 done
 echo pmc_gemm done
