@@ -12,13 +12,12 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 10
+ABI_VERSION = 9
 ROWGEMM_BATCH = 25          # IDDGCN_ROWGEMM_BATCH: entries per iddgcn_rowgemm_batched_f32 call
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
 GEMM_EXACT_F32, GEMM_SPLIT_F16, GEMM_F32_4CHAIN, GEMM_BF16X3 = 0, 1, 2, 3
 PLANES_A, PLANES_C, PLANES_AUX = 1, 2, 4          # iddgcn_rowgemm_t.planes (pre-split edge tables, ABI 4)
-BF16X3_PLANES_BYTES = 393216    # IDDGCN_BF16X3_PLANES_BYTES: one weight's planes for the full-width bf16x3 row GEMM
 
 vp = ctypes.c_void_p
 ci = ctypes.c_int
@@ -40,7 +39,6 @@ class RowGemmArgs(ctypes.Structure):
         ("act", ci), ("aux", vp),
         ("planes", ci),
         ("precision", ci),     # ABI 6/7: operand precision per call (GEMM_EXACT_F32 / F32_4CHAIN / SPLIT_F16 / BF16X3)
-        ("b_planes", vp),      # ABI 10: B pre-split by iddgcn_bf16x3_weight_planes (BF16X3), or NULL
     ]
 
 
@@ -62,7 +60,6 @@ SIGNATURES = {
     "iddgcn_gemm_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci, ci]),
     "iddgcn_rowgemm_batched_f32": (ci, [vp, ctypes.POINTER(RowGemmArgs), ci]),
     "iddgcn_rowgemm_kernel_id": (ci, [ctypes.POINTER(RowGemmArgs)]),
-    "iddgcn_bf16x3_weight_planes": (ci, [vp, vp, ci, vp]),
     "iddgcn_adam_table_f32": (ci, [vp, cll, vp, vp, vp, vp, vp, vp, cf, cf, cf, ci]),
     "iddgcn_step_advance": (ci, [vp, vp, vp, vp]),
     "iddgcn_gemm_tn_narrow_blocks": (ci, [cll]),

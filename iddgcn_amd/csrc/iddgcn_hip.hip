@@ -282,7 +282,6 @@ struct RowGemmP {
     int planes;           // IDDGCN_PLANES_A | _C | _AUX (D = 256 split mode, v3 kernel only)
     int precision;        // IDDGCN_GEMM_* of this call (D = 256 v3 kernels; every other GEMM is exact f32)
     int tiles_per_block;
-    const char* b_planes; // BF16X3: B pre-split for the full-width kernel (ABI 10), or null
 };
 
 // up to ROWGEMM_BATCH independent row GEMMs of one width in one launch (blockIdx.y = entry): the
@@ -2063,262 +2062,6 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
 #undef B3_MAIN_LOOP
 }
 
-// ---- row GEMM, bf16x3 operands, full width ("w4", ABI 10) --------------------------------------------------
-// The b3 kernel above keeps the weight planes in registers, which forces two workgroups per row range (column
-// halves): every A tile is read, DMA'd and converted twice, and each wave reads the whole tile's planes for 16
-// output columns.  Here ONE workgroup owns all 256 columns of a 64-row tile (wave w: columns 32w..32w+31, all 64
-// rows), and the weight planes stream from L2 in k-steps of 32, pre-split once per weight by
-// iddgcn_bf16x3_weight_planes into the wave's fragment order (6 KiB per wave and k-step: 2 k-halves x 3 planes x 64
-// lanes x 16 B; 384 KiB in all, L2-resident).  Per k-step q of a tile:
-//   * A: the tile's 64 rows x 32 k (8 KiB fp32) come to registers, 16 B per lane (global_load_dwordx4, issued three
-//     k-steps ahead), are split into the three bf16 planes by the lane that loaded them and stored to LDS (one 12 KiB
-//     stage: per plane 64 rows x 64 B, the 16-B units of a row XOR-swizzled by (row >> 2) & 3 so the fragment reads
-//     are conflict-free); four stages, one barrier per k-step: stage s + 2 is converted while stage s is read, so row
-//     block 0's fragments of stage s + 1 are read before the barrier that opens it.  Each A value is converted once.
-//   * MFMA: v_mfma_f32_32x32x16_bf16 with the weight fragment as operand A (32 columns x 16 k) and the A rows'
-//     fragment as operand B; per row block of 32 and k-half the six piece products a0w2, a2w0, a1w1, a0w1, a1w0 into
-//     one accumulator and a0w0 into a second, summed in the epilogue (the b3 kernel's split).  24 MFMAs (32 cycles,
-//     24 of them free for other issue) per wave and k-step against 12 ds_read_b128.
-//   * epilogue after k-step 7: the tile's results (hi + lo, the form's combine / activation) stay in registers and
-//     leave one 16-B store per lane per k-step of the NEXT tile: a tile's 64 KiB of stores issued at once queue in
-//     the store path (~14 B/clk/CU) for thousands of cycles, and every later vmcnt wait (loads and stores count in
-//     one in-order counter) sits behind them (128-row tiles with the stores at the tile end: 2.92 ms, without the
-//     stores 2.36, stores into one L2-resident 1 MB window 2.66; profiles/r05/w4/).
-// Every global load is inline asm with an exact vmcnt at its use, so the loads of the next k-steps stay in flight
-// across the barrier and the tile boundary.
-namespace rw4 {
-constexpr int D = 256, NW = 8, TM = 64, NQ = 8, RB = TM / 32;
-constexpr int PLANE = TM * 64;              // one bf16 plane of a stage: 64 rows x 32 k
-constexpr int STAGE = 3 * PLANE;            // 12 KiB
-constexpr int NB = 4;                       // stages in LDS (stage s + 2 is converted while s is read)
-constexpr int WQ = 6 * 1024;                // weight-plane bytes per (wave, k-step of 32)
-constexpr int WBYTES = NW * NQ * WQ;        // 393,216 B
-static_assert(WBYTES == IDDGCN_BF16X3_PLANES_BYTES, "planes size in the C-ABI");
-}  // namespace rw4
-
-// B (256 x 256, or its transpose) -> the w4 kernel's weight planes: byte ((w*16 + q)*3 + p)*1024 + 16*lane holds
-// plane p of B[k][c] for k = 16q + 8(lane >> 5) + e (e = 0..7), c = 32w + (lane & 31).
-__global__ __launch_bounds__(256) void w4_weight_planes_kernel(const float* __restrict__ B, int b_trans,
-                                                               bf16x8* __restrict__ out) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= rw4::NW * 16 * 64) return;
-    const int lane = t & 63, q = (t >> 6) & 15, w = t >> 10;
-    const int c = 32 * w + (lane & 31);
-    bf16x8 p0, p1, p2;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int k = 16 * q + 8 * (lane >> 5) + e;
-        const float v = b_trans ? B[c * 256 + k] : B[k * 256 + c];
-        __bf16 a, b, d;
-        split3(v, a, b, d);
-        p0[e] = a;
-        p1[e] = b;
-        p2[e] = d;
-    }
-    bf16x8* o = out + ((w * 16 + q) * 3) * 64 + lane;
-    o[0] = p0;
-    o[64] = p1;
-    o[128] = p2;
-}
-
-template <int B_, int E_, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B_ < E_) {
-        f(std::integral_constant<int, B_>{});
-        static_for<B_ + 1, E_>(f);
-    }
-}
-// three fragment reads (planes 0, 1, 2) at a compile-time LDS offset
-template <int OFF>
-__device__ __forceinline__ void w4_ds3(u32x4& a, u32x4& b, u32x4& c, unsigned base) {
-    asm volatile("ds_read_b128 %0, %3 offset:%4\n\tds_read_b128 %1, %3 offset:%5\n\tds_read_b128 %2, %3 offset:%6"
-                 : "=v"(a), "=v"(b), "=v"(c)
-                 : "v"(base), "i"(OFF), "i"(OFF + rw4::PLANE), "i"(OFF + 2 * rw4::PLANE)
-                 : "memory");
-}
-// 16 B per lane from sbase + voff + IMM (global_load_dwordx4, saddr form)
-template <int IMM>
-__device__ __forceinline__ void w4_gload(u32x4& d, unsigned voff, const void* sbase) {
-    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(d) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
-}
-// s_waitcnt vmcnt(N); the registers listed become defined after it (the loads' destinations)
-template <int N>
-__device__ __forceinline__ void w4_vmwait6(u32x4 (&w)[6]) {
-    asm volatile("s_waitcnt vmcnt(%6)"
-                 : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5])
-                 : "i"(N)
-                 : "memory");
-}
-template <int N>
-__device__ __forceinline__ void w4_vmwait1(u32x4& a) {
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a) : "i"(N) : "memory");
-}
-
-template <int NV, bool AUX, bool BC>
-__global__ __launch_bounds__(512) void rowgemm256_w4_kernel(RowGemmP p, const char* __restrict__ wpl) {
-    using namespace rw4;
-    static_assert(NV == 0 && !AUX && !BC, "w4: the plain form");
-    __shared__ __attribute__((aligned(16))) char lds[NB * STAGE];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int i = lane & 31, h = lane >> 5;
-    const long long ntiles = ((long long)p.M + TM - 1) / TM;
-    const long long t_beg = (long long)blockIdx.x * p.tiles_per_block;
-    long long t_end = t_beg + p.tiles_per_block;
-    if (t_end > ntiles) t_end = ntiles;
-    if (t_beg >= t_end) return;
-    const long long M = p.M;
-
-    // this lane's A chunk: row ra of the tile, 16 B at k = 32 q + 4 kc4
-    const int ra = tid >> 3, kc4 = tid & 7;
-    const int wofs = ra * 64 + ((((kc4 >> 1) ^ (ra >> 2)) & 3) << 4) + ((kc4 & 1) << 3);
-    const unsigned lbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
-    // fragment reads: row i, 16-B unit 2u + h (k-half u), swizzled
-    const unsigned roff0 = lbase + i * 64 + (((0 + h) ^ ((i >> 2) & 3)) << 4);
-    const unsigned roff1 = lbase + i * 64 + (((2 + h) ^ ((i >> 2) & 3)) << 4);
-    // weight planes of this wave: + q * WQ + (3 u + p) * 1024 + 16 lane
-    const char* wbase = wpl + (long long)wave * NQ * WQ;
-    const unsigned vw0 = lane * 16, vw1 = lane * 16 + 3 * 1024;
-
-    struct TileA {
-        const float* base;
-        unsigned v;
-    };
-    auto tile_a = [&](long long tt) __attribute__((always_inline)) {
-        TileA a;
-        const long long r0 = tt * TM;
-        const long long last = M - 1 - r0;          // rows past M read row M - 1
-        a.base = p.A + r0 * D;
-        a.v = (unsigned)((ra < last ? ra : last) * 1024 + kc4 * 16);
-        return a;
-    };
-    auto load_a = [&](auto QC, const TileA& a, u32x4& d) __attribute__((always_inline)) {
-        constexpr int Q = decltype(QC)::value;
-        w4_gload<Q * 128>(d, a.v, a.base);
-    };
-    auto load_w = [&](auto QC, u32x4 (&d)[6]) __attribute__((always_inline)) {
-        constexpr int Q = decltype(QC)::value;
-        const char* b = wbase + Q * WQ;
-        w4_gload<0>(d[0], vw0, b);
-        w4_gload<1024>(d[1], vw0, b);
-        w4_gload<2048>(d[2], vw0, b);
-        w4_gload<0>(d[3], vw1, b);
-        w4_gload<1024>(d[4], vw1, b);
-        w4_gload<2048>(d[5], vw1, b);
-    };
-    auto convert = [&](const u32x4& a, int buf) __attribute__((always_inline)) {
-        bf16x4 p0, p1, p2;
-        split3x4(__builtin_bit_cast(f32x4, a), p0, p1, p2);
-        char* d = lds + buf * STAGE + wofs;
-        *reinterpret_cast<bf16x4*>(d) = p0;
-        *reinterpret_cast<bf16x4*>(d + PLANE) = p1;
-        *reinterpret_cast<bf16x4*>(d + 2 * PLANE) = p2;
-    };
-
-    f32x16 hi[RB], lo[RB];
-    f32x4 res[RB * 4];                     // the previous tile's results, one 16-B store per k-step
-    u32x4 wr[2][6], ga[2], fx[2][3];
-    // k-step Q: for k-half u and row block rb, the six piece products (fragments of (u, rb) in fx[(2u + rb) & 1],
-    // the next pair's read issued before this pair's MFMAs; (0, 0) was read before the barrier)
-    auto mfma_stage = [&](auto QC) __attribute__((always_inline)) {
-        constexpr int Q = decltype(QC)::value, S = Q & 1, BUF = Q % NB;
-        static_for<0, 2 * RB>([&](auto XC) __attribute__((always_inline)) {
-            constexpr int x = decltype(XC)::value, u = x / RB, rb = x % RB, F = x & 1;
-            if constexpr (x + 1 < 2 * RB) {
-                constexpr int u1 = (x + 1) / RB, rb1 = (x + 1) % RB;
-                w4_ds3<BUF * STAGE + rb1 * 32 * 64>(fx[F ^ 1][0], fx[F ^ 1][1], fx[F ^ 1][2], u1 ? roff1 : roff0);
-                asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(fx[F][0]), "+v"(fx[F][1]), "+v"(fx[F][2])::"memory");
-            } else {
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fx[F][0]), "+v"(fx[F][1]), "+v"(fx[F][2])::"memory");
-            }
-            const bf16x8 x0 = __builtin_bit_cast(bf16x8, fx[F][0]), x1 = __builtin_bit_cast(bf16x8, fx[F][1]),
-                         x2 = __builtin_bit_cast(bf16x8, fx[F][2]);
-            const bf16x8 w0 = __builtin_bit_cast(bf16x8, wr[S][3 * u]), w1 = __builtin_bit_cast(bf16x8, wr[S][3 * u + 1]),
-                         w2 = __builtin_bit_cast(bf16x8, wr[S][3 * u + 2]);
-            f32x16 l = lo[rb];
-            if constexpr (Q == 0 && u == 0) l = f32x16{};
-            l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x2, l, 0, 0, 0);
-            l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, x0, l, 0, 0, 0);
-            l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, x1, l, 0, 0, 0);
-            l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x1, l, 0, 0, 0);
-            l = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, x0, l, 0, 0, 0);
-            lo[rb] = l;
-            f32x16 hh = hi[rb];
-            if constexpr (Q == 0 && u == 0) hh = f32x16{};
-            hi[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, x0, hh, 0, 0, 0);
-        });
-    };
-    // the finished tile's results (lane l: edge row 32 rb + (l & 31), columns 32 wave + 8 j + 4 (l >> 5) + 0..3 in
-    // accumulator elements 4 j .. 4 j + 3) and their k-step-Q store
-    auto finish = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                res[4 * rb + j] = f32x4{hi[rb][4 * j] + lo[rb][4 * j], hi[rb][4 * j + 1] + lo[rb][4 * j + 1],
-                                        hi[rb][4 * j + 2] + lo[rb][4 * j + 2], hi[rb][4 * j + 3] + lo[rb][4 * j + 3]};
-    };
-    __amdgpu_buffer_rsrc_t rc_prev;
-    auto store = [&](int n) __attribute__((always_inline)) {
-        const int rb = n >> 2, j = n & 3;
-        __builtin_amdgcn_raw_buffer_store_b128(res[n], rc_prev, ((32 * rb + i) * D + 32 * wave + 8 * j + 4 * h) * 4, 0, 0);
-    };
-    auto rsrc = [&](long long tt) __attribute__((always_inline)) {
-        const long long r0 = tt * TM;
-        const long long left = M - r0;
-        const unsigned nbytes = (unsigned)((left < TM ? left : TM) * D * 4);
-        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(p.C) + r0 * D * 4, (short)0, nbytes, 0x00020000);
-    };
-
-    // prologue: A(0), A(1), W(0), A(2); stages 0, 1 converted into buffers 0, 1; fragments (0, 0) of stage 0
-    TileA acur = tile_a(t_beg);
-    TileA anxt = tile_a(t_beg + 1 < t_end ? t_beg + 1 : t_beg);
-    load_a(std::integral_constant<int, 0>{}, acur, ga[0]);
-    load_a(std::integral_constant<int, 1>{}, acur, ga[1]);
-    load_w(std::integral_constant<int, 0>{}, wr[0]);
-    w4_vmwait1<7>(ga[0]);
-    convert(ga[0], 0);
-    load_a(std::integral_constant<int, 2>{}, acur, ga[0]);
-    w4_vmwait1<7>(ga[1]);
-    convert(ga[1], 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    w4_ds3<0>(fx[0][0], fx[0][1], fx[0][2], roff0);
-
-    // iteration (tile tt, k-step Q; stage s): W(Q+1), A(s + 3); wait W(Q); MFMAs of stage s (buffer Q % 4); wait
-    // A(s + 2), convert it into buffer (Q + 2) % 4 (last read in iteration s - 2); fragments (0, 0) of stage s + 1
-    // (complete since the previous barrier); store Q of the previous tile; after the last k-step its results; barrier.
-    // vmcnt at W(Q): the ops issued after it = A(s + 2) (1) + the previous iteration's store (0 or 1) + W(Q+1) (6) +
-    // A(s + 3) (1): vmcnt(8) (with a store, A(s + 2) is waited for too); at A(s + 2): vmcnt(7) (with a store, it is
-    // waited for too).  The waits are unconditional: a wait on either side of a branch lets the compiler copy the
-    // loads' destination registers ahead of it (before the data has landed) to merge the two paths.
-    for (long long tt = t_beg; tt < t_end; ++tt) {
-        const bool have_prev = tt > t_beg;
-        static_for<0, NQ>([&](auto QC) __attribute__((always_inline)) {
-            constexpr int Q = decltype(QC)::value, S = Q & 1;
-            load_w(std::integral_constant<int, (Q + 1) % NQ>{}, wr[S ^ 1]);
-            if constexpr (Q + 3 < NQ) load_a(std::integral_constant<int, Q + 3>{}, acur, ga[S ^ 1]);
-            else load_a(std::integral_constant<int, Q + 3 - NQ>{}, anxt, ga[S ^ 1]);
-            w4_vmwait6<8>(wr[S]);
-            mfma_stage(QC);
-            w4_vmwait1<7>(ga[S]);
-            convert(ga[S], (Q + 2) % NB);
-            w4_ds3<((Q + 1) % NB) * STAGE>(fx[0][0], fx[0][1], fx[0][2], roff0);
-            if (have_prev) store(Q);
-            if constexpr (Q == NQ - 1) finish();
-            asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-        });
-        rc_prev = rsrc(tt);
-        acur = anxt;
-        anxt = tile_a(tt + 2 < t_end ? tt + 2 : tt + 1 < t_end ? tt + 1 : tt);
-    }
-#pragma unroll
-    for (int n = 0; n < RB * 4; ++n) store(n);
-}
-
 // ---- TN reduction GEMM, bf16x3 operands: C = A^T B over M rows, partial per workgroup --------------------
 // Wave w owns output rows 32w..32w+31 (columns of A) x all 256 columns (8 accumulator tiles, 128 VGPRs).
 // 16-row tiles of A and B (one v_mfma_f32_32x32x16_bf16 k-step) arrive by LDS-DMA into 1600-B row slots,
@@ -3828,7 +3571,6 @@ RowGemmP to_p(const iddgcn_rowgemm_t& a) {
     p.V = a.V; p.v_idx = a.v_idx; p.v_rel_stride = a.v_rel_stride; p.v_row_stride = a.v_row_stride;
     p.act = a.act; p.aux = a.aux; p.planes = a.planes; p.precision = a.precision;
     p.tiles_per_block = 1;
-    p.b_planes = static_cast<const char*>(a.b_planes);
     return p;
 }
 // Argument check shared by the f32 row-GEMM entries (0 = fine).  Planes operands (IDDGCN_PLANES_*) need
@@ -3883,21 +3625,6 @@ bool b3_select(const RowGemmP& p, int& nv, bool& aux, bool& bc) {
     nv = 0;
     aux = p.act == IDDGCN_ACT_DSIGMOID || p.accumulate;
     return true;
-}
-// The full-width bf16x3 kernel's forms (rowgemm256_w4_kernel<NV, AUX, BC>): b_planes given and a form of b3_select.
-bool w4_select(const RowGemmP& p, int& nv, bool& aux, bool& bc) {
-    if (!p.b_planes || !b3_select(p, nv, aux, bc)) return false;
-    return nv == 0 && !aux && !bc;
-}
-// one workgroup per CU (every one resident), contiguous 128-row tile ranges
-void launch_w4(hipStream_t st, RowGemmP p, int nv, bool aux, bool bc) {
-    const long long nt = ((long long)p.M + rw4::TM - 1) / rw4::TM;
-    long long nb = nt < 256 ? nt : 256;
-    p.tiles_per_block = (int)((nt + nb - 1) / nb);
-    nb = (nt + p.tiles_per_block - 1) / p.tiles_per_block;
-    const dim3 g((unsigned)nb), blk(512);
-    (void)nv; (void)aux; (void)bc;
-    hipLaunchKernelGGL((rowgemm256_w4_kernel<0, false, false>), g, blk, 0, st, p, p.b_planes);
 }
 // ~128 row ranges (a multiple of 8) x 2 column halves: one workgroup per CU, every one resident
 void launch_b3(hipStream_t st, RowGemmP p, int nv, bool aux, bool bc) {
@@ -4382,10 +4109,6 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     if (p.precision == IDDGCN_GEMM_BF16X3) {
         int nv;
         bool aux, bc;
-        if (a->D == 256 && w4_select(p, nv, aux, bc)) {
-            launch_w4(st, p, nv, aux, bc);
-            return launch_status();
-        }
         if (a->D == 256 && b3_select(p, nv, aux, bc)) {
             launch_b3(st, p, nv, aux, bc);
             return launch_status();
@@ -4420,20 +4143,12 @@ int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* a) {
     return launch_status();
 }
 
-int iddgcn_bf16x3_weight_planes(void* stream, const float* B, int b_trans, void* planes) {
-    if (!B || !planes || (reinterpret_cast<uintptr_t>(planes) & 15)) return IDDGCN_E_BAD_ARG;
-    hipLaunchKernelGGL(w4_weight_planes_kernel, dim3(rw4::NW * 16 * 64 / 256), dim3(256), 0,
-                       (hipStream_t)stream, B, b_trans, static_cast<bf16x8*>(planes));
-    return launch_status();
-}
-
 int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* a) {
     if (!a || !dim_ok(a->D)) return -1;
     RowGemmP p = to_p(*a);
     if (p.precision == IDDGCN_GEMM_BF16X3) {
         int nv;
         bool aux, bc;
-        if (a->D == 256 && w4_select(p, nv, aux, bc)) return 600 + 10 * nv + (aux ? 1 : 0) + (bc ? 2 : 0);
         if (a->D == 256 && b3_select(p, nv, aux, bc)) return 500 + 10 * nv + (aux ? 1 : 0) + (bc ? 2 : 0);
         p.precision = IDDGCN_GEMM_EXACT_F32;
     }

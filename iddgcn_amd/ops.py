@@ -125,14 +125,13 @@ def rowgemm_batched(calls):
 
 def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=None, coef_idx=None, V=None,
                   v_idx=None, v_rel_stride=0, v_row_stride=None, act=L.ACT_NONE, aux=None, M=None, planes=0,
-                  precision="exact", b_planes=None):
+                  precision="exact"):
     """C = epilogue(A[a_idx] · B^(T)) (include/iddgcn.h, iddgcn_rowgemm_f32).  planes: L.PLANES_* flags,
     which of A / C / aux are pre-split planes tables (fp32-shaped tensors holding [hi | lo] fp16 rows;
     D = 256, split GEMM mode).  precision, per call: "exact" (v_mfma_f32_32x32x2_f32, bitwise an fmaf chain),
     "exact4" (the same MFMA, four interleaved accumulation chains: the node-level projections), "bf16x3" (fp32
     operands split exactly into three bf16 pieces, six bf16 MFMA products, fp32 accumulation) or "split"
-    (split-fp16 operands, 22 significant bits); D < 256 runs exact f32 in every mode.  b_planes: B (with this
-    b_trans) pre-split by bf16x3_weight_planes, for the full-width bf16x3 kernel (ABI 10)."""
+    (split-fp16 operands, 22 significant bits); D < 256 runs exact f32 in every mode."""
     D = B.shape[0]
     M = C.shape[0] if M is None else M
     R = 0 if coef is None else coef.shape[-1]
@@ -159,20 +158,7 @@ def _rowgemm_args(A, B, C, *, a_idx=None, b_trans=False, accumulate=False, coef=
         accumulate=int(accumulate), R=R, coef=_ptr(coef), coef_idx=_ptr(coef_idx), V=_ptr(V),
         v_idx=_ptr(v_idx), v_rel_stride=int(v_rel_stride),
         v_row_stride=int(D if v_row_stride is None else v_row_stride), act=int(act), aux=_ptr(aux),
-        planes=int(planes), precision=_prec(precision), b_planes=_ptr(b_planes))
-
-
-def bf16x3_weight_planes(B, b_trans=False, out=None):
-    """B (256 x 256 fp32) split exactly into three bf16 planes in the full-width bf16x3 row GEMM's streaming order
-    (include/iddgcn.h iddgcn_bf16x3_weight_planes): pass the result as rowgemm(..., b_planes=...) with the same
-    b_trans.  out: a uint8 tensor of L.BF16X3_PLANES_BYTES bytes on B's device (allocated when None)."""
-    _req(B, _F32, (256, 256), "B")
-    if out is None:
-        out = torch.empty(L.BF16X3_PLANES_BYTES, dtype=torch.uint8, device=B.device)
-    if out.numel() * out.element_size() < L.BF16X3_PLANES_BYTES or not out.is_contiguous():
-        raise L.IddgcnError("b_planes buffer too small")
-    L.check(L.lib().iddgcn_bf16x3_weight_planes(_stream(), _ptr(B), int(b_trans), _ptr(out)), "bf16x3_weight_planes")
-    return out
+        planes=int(planes), precision=_prec(precision))
 
 
 def tn_blocks(M, D):

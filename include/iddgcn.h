@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 10
+#define IDDGCN_ABI_VERSION 9
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -121,19 +121,8 @@ typedef struct {
     int planes;           /* IDDGCN_PLANES_* flags (ABI 4; 0 = every table fp32).  Nonzero needs D = 256,
                              the split-fp16 mode and no a_idx; invalid combinations return IDDGCN_E_BAD_ARG */
     int precision;        /* IDDGCN_GEMM_EXACT_F32 (0), _SPLIT_F16, _F32_4CHAIN or _BF16X3 (per call) */
-    const void* b_planes; /* ABI 10, IDDGCN_GEMM_BF16X3 only: B (with this b_trans) pre-split by
-                             iddgcn_bf16x3_weight_planes, or NULL.  Given, the forms the full-width kernel
-                             takes run on it (kernel id 600 + ...); the results are bitwise those of the
-                             bf16x3 kernel without planes.  B must still be passed. */
 } iddgcn_rowgemm_t;
 int iddgcn_rowgemm_f32(void* stream, const iddgcn_rowgemm_t* args);
-
-/* ABI 10: B (256 x 256 fp32; B^T when b_trans) split exactly into three bf16 planes, laid out in the order
- * the full-width bf16x3 row GEMM streams them (IDDGCN_BF16X3_PLANES_BYTES bytes at `planes`, 16-B aligned).
- * Computed once per weight (per optimizer step), then passed as iddgcn_rowgemm_t.b_planes to every
- * bf16x3 row GEMM with that B and b_trans. */
-#define IDDGCN_BF16X3_PLANES_BYTES 393216
-int iddgcn_bf16x3_weight_planes(void* stream, const float* B, int b_trans, void* planes);
 
 /* Which kernel iddgcn_rowgemm_f32 would run for these arguments (a test / benchmark hook; nothing is
  * launched): 300 + 10*NV + aux + 2*coef + 8*(broadcast V with R > 2 coefficients) + 1000 for the planes
@@ -141,8 +130,7 @@ int iddgcn_bf16x3_weight_planes(void* stream, const float* B, int b_trans, void*
  * tables: 1, 2, or capacity 4 / 8 for R <= 8, whose LDS slabs keep 7 distinct V rows per 32-row tile
  * and read further ones from L2); 100 for the register-staged kernel (D < 256, and D = 256 forms the v3
  * kernel does not take: a gathered V with the sigma' epilogue, V rows that are not dense); 500 + 10*NV + aux
- * (+ 2 for broadcast V rows) for the bf16x3 row GEMM (IDDGCN_GEMM_BF16X3 forms it takes); 600 + the same for the
- * full-width bf16x3 row GEMM (b_planes given, forms it takes); -1 for an invalid D. */
+ * (+ 2 for broadcast V rows) for the bf16x3 row GEMM (IDDGCN_GEMM_BF16X3 forms it takes); -1 for an invalid D. */
 int iddgcn_rowgemm_kernel_id(const iddgcn_rowgemm_t* args);
 
 /* C[D][D] (+)= A^T · B over M rows (A, B are M x D).  Two stages: each of n_blocks

@@ -54,6 +54,7 @@ def main():
         assert all(np.array_equal(init[f"relw{l}"], ref[f"relw{l}"]) for l in (1, 2, 3))
         model = get_IDDGCN_Model(N_ENT, N_REL, DIM, DIM, 89, None, 0, a.fold, init="tf27")
         model._set_named(init)
+        model._invalidate()
         model.neg_triples = d["X_train_neg"][None]
         model.compile(loss=BinaryCrossentropy(), optimizer=Adam(learning_rate=0.001))
         model.fit(x=x, y=np.ones((1, X.shape[1])), epochs=a.epochs, batch_size=100, verbose=0)

@@ -1,7 +1,6 @@
 """Run one edge-GEMM case a few times at config-3 shape (for rocprofv3 --pmc passes).
 
-usage: python tools/gemm_probe.py {fwd,bwd,plain,tn,fwd8} {split,exact,bf16x3,bf16x3w4} [reps]
-bf16x3w4: bf16x3 with the weight pre-split (b_planes: the full-width kernel where it takes the form)
+usage: python tools/gemm_probe.py {fwd,bwd,plain,tn,fwd8} {split,exact} [reps]
 fwd8: the config-5 form (R = 8 relations, bf16 edge tables, degree 50) at T = 10M, N = 200k
 """
 import sys
@@ -21,28 +20,23 @@ def main(case, mode, reps=3, T=4_000_000, N=100_000, D=256, R=2):
     A = torch.rand(T, D, device=dev, generator=g)
     S = torch.randn(D, D, device=dev, generator=g)
     C = torch.empty(T, D, device=dev)
-    kw = {}
-    if mode == "bf16x3w4":
-        mode = "bf16x3"
-        kw = dict(b_planes=ops.bf16x3_weight_planes(S, case == "bwd"))
     if case == "fwd8":
         A = A.bfloat16()
         C = C.bfloat16()
         W = torch.rand(T, R, device=dev, generator=g)
         P = torch.randn(R, N, D, device=dev, generator=g)
         t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
-        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID, precision=mode, **kw)  # noqa
+        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID, precision=mode)  # noqa
     elif case == "fwd":
         W = torch.rand(T, R, device=dev, generator=g)
         P = torch.randn(R, N, D, device=dev, generator=g)
         t = torch.sort(torch.randint(0, N, (T,), device=dev, generator=g)).values.int()
-        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID, precision=mode,
-                                 **kw)  # noqa
+        fn = lambda: ops.rowgemm(A, S, C, coef=W, V=P, v_idx=t, v_rel_stride=N * D, act=L.ACT_SIGMOID, precision=mode)  # noqa
     elif case == "bwd":
         aux = torch.rand(T, D, device=dev, generator=g)
-        fn = lambda: ops.rowgemm(A, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux, precision=mode, **kw)  # noqa
+        fn = lambda: ops.rowgemm(A, S, C, b_trans=True, act=L.ACT_DSIGMOID, aux=aux, precision=mode)  # noqa
     elif case == "plain":
-        fn = lambda: ops.rowgemm(A, S, C, precision=mode, **kw)  # noqa
+        fn = lambda: ops.rowgemm(A, S, C, precision=mode)  # noqa
     else:
         B = torch.randn(T, D, device=dev, generator=g)
         slab = torch.empty(ops.tn_blocks(T, D) * D * D, device=dev)
