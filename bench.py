@@ -50,9 +50,15 @@ GEMM_NOTE = {
 }
 # the arithmetic the path computes in, per GEMM mode (the bench line's "dtype")
 DTYPE = {"split": "f32 (D=256 GEMMs on split-fp16x2 operands, fp32 accumulate)", "exact": "f32", "bf16x3": "f32"}
-DTYPE_BF16 = ("bf16 edge tables (x^l, do^l) with bf16 MFMA for the edge GEMMs (weights as bf16 hi+lo), fp32 node "
-              "tables, accumulation and epilogues, node-level GEMMs on split-fp16 operands (perf-only mode, BASELINE "
-              "config 5)")
+DTYPE_BF16 = {
+    "hilo": ("bf16 edge tables (x^l, do^l) with bf16 MFMA for the edge GEMMs (weights as bf16 hi+lo), fp32 node "
+             "tables, accumulation and epilogues, node-level GEMMs on split-fp16 operands (perf-only mode, BASELINE "
+             "config 5)"),
+    "bf16": ("bf16 edge tables (x^l, do^l) with bf16 x bf16 MFMA for the edge GEMMs (every edge-GEMM operand rounded "
+             "to bf16 once: weights, and the R = 8 combine's node rows and coefficients; include/iddgcn.h "
+             "IDDGCN_GEMM_BF16), fp32 node tables, accumulation and epilogues, node-level GEMMs on split-fp16 "
+             "operands (perf-only mode, BASELINE config 5: 'bf16 features with MFMA XW')"),
+}
 
 CONFIGS = {
     2: dict(name="synthetic-fold0-shape", N=845, R=4, M=37_510, D=64, scaling="weak"),
@@ -60,7 +66,7 @@ CONFIGS = {
     4: dict(name="synthetic-4", N=1_000_000, R=2, M=20_000_000, D=256, scaling="strong"),
     # 40M positives, 10M negatives (one per 4 positives), generated on the device
     5: dict(name="synthetic-5", N=1_000_000, R=8, M=40_000_000, D=256, scaling="strong", neg_every=4,
-            features="bf16", gemm="split"),
+            features="bf16", gemm="split", edge_mfma="bf16"),
 }
 
 
@@ -88,7 +94,7 @@ def launch_ranks(args):
     return None
 
 
-def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4):
+def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4, edge_mfma="hilo"):
     """Roofline of one edge-level GEMM launch.
 
     flops: 2*D^2*T algorithmic (x3 f16 MFMA instructions on the f16 peak in split mode, x6 bf16 ones in bf16x3);
@@ -96,14 +102,15 @@ def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4):
     distinct P_r rows (R*N*D once); bwd reads do and the sigma' operand x, writes do' (the layer-2 bwd,
     "rec", rebuilds x^1 from the distinct ES1 / P^1 rows and W^1[h_e] instead of reading it); dS reads
     x and do (eb = bytes per edge-table element: 4, or 2 in the bf16-feature mode, whose GEMMs run 2 bf16
-    MFMAs per k-step).  bound = whichever roofline time is larger."""
+    MFMAs per k-step with hi + lo weights, 1 with bf16 weights: edge_mfma).  bound = whichever roofline time is
+    larger."""
     flops = 2.0 * D * D * T
     nbytes = {"tail_fwd_gemm": 2.0 * eb * D * T + 4.0 * R * T + 4.0 * T + 4.0 * R * N * D,
               "tail_bwd_gemm": 3.0 * eb * D * T,
               "tail_bwd_rec_gemm": 2.0 * eb * D * T + 4.0 * R * T + 4.0 * T + 4.0 * (R + 1) * N * D,
               "tail_dS_tn": 2.0 * eb * D * T}[name]
     if eb == 2:
-        hw_flops, peak_f = 2 * flops, MFMA_F16_PEAK_TFLOPS
+        hw_flops, peak_f = (1 if edge_mfma == "bf16" else 2) * flops, MFMA_F16_PEAK_TFLOPS
     elif gemm == "bf16x3":
         hw_flops, peak_f = 6 * flops, MFMA_F16_PEAK_TFLOPS
     elif gemm == "split":
@@ -290,7 +297,7 @@ def cpu_baseline(cfg, frac=0.05, min_steps=3, budget_s=60.0):
                        f"{os.cpu_count()}-CPU host ({cpu_model()})")}
 
 
-def step_roofline(N, R, D, T, M, gemm, features, ms_per_step):
+def step_roofline(N, R, D, T, M, gemm, features, ms_per_step, edge_mfma="hilo"):
     """Whole-step roofline (T_roof = W_gemm / P_mfma + Q_hbm / BW, fraction =
     T_roof / T_measured), for one rank's step.  Two forms: the BASELINE formula as written (W_gemm on the f32 MFMA
     peak), and the same work on the peak of the MFMAs this mode issues (bf16x3: 6 bf16 products per fp32 product on
@@ -303,7 +310,7 @@ def step_roofline(N, R, D, T, M, gemm, features, ms_per_step):
     hw, peak = {"exact": (1, MFMA_F32_PEAK_TFLOPS), "split": (3, MFMA_F16_PEAK_TFLOPS),
                 "bf16x3": (6, MFMA_F16_PEAK_TFLOPS)}[gemm]
     if features == "bf16":
-        hw, peak = 2, MFMA_F16_PEAK_TFLOPS
+        hw, peak = (1 if edge_mfma == "bf16" else 2), MFMA_F16_PEAK_TFLOPS
     t_hbm = Q / (HBM_PEAK_GBS * 1e9) * 1e3
     t_f32 = W / (MFMA_F32_PEAK_TFLOPS * 1e12) * 1e3
     t_mode = hw * W / (peak * 1e12) * 1e3
@@ -373,7 +380,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         lab = np.concatenate([np.ones(max(0, min(hi, npos) - lo), np.float32),
                               np.zeros(max(0, hi - max(lo, npos)), np.float32)])
     feat = args.features or cfg.get("features", "f32")
-    eng = Engine(N, R, D, dev, gemm=gemm, features=feat, planes=not args.no_planes)
+    emfma = cfg.get("edge_mfma", "hilo") if feat == "bf16" else "hilo"
+    eng = Engine(N, R, D, dev, gemm=gemm, features=feat, planes=not args.no_planes, edge_mfma=emfma)
     eng.overlap = args.overlap
     adj = get_adj_mats(pos, N, R, device=dev)            # device graph build (bit-identical to the host's)
     ed = eng.edges(tri, lab)
@@ -389,9 +397,10 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     elif shard == "spmm" and world > 1:
         eng.spmm_shard = RelationShard(R, N)     # row-partitioned SpMMs, node GEMMs replicated
 
-    def timed_run(mode, probe):
+    def timed_run(mode, probe, edge_mfma=emfma):
         """W warm-up steps, then K timed steps between barriers + synchronize; max over ranks."""
         eng.gemm = mode
+        eng.edge_mfma = edge_mfma
         P.load(init)                       # every mode starts from the same parameters
         opt = KerasAdam(P)
         for _ in range(warmup):
@@ -420,17 +429,18 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     elapsed, loss_val, probe = timed_run(gemm, probe_kernels)
     consist = rank_consistency(P.buf) if world > 1 else None
     out = {"value": M / (elapsed / steps), "ms_per_step": elapsed / steps * 1e3,
-           "scaling": cfg["scaling"], "dtype": DTYPE_BF16 if feat == "bf16" else DTYPE[gemm],
-           "gemm_operands": GEMM_NOTE[gemm] + ("; edge GEMMs bf16 (features=bf16)" if feat == "bf16" else ""),
+           "scaling": cfg["scaling"], "dtype": DTYPE_BF16[emfma] if feat == "bf16" else DTYPE[gemm],
+           "gemm_operands": GEMM_NOTE[gemm] + (f"; edge GEMMs on bf16 edge tables, edge_mfma={emfma}"
+                                               if feat == "bf16" else ""),
            "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
                       "scored_edges": T, "scored_edges_per_gpu": ed.T, "feat_dim": D,
                       "parallelism": (f"node-rows{world}" if eng.row_shard else f"edge-dp{world}")
                       + ("+relation-sharded-nodes" if eng.node_shard else "")
                       + ("+row-partitioned-spmm" if eng.spmm_shard else ""),
-                      "gemm": gemm, "features": feat},
+                      "gemm": gemm, "features": feat, **({"edge_mfma": emfma} if feat == "bf16" else {})},
            "scored_edges_per_s": T / (elapsed / steps), "loss": loss_val, "steps": steps, "warmup": warmup,
            "step_roofline": step_roofline(N, R, D, ed.T, M, gemm, feat,
-                                          elapsed / steps * 1e3)}
+                                          elapsed / steps * 1e3, edge_mfma=emfma)}
     if world > 1:
         out["ranks_consistent"] = consist == 0.0
         out["params_max_abs_diff_vs_rank0"] = consist
@@ -446,12 +456,19 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         el2, loss2, _ = timed_run(mode2, False)
         out["other_gemm_mode"] = {"gemm": mode2, "dtype": DTYPE[mode2], "value": M / (el2 / steps),
                                   "ms_per_step": el2 / steps * 1e3, "loss": loss2}
+    if other_mode and feat == "bf16":
+        # the other operand form of the bf16 edge GEMMs on the same engine and inputs: weights as bf16 hi + lo
+        em2 = "hilo" if emfma == "bf16" else "bf16"
+        el2, loss2, _ = timed_run(gemm, False, edge_mfma=em2)
+        out["other_edge_mfma"] = {"edge_mfma": em2, "dtype": DTYPE_BF16[em2], "value": M / (el2 / steps),
+                                  "ms_per_step": el2 / steps * 1e3, "loss": loss2}
     if probe:
         # dominant kernel: largest total event time inside the timed steps; its roofline is the larger
         # of the MFMA time (hardware MFMA work on the mode's peak) and the HBM time (algorithmic bytes)
         kt = {k: [a.elapsed_time(b) for a, b in v] for k, v in probe.items()}
         dom = max(kt, key=lambda k: sum(kt[k]))
-        rl = kernel_roofline(dom, N, R, D, ed.T, gemm, statistics.mean(kt[dom]), eb=2 if feat == "bf16" else 4)
+        rl = kernel_roofline(dom, N, R, D, ed.T, gemm, statistics.mean(kt[dom]), eb=2 if feat == "bf16" else 4,
+                             edge_mfma=emfma)
         rl["traffic"], rl["traffic_source"] = pmc_traffic(dom, gemm, cfg["name"], world)
         rl["box_stream_GBs"] = stream_probe(torch, dev, ed.T, D)
         out["kernel_ms_per_step"] = {k: sum(v) / steps for k, v in kt.items()}
@@ -564,7 +581,9 @@ def main():
                                      steps=min(args.steps, 5), warmup=1))
             continue
         try:
-            o = run_workload(cid, args, world, rank, dev, args.gemm, False, shard=shard,
+            # config 5 (bf16 edge tables) also times the edge GEMMs' other operand form on the same engine
+            o = run_workload(cid, args, world, rank, dev, args.gemm,
+                             CONFIGS[cid].get("features") == "bf16" and not args.no_other_mode, shard=shard,
                              steps=min(args.steps, 5), warmup=1)
         except torch.OutOfMemoryError as e:      # one process: a secondary workload never costs the headline line
             torch.cuda.empty_cache()

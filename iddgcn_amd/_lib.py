@@ -12,11 +12,11 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 9
+ABI_VERSION = 10
 ROWGEMM_BATCH = 25          # IDDGCN_ROWGEMM_BATCH: entries per iddgcn_rowgemm_batched_f32 call
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
-GEMM_EXACT_F32, GEMM_SPLIT_F16, GEMM_F32_4CHAIN, GEMM_BF16X3 = 0, 1, 2, 3
+GEMM_EXACT_F32, GEMM_SPLIT_F16, GEMM_F32_4CHAIN, GEMM_BF16X3, GEMM_BF16 = 0, 1, 2, 3, 4
 PLANES_A, PLANES_C, PLANES_AUX = 1, 2, 4          # iddgcn_rowgemm_t.planes (pre-split edge tables, ABI 4)
 
 vp = ctypes.c_void_p

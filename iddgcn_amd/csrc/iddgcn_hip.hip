@@ -556,7 +556,8 @@ __device__ __forceinline__ float wave_max(float v) {             // max over the
 // PL (split mode): the planes form (IDDGCN_PLANES_*) of the variant: AUX kernels read the sigma' operand
 // as planes rows, gathered-combine kernels (NV = 1, 2) write C as planes rows.
 // (A planes rows are a run-time flag of every X3 kernel: convert_rows just skips.)
-template <int NV, bool AUX, bool HAS_COEF, bool X3, bool CW = false, bool BF = false, bool PL = false, bool C4 = false>
+template <int NV, bool AUX, bool HAS_COEF, bool X3, bool CW = false, bool BF = false, bool PL = false, bool C4 = false,
+          bool W1 = false>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     using namespace r3;
     // A row pitch: bf16 rows (BF) need 512 B of the 1040-B fp32 row; a 528-B pitch keeps the same bank
@@ -568,6 +569,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
                   "PL: split-mode sigma' backward or R <= 2 gathered forward");
     static_assert(!BF || X3, "BF: the 16-bit A-plane pipeline");
     static_assert(!C4 || (!X3 && NV == 0 && !AUX && !HAS_COEF), "C4: the f32 plain form (node projections)");
+    static_assert(!W1 || BF, "W1: bf16 weights, bf16-feature calls only");
     static_assert(NV <= 2 || NV == 4 || NV == 8, "gathered V: 1, 2 tables, or capacity 4 / 8");
     constexpr bool WIDE = NV > 2;                      // capped slabs, run-time R <= NV
     // capped V slabs r >= 1 (rows past the cap read from L2): WIDE
@@ -1073,7 +1075,7 @@ _Pragma("unroll") \
                     if (q + 1 < D / 16) ah[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + 8 * (q + 1))); \
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, bhi[q]), \
                                                                   __builtin_bit_cast(bf16x8, ah[cu]), acc, 0, 0, 0); \
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, blo[q]), \
+                    if constexpr (!W1) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, blo[q]), \
                                                                   __builtin_bit_cast(bf16x8, ah[cu]), acc, 0, 0, 0); \
                     __builtin_amdgcn_sched_barrier(0); \
                 } \
@@ -3664,7 +3666,12 @@ void launch_v3(hipStream_t st, RowGemmBatch& pb, int n, const V3Sel& sel, bool b
     if (nbmax == 0) return;
     const dim3 g((unsigned)nbmax, (unsigned)n), blk(512);
     if (bf) {      // bf16 edge tables: gathered-combine forward, sigma' backward, plain
-#define V3B(NV, AUX, HC) hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, false, true>), g, blk, 0, st, pb)
+#define V3B(NV, AUX, HC)                                                                                         \
+    do {                                                                                                          \
+        if (pb.p[0].precision == IDDGCN_GEMM_BF16)                                                                \
+            hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, false, true, false, false, true>), g, blk, 0, st, pb); \
+        else hipLaunchKernelGGL((rowgemm256_v3_kernel<NV, AUX, HC, true, false, true>), g, blk, 0, st, pb);        \
+    } while (0)
         if (sel.nv == 1) V3B(1, false, true);
         else if (sel.nv == 2) V3B(2, false, true);
         else if (sel.nv == 4) V3B(4, false, true);
@@ -3779,6 +3786,7 @@ constexpr int LDSB = NBUF * ABUF + NW * WREG;            // 156,672 B
 static_assert(LDSB <= 160 * 1024, "LDS budget");
 }  // namespace fg8
 
+template <bool HL>
 __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     using namespace fg8;
     __shared__ __attribute__((aligned(16))) char lds[LDSB];
@@ -3810,7 +3818,7 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     auto clampe = [&](long long e) __attribute__((always_inline)) { return e > Mlast ? Mlast : e; };
 
     // weights: lane (g, i16), column block cb, k-step q: S[32q + 8g + j][c0 + 16cb + i16], j < 8, as bf16 hi + lo
-    bf16x8 wh[2][8], wl[2][8];
+    bf16x8 wh[2][8], wl[2][HL ? 8 : 1];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -3820,7 +3828,7 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
                 const float w = p.B[(32 * q + 8 * g + j) * D + c0 + 16 * cb + i16];
                 const __bf16 hi = (__bf16)w;
                 wh[cb][q][j] = hi;
-                wl[cb][q][j] = (__bf16)(w - (float)hi);
+                if constexpr (HL) wl[cb][q][j] = (__bf16)(w - (float)hi);
             }
 
     // vector-memory ops this wave has issued (wave-uniform): a wait for "op k and everything older" is
@@ -3910,7 +3918,7 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
                     const float x = s < u ? vp[32 * j] : 0.f;
                     const __bf16 hi = (__bf16)x;
                     vh[cb][j] = hi;
-                    vl[cb][j] = (__bf16)(x - (float)hi);
+                    if constexpr (HL) vl[cb][j] = (__bf16)(x - (float)hi);
                 }
             }
 #pragma unroll
@@ -3924,13 +3932,15 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
                     const float x = slot[rb] == s ? (j < 4 ? lo4[j] : hi4[j - 4]) : 0.f;
                     const __bf16 hi = (__bf16)x;
                     ch[j] = hi;
-                    cl[j] = (__bf16)(x - (float)hi);
+                    if constexpr (HL) cl[j] = (__bf16)(x - (float)hi);
                 }
 #pragma unroll
                 for (int cb = 0; cb < 2; ++cb) {
                     accP[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], ch, accP[rb][cb], 0, 0, 0);
-                    accP[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], cl, accP[rb][cb], 0, 0, 0);
-                    accP[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl[cb], ch, accP[rb][cb], 0, 0, 0);
+                    if constexpr (HL) {
+                        accP[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh[cb], cl, accP[rb][cb], 0, 0, 0);
+                        accP[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl[cb], ch, accP[rb][cb], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -3980,7 +3990,7 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
 #pragma unroll
                 for (int rb = 0; rb < 4; ++rb) {
                     acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[cb][q], x[cu][rb], acc[rb][cb], 0, 0, 0);
-                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[cb][q], x[cu][rb], acc[rb][cb], 0, 0, 0);
+                    if constexpr (HL) acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[cb][q], x[cu][rb], acc[rb][cb], 0, 0, 0);
                 }
             // the previous tile's block q: its VALU and store issue in the shadow of this k-step's MFMAs
             if (tprev >= 0) finish(tprev, q);
@@ -4034,7 +4044,8 @@ void launch_fwd_gather8(hipStream_t st, RowGemmP p) {
     long long nb = ntiles < 256 ? ntiles : 256;
     p.tiles_per_block = (int)((ntiles + nb - 1) / nb);
     nb = (ntiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    hipLaunchKernelGGL(fwd_gather8_bf16_kernel, dim3((unsigned)nb), dim3(512), 0, st, p);
+    if (p.precision == IDDGCN_GEMM_BF16) hipLaunchKernelGGL(fwd_gather8_bf16_kernel<false>, dim3((unsigned)nb), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL(fwd_gather8_bf16_kernel<true>, dim3((unsigned)nb), dim3(512), 0, st, p);
 }
 
 // the config-5 tail reduction on MFMAs (tail_seg_mfma8_kernel), with or without the head chain's node terms

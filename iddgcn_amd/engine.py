@@ -272,7 +272,8 @@ class Engine:
     opt-in faster mode.  Other widths and all non-GEMM kernels are exact f32 in every mode.
     """
 
-    def __init__(self, num_entities, num_relations, dim, device=None, gemm="exact", features="f32", planes=True):
+    def __init__(self, num_entities, num_relations, dim, device=None, gemm="exact", features="f32", planes=True,
+                 edge_mfma="hilo"):
         if dim not in (32, 64, 128, 256):
             raise L.IddgcnError("embedding dim must be one of 32, 64, 128, 256")
         if features not in ("f32", "bf16"):
@@ -283,6 +284,15 @@ class Engine:
         # the edge GEMMs on bf16 MFMA; node tables, weights, accumulation and epilogues stay fp32
         self.features = features
         self.edge_dtype = torch.bfloat16 if features == "bf16" else torch.float32
+        # operands of the bf16 edge GEMMs (include/iddgcn.h IDDGCN_GEMM_BF16): "hilo" keeps the weights (and the R = 8
+        # combine's node rows / coefficients) as a bf16 hi + lo pair, 16 significant bits, so the edge tables' bf16
+        # storage is the only rounding beyond fp32; "bf16" rounds every MFMA operand to bf16 once (one product per
+        # term, fp32 accumulation: config 5's "bf16 features with MFMA XW" as autocast runs it)
+        if edge_mfma not in ("hilo", "bf16"):
+            raise L.IddgcnError("edge_mfma must be 'hilo' or 'bf16'")
+        if edge_mfma == "bf16" and features != "bf16":
+            raise L.IddgcnError("edge_mfma='bf16' needs features='bf16' (bf16 edge tables)")
+        self.edge_mfma = edge_mfma
         if not 1 <= num_relations <= 8:
             raise L.IddgcnError("num_relations must be in [1, 8]")
         if gemm not in GEMM_MODES:
@@ -349,6 +359,12 @@ class Engine:
         if mode is not None and mode not in PROJ_MODES:
             raise L.IddgcnError(f"proj_gemm must be None or one of {sorted(PROJ_MODES)}")
         self._proj_gemm = mode
+
+    @property
+    def edge_gemm(self):
+        """Precision of the edge-level row GEMMs (the tail chain's forward and sigma' backward): "bf16" with
+        edge_mfma="bf16" (bf16 edge tables), else ``row_gemm``."""
+        return "bf16" if self.edge_mfma == "bf16" else self.row_gemm
 
     @property
     def use_planes(self):
@@ -460,7 +476,7 @@ class Engine:
             with self._mark("tail_fwd_gemm"):
                 ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID,
-                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, **pr)
+                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, precision=self.edge_gemm)
         # DistMult (+ BCE and backward seed when training)
         if train:
             # one pass over head segments: p / loss / drel partials, the tail seed do^3 (per edge)
@@ -526,7 +542,7 @@ class Engine:
                     ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)
                 with self._mark("tail_bwd_gemm"):
                     ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
-                                planes=L.PLANES_AUX if pl else 0, **pr)
+                                planes=L.PLANES_AUX if pl else 0, precision=self.edge_gemm)
             if side is not None:
                 torch.cuda.current_stream().wait_stream(side)
             # head side (node level)
@@ -650,7 +666,7 @@ class Engine:
             with self._mark("tail_fwd_gemm"):
                 ops.rowgemm(ws.xt[l - 1], P[f"S{l + 1}"], ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID,
-                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, **pr)
+                            planes=(L.PLANES_A | (L.PLANES_C if l == 1 else 0)) if pl else 0, precision=self.edge_gemm)
         x3.wait()
         if train:
             scale, bce = self._dm_seed(T)
@@ -700,7 +716,7 @@ class Engine:
                     ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)
                 with self._mark("tail_bwd_gemm"):
                     ops.rowgemm(do, Sl, ws.xt[l - 1], b_trans=True, act=L.ACT_DSIGMOID, aux=ws.xt[l - 1],
-                                planes=L.PLANES_AUX if pl else 0, **pr)
+                                planes=L.PLANES_AUX if pl else 0, precision=self.edge_gemm)
             seeds.wait()
             ops.head_wsum(ed.hptr, ed.hperm, ws.dWedge, ws.ep)
             sh.reduce_scatter(ws.ep)             # dWedge head sums -> the heads' owners

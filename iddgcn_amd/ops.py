@@ -25,17 +25,18 @@ def _ptr(t):
 
 
 _PRECISION = {"exact": L.GEMM_EXACT_F32, "split": L.GEMM_SPLIT_F16, "exact4": L.GEMM_F32_4CHAIN,
-              "bf16x3": L.GEMM_BF16X3,
+              "bf16x3": L.GEMM_BF16X3, "bf16": L.GEMM_BF16,
               L.GEMM_EXACT_F32: L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16: L.GEMM_SPLIT_F16,
-              L.GEMM_F32_4CHAIN: L.GEMM_F32_4CHAIN, L.GEMM_BF16X3: L.GEMM_BF16X3}
+              L.GEMM_F32_4CHAIN: L.GEMM_F32_4CHAIN, L.GEMM_BF16X3: L.GEMM_BF16X3, L.GEMM_BF16: L.GEMM_BF16}
 
 
 def _prec(precision):
     """GEMM operand precision of one call (include/iddgcn.h IDDGCN_GEMM_*): "exact" / "split" / "exact4" (f32
     MFMA with four interleaved accumulation chains: row GEMMs, plain form at D = 256) / "bf16x3" (every fp32
-    operand split exactly into three bf16 pieces, six bf16 MFMA products, fp32 accumulation) or the constant."""
+    operand split exactly into three bf16 pieces, six bf16 MFMA products, fp32 accumulation) / "bf16" (bf16 edge
+    tables only: every MFMA operand rounded to bf16, one product per term) or the constant."""
     if precision not in _PRECISION:
-        raise L.IddgcnError(f"precision must be 'exact', 'split', 'exact4' or 'bf16x3', got {precision!r}")
+        raise L.IddgcnError(f"precision must be 'exact', 'split', 'exact4', 'bf16x3' or 'bf16', got {precision!r}")
     return _PRECISION[precision]
 
 
@@ -168,8 +169,8 @@ def tn_blocks(M, D):
 def _tn_prec(precision):
     """Operand precision of a TN GEMM: "exact", "bf16x3" or "split" (include/iddgcn.h; the TN kernels take no
     four-chain form, so "exact4" is refused here rather than by the C side's IDDGCN_E_BAD_ARG)."""
-    if precision == "exact4":
-        raise L.IddgcnError("gemm_tn: precision 'exact4' is a row-GEMM form; use 'exact', 'bf16x3' or 'split'")
+    if precision in ("exact4", "bf16", L.GEMM_F32_4CHAIN, L.GEMM_BF16):
+        raise L.IddgcnError(f"gemm_tn: precision {precision!r} is a row-GEMM form; use 'exact', 'bf16x3' or 'split'")
     return _prec(precision)
 
 

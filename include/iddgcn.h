@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 9
+#define IDDGCN_ABI_VERSION 10
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -60,11 +60,19 @@ extern "C" {
  *     Row GEMMs: the plain form, C += A B (accumulate with act none), the gathered-combine forward with
  *     R = 1 or 2 per-edge coefficients (no coef_idx), broadcast V rows (v_row_stride 0, R <= 2, plain or
  *     sigma') and the sigma' backward, without a_idx / planes; every other form takes the exact f32 kernel.  TN GEMMs: D = 256.  Deterministic; not bitwise equal to the exact mode.
+ *   IDDGCN_GEMM_BF16 (ABI 10; iddgcn_rowgemm_bf16 only, i.e. bf16 edge tables): every MFMA operand rounded to
+ *     bf16 once (RNE) — the weights, and in the R = 8 gathered forward also the node rows and per-edge
+ *     coefficients of the combine — one bf16 x bf16 product per term, fp32 accumulation and epilogue
+ *     (BASELINE config 5's "bf16 features with MFMA XW", as autocast would run it).  With bf16 A rows the
+ *     weight's own rounding (2^-9 relative) is the size of the A rounding and of the output's bf16 store;
+ *     any other precision on a bf16 call keeps the weights (and combine operands) as a bf16 hi + lo pair
+ *     (16 significant bits).  iddgcn_rowgemm_f32 rejects it (IDDGCN_E_BAD_ARG).
  * Row GEMMs for D < 256 and every other kernel compute in exact f32 (or F32_4CHAIN where asked). */
 #define IDDGCN_GEMM_EXACT_F32 0
 #define IDDGCN_GEMM_SPLIT_F16 1
 #define IDDGCN_GEMM_F32_4CHAIN 2
 #define IDDGCN_GEMM_BF16X3 3
+#define IDDGCN_GEMM_BF16 4
 
 /* Pre-split edge tables ("planes", ABI 4; D = 256, split-fp16 GEMM mode only).  A row of values in
  * [0, 1] (sigmoid outputs) stored as 8 column blocks of 128 B, block b = [hi f16 of columns 32b..32b+31 |
@@ -297,7 +305,8 @@ int iddgcn_step_advance(void* stream, int* step, float* loss_history, const floa
  * The edge tables x^1..x^3 and the edge-level gradients do^l are stored as bf16 (512-B rows at D = 256,
  * passed as void*); node tables, weights, coefficients, accumulation and every epilogue stay fp32.
  * GEMMs multiply bf16 edge rows by the weights as a bf16 hi + lo pair (two v_mfma_f32_32x32x16_bf16 per
- * k-step), so the only rounding beyond fp32 is the bf16 storage of the edge tables.  D = 256 only. */
+ * k-step), so the only rounding beyond fp32 is the bf16 storage of the edge tables; with precision
+ * IDDGCN_GEMM_BF16 (ABI 10) the weights are bf16 too (one product per k-step).  D = 256 only. */
 
 /* iddgcn_rowgemm_f32 with A, aux and C bf16: the edge forward (gathered V, R <= 8, coefficients per row),
  * the sigma' backward (act DSIGMOID with aux) and plain forms; no accumulate, no broadcast V. */

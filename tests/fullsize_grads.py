@@ -62,13 +62,17 @@ def local_oracle(params, pos, tri_s, lab_s, N, R, dtype):
 
 
 def engine_grads(eng, P, adj, tri_s, lab_s, gemm, cuda):
-    """The engine's loss_and_grads on the sampled scored edges with the FULL device adjacency."""
-    eng.gemm = gemm
+    """The engine's loss_and_grads on the sampled scored edges with the FULL device adjacency.  ``gemm``: the
+    engine's GEMM mode, optionally "/bf16" for bf16 edge-GEMM operands (Engine.edge_mfma, bf16 edge tables)."""
+    mode, _, em = gemm.partition("/")
+    eng.gemm = mode
+    eng.edge_mfma = em or "hilo"
     ed = eng.edges(tri_s, lab_s)
     G = FlatParams(eng.N, eng.R, eng.D, cuda)
     loss_sum, p = eng.loss_and_grads(P, G, adj, ed)
     out = (float(loss_sum.item()) / len(tri_s), p.cpu().numpy(), G.to_numpy())
     del G, ed
+    eng.edge_mfma = "hilo"
     eng.release()
     return out
 

@@ -4,7 +4,9 @@ accumulation and fp32 epilogues.
 
 Kernel bars: each bf16 kernel against an fp64 torch reference of the same op evaluated on the SAME
 bf16-rounded inputs — the only extra error allowed is the bf16 rounding of the output (2^-8 relative)
-and the bf16 hi+lo representation of the weights (2^-16 relative): outputs within 6e-3 of max|ref|
+and the bf16 hi+lo representation of the weights (2^-16 relative; with IDDGCN_GEMM_BF16 the reference takes the
+weights, and in the R = 8 forward the combine's node rows and coefficients, rounded to bf16 as the kernel does, so
+the same bars hold): outputs within 6e-3 of max|ref|
 for bf16-stored results, 1e-5 for fp32 results (TN partials, dP, logits of exact bf16 inputs).
 Model bar: a bf16-mode training step against the fp32 engine on the same inputs — loss within 2e-2 relative,
 probabilities within 2e-2, every gradient within 5e-2 of its max|g| (plus a floor of 1e-6 of the step's largest
@@ -37,8 +39,9 @@ def tails(M, N, g):
     return torch.repeat_interleave(torch.arange(N), lengths)[:M]
 
 
+@pytest.mark.parametrize("precision", ["exact", "bf16"])
 @pytest.mark.parametrize("R", [1, 2, 8])
-def test_rowgemm_bf16_forward_combine(R, cuda):
+def test_rowgemm_bf16_forward_combine(R, precision, cuda):
     g = torch.Generator().manual_seed(R)
     N, M = 3000, 40_007
     A = bf(torch.rand(M, D, generator=g)).to(cuda)
@@ -48,17 +51,26 @@ def test_rowgemm_bf16_forward_combine(R, cuda):
     t = tails(M, N, g).to(cuda)
     ref = torch.sigmoid(A.double() @ S + sum(W[:, r:r + 1] * P[r][t] for r in range(R)))
     C = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
-    ops.rowgemm(A, S.float(), C, coef=W.float(), V=P.float(), v_idx=t.int(), v_rel_stride=N * D, act=L.ACT_SIGMOID)
+    ops.rowgemm(A, S.float(), C, coef=W.float(), V=P.float(), v_idx=t.int(), v_rel_stride=N * D, act=L.ACT_SIGMOID,
+                precision=precision)
     assert maxrel(C, ref) <= 6e-3
 
 
+def rb(x):
+    """x rounded to bf16 (RNE), as float64: an operand of the IDDGCN_GEMM_BF16 form."""
+    return x.float().to(torch.bfloat16).double()
+
+
+@pytest.mark.parametrize("precision", ["exact", "bf16"])
 @pytest.mark.parametrize("case", ["sorted", "short_runs", "unsorted", "tiny", "one_tile", "linear"])
-def test_fwd_gather8_bf16(case, cuda):
+def test_fwd_gather8_bf16(case, precision, cuda):
     """The R = 8 forward of the bf16-feature mode (fwd_gather8_bf16_kernel: x S and the gathered combine both on
     bf16 MFMAs, the tile's distinct V rows as the combine's k axis): element-wise within the bf16 rounding of the
     output (2^-8 relative) plus 1e-5 of max|ref| of the fp64 reference on the same bf16 inputs.  Tails sorted with
     runs of 4-60 and of 1-3 edges (up to 32 distinct V rows per tile), unsorted (the slots past the 8 staged ones),
-    ragged and tiny M, and no activation."""
+    ragged and tiny M, and no activation.  precision "bf16" (IDDGCN_GEMM_BF16): the weights, node rows and
+    coefficients enter the MFMAs rounded to bf16, so the fp64 reference takes them rounded the same way (the products
+    of bf16 values are exact in fp32: the same bar)."""
     g = torch.Generator().manual_seed(hash(case) % 1000)
     N, M = 5000, {"tiny": 45, "one_tile": 32}.get(case, 60_013)
     if case == "short_runs":
@@ -73,11 +85,13 @@ def test_fwd_gather8_bf16(case, cuda):
     W = torch.rand(M, 8, generator=g, dtype=torch.float64).to(cuda)
     P = torch.randn(8, N, D, generator=g, dtype=torch.float64).to(cuda)
     t = t.to(cuda)
-    z = A.double() @ S.float().double() + sum(W.float().double()[:, r:r + 1] * P.float().double()[r][t] for r in range(8))
+    op = rb if precision == "bf16" else (lambda x: x.float().double())
+    z = A.double() @ op(S) + sum(op(W)[:, r:r + 1] * op(P)[r][t] for r in range(8))
     act = L.ACT_NONE if case == "linear" else L.ACT_SIGMOID
     ref = z if case == "linear" else torch.sigmoid(z)
     C = torch.full((M + 7, D), float("nan"), dtype=torch.bfloat16, device=cuda)
-    ops.rowgemm(A, S.float(), C[:M], coef=W.float(), V=P.float(), v_idx=t.int(), v_rel_stride=N * D, act=act)
+    ops.rowgemm(A, S.float(), C[:M], coef=W.float(), V=P.float(), v_idx=t.int(), v_rel_stride=N * D, act=act,
+                precision=precision)
     err = (C[:M].double() - ref).abs()
     assert (err <= 2 ** -8 * ref.abs() + 1e-5 * ref.abs().max()).all(), err.max().item()
     assert C[M:].isnan().all()                 # nothing past row M is written
@@ -128,7 +142,11 @@ def test_fwd_gather8_bf16_offsets_past_2e32(cuda):
     assert (err <= 2 ** -8 * ref.abs() + 1e-5 * ref.abs().max()).all(), err.max().item()
 
 
-def test_rowgemm_bf16_backward_dsigmoid(cuda):
+@pytest.mark.parametrize("precision", ["exact", "bf16"])
+def test_rowgemm_bf16_backward_dsigmoid(precision, cuda):
+    """The sigma' backward on bf16 tables; precision "bf16" (IDDGCN_GEMM_BF16): the weights rounded to bf16, so the
+    fp64 reference takes them rounded too and every element must sit within the output's bf16 rounding (2^-8
+    relative) plus 1e-5 of max|ref|."""
     g = torch.Generator().manual_seed(7)
     M = 30_001
     dO = bf(torch.randn(M, D, generator=g) * 1e-4).to(cuda)
@@ -136,11 +154,23 @@ def test_rowgemm_bf16_backward_dsigmoid(cuda):
     X = bf(torch.rand(M, D, generator=g)).to(cuda)
     ref = (dO.double() @ S.t()) * X.double() * (1 - X.double())
     C = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
-    ops.rowgemm(dO, S.float(), C, b_trans=True, act=L.ACT_DSIGMOID, aux=X)
+    ops.rowgemm(dO, S.float(), C, b_trans=True, act=L.ACT_DSIGMOID, aux=X, precision=precision)
     assert maxrel(C, ref) <= 6e-3
+    if precision == "bf16":
+        ref_b = (dO.double() @ rb(S).t()) * X.double() * (1 - X.double())
+        err = (C.double() - ref_b).abs()
+        assert (err <= 2 ** -8 * ref_b.abs() + 1e-5 * ref_b.abs().max()).all(), err.max().item()
     Xi = X.clone()                     # in place over the sigma' operand, as the engine runs it
-    ops.rowgemm(dO, S.float(), Xi, b_trans=True, act=L.ACT_DSIGMOID, aux=Xi)
+    ops.rowgemm(dO, S.float(), Xi, b_trans=True, act=L.ACT_DSIGMOID, aux=Xi, precision=precision)
     assert torch.equal(Xi, C)
+
+
+def test_rowgemm_bf16_precision_refused_on_fp32_tables(cuda):
+    """IDDGCN_GEMM_BF16 is a bf16-table form: iddgcn_rowgemm_f32 refuses it (IDDGCN_E_BAD_ARG, nothing launched)."""
+    A = torch.rand(64, D, device=cuda)
+    C = torch.empty(64, D, device=cuda)
+    with pytest.raises(L.IddgcnError):
+        ops.rowgemm(A, torch.randn(D, D, device=cuda), C, precision="bf16")
 
 
 @pytest.mark.parametrize("M", [31, 5003, 300_017])
@@ -192,8 +222,9 @@ def test_combine_tail_seg_distmult_bf16(R, cuda):
     assert torch.equal(s, s32) and torch.equal(p, p32)
 
 
+@pytest.mark.parametrize("edge_mfma", ["hilo", "bf16"])
 @pytest.mark.parametrize("R", [2, 8])
-def test_bf16_mode_step_tracks_fp32(R, cuda):
+def test_bf16_mode_step_tracks_fp32(R, edge_mfma, cuda):
     N = 1500
     pos, neg = synthetic_graph(N, R, 16000, seed=40 + R)
     tri = np.concatenate([pos, neg])
@@ -205,7 +236,7 @@ def test_bf16_mode_step_tracks_fp32(R, cuda):
                        f"Wa{l}": rng.standard_normal((D, R)) / np.sqrt(D), f"ba{l}": rng.standard_normal(R) * 0.1})
     out = {}
     for feat in ("f32", "bf16"):
-        eng = Engine(N, R, D, cuda, features=feat)
+        eng = Engine(N, R, D, cuda, features=feat, edge_mfma=edge_mfma if feat == "bf16" else "hilo")
         P, G = FlatParams(N, R, D, cuda), FlatParams(N, R, D, cuda)
         P.load(params)
         adj = eng.adjacency(get_adj_mats(pos, N, R))

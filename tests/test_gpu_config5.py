@@ -11,6 +11,8 @@ D=256, the bf16-feature mode: edge tables x^1..x^3 stored as bf16, edge GEMMs on
     elements whose bf16 rounding lands the other way (each such flip moves one element of x_t^l by one bf16
     ulp, up to 2^-9, and the next layers carry it on); bars: logits 2e-2 at most and 5e-3 on 99% of the
     edges, probabilities 5e-3.
+    The edge GEMMs' operands are checked in both forms: the weights (and the R = 8 combine's node rows and
+    coefficients) as bf16 hi + lo, and rounded to bf16 (Engine(edge_mfma="bf16"), the form bench.py times).
   * A full training step is finite and bitwise deterministic run to run.
   * The backward at this size against the oracle (tests/fullsize_grads.py): a sampled step with the FULL
     40M-entry adjacency and the R = 8 node tables (R·N·D = 2^31 elements: offsets past 32 bits), every gradient
@@ -74,13 +76,15 @@ def test_config5_device_negatives_bit_exact(cfg5):
     assert np.array_equal(neg[:, 0], rh) and np.array_equal(neg[:, 1], rr) and np.array_equal(neg[:, 2], rt)
 
 
-@pytest.mark.parametrize("gemm", ["exact", "split"])
-def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, gemm, cuda):
-    """``gemm``: the node-level GEMMs' operand precision; "split" (split-fp16 node projections) is the mode
-    bench.py times for config 5 (CONFIGS[5]["gemm"])."""
+@pytest.mark.parametrize("gemm,edge_mfma", [("exact", "hilo"), ("split", "hilo"), ("split", "bf16")])
+def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, gemm, edge_mfma, cuda):
+    """``gemm``: the node-level GEMMs' operand precision; ``edge_mfma``: the edge GEMMs' operands (weights and the R = 8
+    combine's node rows / coefficients as bf16 hi + lo, or rounded to bf16: IDDGCN_GEMM_BF16).  ("split", "bf16") is
+    what bench.py times for config 5 (CONFIGS[5]); the same bars for every combination."""
     params = mild_params()
     eng, ed, sample = cfg5["eng"], cfg5["ed"], cfg5["sample"]
     eng.gemm = gemm
+    eng.edge_mfma = edge_mfma
     P = FlatParams(N, R, D, cuda)
     P.load(params)
     p, s = eng.predict(P, cfg5["adj"], ed, logits=True)
@@ -97,6 +101,7 @@ def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, gemm, cuda):
     del P
     eng.release()
     eng.gemm = "exact"
+    eng.edge_mfma = "hilo"
 
 
 def test_config5_step_finite_and_deterministic(cfg5, cuda):
@@ -128,7 +133,9 @@ def test_config5_step_grads_vs_oracle_sample(cfg5, features, cuda):
                             saturating=False, what="config 5 f32")
         eng.release()
     else:
-        # both node-GEMM operand modes: "split" is what bench.py times for config 5
-        check_sampled_grads(cfg5["eng"], cfg5["adj"], mild_params(3), cfg5["pos"], tri_s, lab_s, ("exact", "split"),
-                            cuda, saturating=False, what="config 5 bf16", bar=5e-2, loss_bar=2e-2, p_bar=2e-2)
+        # both node-GEMM operand modes, and split with bf16 edge-GEMM operands: "split/bf16" is what bench.py times
+        # for config 5
+        check_sampled_grads(cfg5["eng"], cfg5["adj"], mild_params(3), cfg5["pos"], tri_s, lab_s,
+                            ("exact", "split", "split/bf16"), cuda, saturating=False, what="config 5 bf16", bar=5e-2,
+                            loss_bar=2e-2, p_bar=2e-2)
         cfg5["eng"].gemm = "exact"

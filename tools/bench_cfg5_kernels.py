@@ -77,6 +77,13 @@ def main():
                         lambda: [ws.dz])
     dS = torch.empty(D, D, device=dev)
     cases["TN bf16 (dS)"] = (lambda: ops.gemm_tn(ws.xt[0], ws.xt[1], dS, ws.tn_slab), lambda: [dS])
+    # the sigma' backward edge GEMM (do^2 . S3^T) * x2 (1 - x2) written to a scratch bf16 table (timing + comparison)
+    bwd_out = torch.empty_like(ws.xt[0])
+    cases["sigma' bwd GEMM"] = (lambda: ops.rowgemm(ws.xt[1], P["S3"], bwd_out, b_trans=True, act=L.ACT_DSIGMOID,
+                                                    aux=ws.xt[0], precision=eng.row_gemm), lambda: [bwd_out])
+    cases["sigma' bwd GEMM bf16 ops"] = (lambda: ops.rowgemm(ws.xt[1], P["S3"], bwd_out, b_trans=True,
+                                                             act=L.ACT_DSIGMOID, aux=ws.xt[0], precision="bf16"),
+                                         lambda: [bwd_out])
     only = os.environ.get("IDDGCN_CFG5_CASES")      # comma-separated case names (and "fwd") to time; default all
     if only:
         cases = {k: v for k, v in cases.items() if k in only.split(",")}
@@ -103,9 +110,10 @@ def main():
         if lp:
             L._lib = load_lenient(lp)
         tag = lp.split("/")[-1] if lp else "default"
-        ms = timeit(lambda: ops.rowgemm(ws.xt[1], P["S3"], ws.xt[2], coef=ws.Wedge[2], V=ws.P[2], v_idx=ed.t,
-                                        v_rel_stride=N * D, act=L.ACT_SIGMOID, precision=eng.row_gemm), reps=3)
-        print(f"{tag:14s} {'fwd R8 edge GEMM':24s} {ms:8.3f} ms", flush=True)
+        for prec, lab in ((eng.row_gemm, "fwd R8 edge GEMM"), ("bf16", "fwd R8 edge GEMM bf16 ops")):
+            ms = timeit(lambda: ops.rowgemm(ws.xt[1], P["S3"], ws.xt[2], coef=ws.Wedge[2], V=ws.P[2], v_idx=ed.t,
+                                            v_rel_stride=N * D, act=L.ACT_SIGMOID, precision=prec), reps=3)
+            print(f"{tag:14s} {lab:24s} {ms:8.3f} ms", flush=True)
 
 
 if __name__ == "__main__":
