@@ -57,7 +57,8 @@ DTYPE_BF16 = {
     "bf16": ("bf16 edge tables (x^l, do^l) with bf16 x bf16 MFMA for the edge GEMMs (every edge-GEMM operand rounded "
              "to bf16 once: weights, and the R = 8 combine's node rows and coefficients; include/iddgcn.h "
              "IDDGCN_GEMM_BF16), fp32 node tables, accumulation and epilogues, node-level GEMMs on split-fp16 "
-             "operands (perf-only mode, BASELINE config 5: 'bf16 features with MFMA XW')"),
+             "operands (perf-only opt-in form of BASELINE config 5's 'bf16 features with MFMA XW': 8x the logit error of "
+             "hi+lo weights at the 99% quantile, DESIGN.md)"),
 }
 
 CONFIGS = {
@@ -66,7 +67,7 @@ CONFIGS = {
     4: dict(name="synthetic-4", N=1_000_000, R=2, M=20_000_000, D=256, scaling="strong"),
     # 40M positives, 10M negatives (one per 4 positives), generated on the device
     5: dict(name="synthetic-5", N=1_000_000, R=8, M=40_000_000, D=256, scaling="strong", neg_every=4,
-            features="bf16", gemm="split", edge_mfma="bf16"),
+            features="bf16", gemm="split", edge_mfma="hilo"),
 }
 
 

@@ -63,10 +63,11 @@ extern "C" {
  *   IDDGCN_GEMM_BF16 (ABI 10; iddgcn_rowgemm_bf16 only, i.e. bf16 edge tables): every MFMA operand rounded to
  *     bf16 once (RNE) — the weights, and in the R = 8 gathered forward also the node rows and per-edge
  *     coefficients of the combine — one bf16 x bf16 product per term, fp32 accumulation and epilogue
- *     (BASELINE config 5's "bf16 features with MFMA XW", as autocast would run it).  With bf16 A rows the
- *     weight's own rounding (2^-9 relative) is the size of the A rounding and of the output's bf16 store;
- *     any other precision on a bf16 call keeps the weights (and combine operands) as a bf16 hi + lo pair
- *     (16 significant bits).  iddgcn_rowgemm_f32 rejects it (IDDGCN_E_BAD_ARG).
+ *     (an opt-in form of BASELINE config 5's "bf16 features with MFMA XW", as autocast would run it): fewer
+ *     MFMAs, but the weights' own rounding (2^-9 relative per product) reaches the logits — at config 5, 8x the
+ *     99%-quantile logit error of the hi + lo form.  Any other precision on a bf16 call keeps the
+ *     weights (and combine operands) as a bf16 hi + lo pair (16 significant bits).  iddgcn_rowgemm_f32 rejects
+ *     it (IDDGCN_E_BAD_ARG).
  * Row GEMMs for D < 256 and every other kernel compute in exact f32 (or F32_4CHAIN where asked). */
 #define IDDGCN_GEMM_EXACT_F32 0
 #define IDDGCN_GEMM_SPLIT_F16 1

@@ -12,7 +12,8 @@ D=256, the bf16-feature mode: edge tables x^1..x^3 stored as bf16, edge GEMMs on
     ulp, up to 2^-9, and the next layers carry it on); bars: logits 2e-2 at most and 5e-3 on 99% of the
     edges, probabilities 5e-3.
     The edge GEMMs' operands are checked in both forms: the weights (and the R = 8 combine's node rows and
-    coefficients) as bf16 hi + lo, and rounded to bf16 (Engine(edge_mfma="bf16"), the form bench.py times).
+    coefficients) as bf16 hi + lo (the form bench.py times), and rounded to bf16 (Engine(edge_mfma="bf16"), opt-in,
+    at its own measured bars).
   * A full training step is finite and bitwise deterministic run to run.
   * The backward at this size against the oracle (tests/fullsize_grads.py): a sampled step with the FULL
     40M-entry adjacency and the R = 8 node tables (R·N·D = 2^31 elements: offsets past 32 bits), every gradient
@@ -79,8 +80,12 @@ def test_config5_device_negatives_bit_exact(cfg5):
 @pytest.mark.parametrize("gemm,edge_mfma", [("exact", "hilo"), ("split", "hilo"), ("split", "bf16")])
 def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, gemm, edge_mfma, cuda):
     """``gemm``: the node-level GEMMs' operand precision; ``edge_mfma``: the edge GEMMs' operands (weights and the R = 8
-    combine's node rows / coefficients as bf16 hi + lo, or rounded to bf16: IDDGCN_GEMM_BF16).  ("split", "bf16") is
-    what bench.py times for config 5 (CONFIGS[5]); the same bars for every combination."""
+    combine's node rows / coefficients as bf16 hi + lo, or rounded to bf16: IDDGCN_GEMM_BF16).  ("split", "hilo") is
+    what bench.py times for config 5 (CONFIGS[5]), at the bars above.  The opt-in bf16-operand form adds the weights'
+    own bf16 rounding to every product (measured: logits 3.2e-2 max, 1.75e-2 at the 99% quantile, 4.3e-3 median,
+    against 9.8e-3 / 2.2e-3 / 3e-7 for hi + lo; tools/cfg5_operand_error.py, profiles/r05/cfg5/cfg5_operand_error.txt)
+    and is held to 5e-2 max and 2.5e-2 on 99% of the edges, probabilities 1e-2."""
+    bars = (5e-2, 2.5e-2, 1e-2) if edge_mfma == "bf16" else (2e-2, 5e-3, 5e-3)
     params = mild_params()
     eng, ed, sample = cfg5["eng"], cfg5["ed"], cfg5["sample"]
     eng.gemm = gemm
@@ -92,9 +97,9 @@ def test_config5_bf16_forward_vs_oracle_on_rounded_tables(cfg5, gemm, edge_mfma,
     bf = lambda x: x.to(torch.bfloat16).to(x.dtype)  # noqa: E731   the engine's bf16 storage of x_t^l
     p64, s64, _ = forward_detail(params, cfg5["tri"], cfg5["coo"], N, dtype=torch.float64, tail_round=bf)
     err = np.abs(ss - s64)
-    assert err.max() <= 2e-2 and np.quantile(err, 0.99) <= 5e-3, \
+    assert err.max() <= bars[0] and np.quantile(err, 0.99) <= bars[1], \
         f"logits: max err {err.max():.2e}, 99% {np.quantile(err, 0.99):.2e} (max|s| {np.abs(s64).max():.2f})"
-    assert np.abs(ps - p64).max() <= 5e-3
+    assert np.abs(ps - p64).max() <= bars[2]
     # and the bf16 storage is what the engine's tables hold: its layer-3 tail rows are bf16 values
     _, xt3 = eng.layer_outputs(ed, rows=sample[:64])[2]
     assert torch.equal(xt3, xt3.to(torch.bfloat16).float())
@@ -133,8 +138,8 @@ def test_config5_step_grads_vs_oracle_sample(cfg5, features, cuda):
                             saturating=False, what="config 5 f32")
         eng.release()
     else:
-        # both node-GEMM operand modes, and split with bf16 edge-GEMM operands: "split/bf16" is what bench.py times
-        # for config 5
+        # both node-GEMM operand modes ("split" is what bench.py times for config 5), and split with the opt-in bf16
+        # edge-GEMM operands
         check_sampled_grads(cfg5["eng"], cfg5["adj"], mild_params(3), cfg5["pos"], tri_s, lab_s,
                             ("exact", "split", "split/bf16"), cuda, saturating=False, what="config 5 bf16", bar=5e-2,
                             loss_bar=2e-2, p_bar=2e-2)
