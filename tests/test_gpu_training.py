@@ -11,8 +11,8 @@ tests/test_tf_random.py), so fit() here starts where the reference started.
 
 Bars, per fold: the trained model's eval ROC-AUC (IDDGCN_eval.py:35-122: graph = X_train + test positives, scored
 on test positives + negatives) within 0.001 of the AUC of the bundled trained weights on the same eval path; the
-trained weights within 5% (max |w - w_ref| / max |w_ref| per parameter) of the bundled ones — 50% for fold 4,
-whose trajectory drifts further from the reference's (its AUC still lands within the bar).  Measured (round 4,
+trained weights within 5% (max |w - w_ref| / max |w_ref| per parameter) of the bundled ones — 30% for fold 4,
+whose trajectory drifts further from the reference's (its AUC still lands within the bar; W_BAR below).  Measured (round 4,
 profiles/r04/train/train_tf27.json): AUC 0.9072 / 0.8841 / 0.8831 / 0.9147 / 0.9076 vs 0.9072 / 0.8841 / 0.8832 /
 0.9148 / 0.9068; weights within 0.4-1.3% for E, 0.02-0.7% for K, S, rel, the layer-3 bias the furthest at
 0.8-2.5% (folds 0-3), up to 27% (fold 4, W_alpha^3).
@@ -24,7 +24,10 @@ from iddgcn_amd.graph import get_adj_mats
 
 pytestmark = pytest.mark.gpu
 N_ENT, N_REL, DIM = 845, 4, 64
-W_BAR = {0: 0.05, 1: 0.05, 2: 0.05, 3: 0.05, 4: 0.5}
+# fold 4: every one of ten runs of ours (five summation orders, four 1-ulp perturbations of the start) lands 0.258-0.266
+# from the bundled file and within 1.9% of each other; the fold is 5-24x more order-sensitive than folds 0-2 and no
+# semantic difference was found (DESIGN.md "Fold 4", profiles/r05/train/)
+W_BAR = {0: 0.05, 1: 0.05, 2: 0.05, 3: 0.05, 4: 0.3}
 
 
 def _eval_auc(model, d):
