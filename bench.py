@@ -200,6 +200,53 @@ def reference_init(np, N, R, D, seed):
     return p
 
 
+FOLD0_REFERENCE_AUC = 0.9072     # the reference's eval ROC-AUC of fold 0 with its bundled trained weights
+
+
+def fold0_auc(dev, epochs=5000):
+    """The metric's second part, "AUC vs reference on fold-0" (BASELINE.json): the reference's fold-0 split and
+    weights, converted once into tests/golden/ (data fixtures: fold0_data.npz, weights_fold0.npz), through the product
+    API (get_IDDGCN_Model -> predict / fit: IDDGCN_eval.py:35-122, IDDGCN.py:287-412).  Two numbers: the eval AUC with
+    the reference's bundled trained weights, and the eval AUC after training fold 0 from TF 2.7's replayed initial
+    weights for the reference's 5000 epochs (fit() on the kernels, HIP-graph replay), each beside the reference's
+    0.9072; plus the training time."""
+    import numpy as np
+    from sklearn.metrics import roc_auc_score
+    from iddgcn_amd import Adam, BinaryCrossentropy, get_IDDGCN_Model
+    from iddgcn_amd.graph import get_adj_mats
+    n_ent, n_rel, dim = 845, 4, 64
+    gold = os.path.join(ROOT, "tests", "golden")
+    d = np.load(os.path.join(gold, "fold0_data.npz"))
+    adj_eval = get_adj_mats(np.concatenate([d["X_train"], d["X_test"]]), n_ent, n_rel)
+    Xt = np.concatenate([d["X_test"], d["neg_X_test"]])[None]
+    y = np.concatenate([np.ones(len(d["X_test"])), np.zeros(len(d["neg_X_test"]))])
+
+    def auc(model):
+        p = model.predict(x=[np.arange(n_ent)[None], Xt[:, :, 0], Xt[:, :, 1], Xt[:, :, 2], adj_eval])[0]
+        return float(roc_auc_score(y, p))
+
+    ref_model = get_IDDGCN_Model(n_ent, n_rel, dim, dim, 89, None, 0, 0)
+    ref_model.load_weights(os.path.join(gold, "weights_fold0.npz"))
+    a_bundled = auc(ref_model)
+    model = get_IDDGCN_Model(n_ent, n_rel, dim, dim, 89, None, 0, 0, init="tf27")
+    model.neg_triples = d["X_train_neg"][None]
+    model.compile(loss=BinaryCrossentropy(), optimizer=Adam(learning_rate=0.001))
+    X = d["X_train"][None]
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    model.fit(x=[np.arange(n_ent)[None], X[:, :, 0], X[:, :, 1], X[:, :, 2], get_adj_mats(d["X_train"], n_ent, n_rel)],
+              y=np.ones((1, X.shape[1])), epochs=epochs, batch_size=100, verbose=0)
+    torch.cuda.synchronize()
+    fit_s = time.perf_counter() - t0
+    a_trained = auc(model)
+    return {"reference": FOLD0_REFERENCE_AUC, "bundled_weights": a_bundled,
+            "trained_from_replayed_init": a_trained, "epochs": epochs, "fit_s": fit_s,
+            "delta_bundled": a_bundled - FOLD0_REFERENCE_AUC, "delta_trained": a_trained - FOLD0_REFERENCE_AUC,
+            "within_0.001": abs(a_bundled - FOLD0_REFERENCE_AUC) <= 1e-3 and abs(a_trained - FOLD0_REFERENCE_AUC) <= 1e-3,
+            "source": "tests/golden/fold0_data.npz + weights_fold0.npz (the reference's bundled fold-0 files, converted)"}
+
+
 def cpu_model():
     """The host CPU's model name (/proc/cpuinfo), for the cpu_baseline record (core count and CPU
     model next to every CPU number)."""
@@ -492,6 +539,8 @@ def main():
                          "row-partitioned SpMMs; default 4 5 (BASELINE configs 4 and 5), plus 4e with more than one "
                          "GPU; none to skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fold0-auc", action="store_true",
+                    help="skip the metric's second part: the fold-0 eval AUC (bundled weights, and trained from scratch)")
     ap.add_argument("--no-planes", action="store_true",
                     help="fp32 tail tables x^1, x^2 instead of the pre-split planes form (A/B)")
     ap.add_argument("--shard", default=None, choices=["edge", "node", "relation", "spmm"],
@@ -596,6 +645,11 @@ def main():
         also.append(o)
     if also:
         result["also"] = also
+    if rank == 0 and not args.no_fold0_auc:
+        try:
+            result["fold0_auc"] = fold0_auc(dev)
+        except Exception as e:                   # reported, never costs the bench line
+            result["fold0_auc"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(CONFIGS[args.config])
     if rank == 0:
