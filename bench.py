@@ -645,7 +645,7 @@ def main():
         also.append(o)
     if also:
         result["also"] = also
-    if rank == 0 and not args.no_fold0_auc:
+    if world == 1 and not args.no_fold0_auc:       # (at N > 1, fit() would shard fold 0 over the ranks: N = 1 only)
         try:
             result["fold0_auc"] = fold0_auc(dev)
         except Exception as e:                   # reported, never costs the bench line

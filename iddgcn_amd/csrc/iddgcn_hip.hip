@@ -560,9 +560,11 @@ template <int NV, bool AUX, bool HAS_COEF, bool X3, bool CW = false, bool BF = f
           bool W1 = false>
 __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     using namespace r3;
-    // A row pitch: bf16 rows (BF) need 512 B of the 1040-B fp32 row; a 528-B pitch keeps the same bank
-    // pattern for the fragment reads (4i mod 64) and lets the wide R = 8 form keep three A buffers
-    constexpr int LDA = BF ? 132 : r3::LDA;
+    // A row pitch: bf16 rows (BF) need 512 B of the 1040-B fp32 row; round 4 padded them to 528 B (the fragment reads'
+    // bank pattern 4i mod 64), which also let the wide R = 8 form keep three A buffers
+    // (BF, round 5: 512-B slots with the 16-B chunks of row r XOR-swizzled by r & 15, two rows per full-wave DMA;
+    // the swizzle keeps the fragment reads conflict-free without the pad)
+    constexpr int LDA = BF ? 128 : r3::LDA;
     constexpr int A_FLOATS = TR * LDA;
     const RowGemmP p = pb.p[blockIdx.y];
     static_assert(!PL || (X3 && !BF && !CW && ((AUX && NV == 0) || (!AUX && (NV == 1 || NV == 2)))),
@@ -735,16 +737,23 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
 #pragma unroll
             for (int j = 0; j < ROWS_PER_WAVE; ++j) sa[j] = __builtin_amdgcn_readlane(v, j);
         }
+        if constexpr (BF) {
+            // two 512-B bf16 rows per full-wave DMA: lane i -> row r0 + (i >> 5), LDS chunk i & 31 of its slot,
+            // global chunk (i & 31) ^ (row & 15)
 #pragma unroll
-        for (int j = 0; j < ROWS_PER_WAVE; ++j) {
-            const int r = wave * ROWS_PER_WAVE + j;
-            const long long e = clampe(t * TR + r);
-            const long long src = p.a_idx ? (long long)sa[j] : e;
-            if constexpr (BF) {      // a 512-B bf16 row: 32 lanes, straight into the row's hi-plane slot
-                const char* g = reinterpret_cast<const char*>(p.A) + src * D * 2 + (lane & 31) * 16;
-                if (lane < 32)
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * LDA), 16, 0, 0);
-            } else {
+            for (int j = 0; j < ROWS_PER_WAVE / 2; ++j) {
+                const int r0 = wave * ROWS_PER_WAVE + 2 * j;
+                const int r = r0 + (lane >> 5);
+                const long long src = p.a_idx ? (long long)((lane >> 5) ? sa[2 * j + 1] : sa[2 * j]) : clampe(t * TR + r);
+                const char* g = reinterpret_cast<const char*>(p.A) + src * D * 2 + ((lane & 31) ^ (r & 15)) * 16;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r0 * LDA), 16, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < ROWS_PER_WAVE; ++j) {
+                const int r = wave * ROWS_PER_WAVE + j;
+                const long long e = clampe(t * TR + r);
+                const long long src = p.a_idx ? (long long)sa[j] : e;
                 const float* g = p.A + src * D + lane * 4;
                 __builtin_amdgcn_global_load_lds((gbl_vptr)g, (lds_vptr)(bufA + b * A_FLOATS + r * LDA), 16, 0, 0);
             }
@@ -1007,6 +1016,7 @@ __global__ __launch_bounds__(512) void rowgemm256_v3_kernel(RowGemmBatch pb) {
     auto wait_newest = [&](int n) __attribute__((always_inline)) {
         if (n >= 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
         else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
@@ -1027,7 +1037,7 @@ _Pragma("unroll") \
             const bool more = t + PD < t_end; \
             if (more) dma_A(t + PD, PD == 2 ? b2 : b1); \
             /* ops issued so far this iteration (the youngest): the A(t+PD) rows */ \
-            const int n_new = more ? ROWS_PER_WAVE : 0; \
+            const int n_new = more ? (BF ? ROWS_PER_WAVE / 2 : ROWS_PER_WAVE) : 0; \
             if (LATE && t > t_beg) { \
                 wait_newest(n_new);          /* slabs(t-1), idx(t) and every older op */ \
                 epilogue(t - 1, acc); \
@@ -1066,13 +1076,15 @@ _Pragma("unroll") \
                 /* bf16 A fragments straight from the row; W hi and lo, one accumulator */ \
 _Pragma("unroll") \
                 for (int j = 0; j < 16; ++j) acc[j] = 0.f; \
-                const float* arow = bufA + b * A_FLOATS + i * LDA + 4 * h; \
+                /* row i, logical chunk 2q + h at physical chunk (2q + h) ^ (i & 15) = 2q ^ (h ^ (i & 15)) */ \
+                const float* arow = bufA + b * A_FLOATS + i * LDA; \
+                const int su = 4 * (h ^ (i & 15)); \
                 f16x8 ah[2]; \
-                ah[0] = __builtin_bit_cast(f16x8, ld4(arow)); \
+                ah[0] = __builtin_bit_cast(f16x8, ld4(arow + su)); \
 _Pragma("unroll") \
                 for (int q = 0; q < D / 16; ++q) { \
                     const int cu = q & 1; \
-                    if (q + 1 < D / 16) ah[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + 8 * (q + 1))); \
+                    if (q + 1 < D / 16) ah[cu ^ 1] = __builtin_bit_cast(f16x8, ld4(arow + ((8 * (q + 1)) ^ su))); \
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, bhi[q]), \
                                                                   __builtin_bit_cast(bf16x8, ah[cu]), acc, 0, 0, 0); \
                     if constexpr (!W1) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, blo[q]), \
@@ -1558,16 +1570,18 @@ __device__ __forceinline__ void wait_vm(int n) {
 #undef WVM
 }
 // TN reduction GEMM over bf16 edge tables, transposed reads (round 4; replaces gemm_tn256_bf16_kernel's in-LDS
-// software transpose: 32 two-byte LDS reads and 8 writes per lane per tile and two barriers).  The 512-B rows of
-// A and B arrive by LDS-DMA (32 lanes per row) into 576-B row slots (144 dwords = 16 mod 64 banks: the 32 lanes of a
-// transposed read, 4 rows x 64 B, are conflict-free), three 32-row buffers deep (four ran slower: 11.55 vs 11.06 ms
-// per config-5 launch, profiles/r04/cfg5/tn_bf16t_ab.txt); the MFMA fragments (8 consecutive
-// rows of one column) come straight from the row-major rows through ds_read_b64_tr_b16.  Wave w owns output rows
-// 32w..32w+31 (columns of A) x all 256 columns (8 accumulator tiles); one v_mfma_f32_32x32x16_bf16 per (k-step,
-// column tile), rows 16s..16s+15 of the tile in k-step s with the same lane k-order as the old kernel, so the
-// partials are bitwise its own.  One barrier per tile.
+// software transpose).  The 512-B rows of A and B land in LDS by LDS-DMA, three 32-row buffers deep; the MFMA
+// fragments (8 consecutive rows of one column) come straight from the row-major rows through ds_read_b64_tr_b16.
+// Round 5: the rows sit in 512-B slots with their 16-B chunks XOR-swizzled (chunk c of row r at chunk c ^ 4(r & 3)),
+// so one full-wave DMA (64 lanes x 16 B) fills TWO row slots — each lane picks the global chunk that belongs at its
+// LDS position — where the round-4 layout (576-B slots, the pad making the transposed reads conflict-free) needed a
+// half-wave DMA per row: 4 instead of 8 DMA issues per wave per tile.  The transposed reads stay conflict-free: a
+// 32-lane half reads 4 rows x 64 B, and the swizzle puts the 4 rows' 64-B pieces on the 4 different quarters of the
+// 256-B bank row.  Wave w owns output rows 32w..32w+31 (columns of A) x all 256 columns (8 accumulator tiles); one
+// v_mfma_f32_32x32x16_bf16 per (k-step, column tile), rows 16s..16s+15 of the tile in k-step s with the same lane
+// k-order as before, so the partials are bitwise the round-4 kernel's.  One barrier per tile.
 namespace tbf {
-constexpr int D = 256, TK = 32, PT = 576, OPB = TK * PT, BUF = 2 * OPB, NBUF = 3, PD = NBUF - 1;
+constexpr int D = 256, TK = 32, PT = 512, OPB = TK * PT, BUF = 2 * OPB, NBUF = 3, PD = NBUF - 1;   // 4 buffers: 10.1 vs 9.8 ms
 }  // namespace tbf
 __device__ __forceinline__ bf16x8 tr_frag_bf(const char* p0) {
     typedef __attribute__((address_space(3))) v4s16* l4p;
@@ -1581,7 +1595,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_bf16t_kernel(long long M, long
                                                                float* __restrict__ slab) {
     using namespace tbf;
     static_assert(NBUF * BUF <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(16))) char lds[NBUF * BUF];     // [buf][A | B][TK][PT]
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * BUF];     // [buf][A | B][TK][PT], chunks swizzled
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     f32x16 acc[8];
@@ -1593,42 +1607,61 @@ __global__ __launch_bounds__(512) void gemm_tn256_bf16t_kernel(long long M, long
     long long r_end = r_beg + rows_per_block;
     if (r_end > M) r_end = M;
     const long long nt = r_end > r_beg ? (r_end - r_beg + TK - 1) / TK : 0;
-    // rows 4w .. 4w+3 of both operands of tile t into buffer bb, 32 lanes (16 B each) per row, rows past the range
-    // as zeros; returns the LDS-DMA count (wave-uniform)
+    // rows 4w .. 4w+3 of both operands of tile t into buffer bb; returns the LDS-DMA count (wave-uniform).  A full
+    // tile: two DMAs per operand, each filling the slots of rows (r, r+1): lane i -> row r + (i >> 5), LDS chunk
+    // i & 31, global chunk (i & 31) ^ 4((r + (i >> 5)) & 3).  The range's last, partial tile: one half-wave DMA per
+    // row in range (lane i < 32 -> LDS chunk i, global chunk i ^ 4(r & 3)), fp32 zeros for the rows past it.
     auto stage = [&](long long t, int bb) __attribute__((always_inline)) {
+        const long long t0 = r_beg + t * TK;
         int n = 0;
+        if (t0 + TK <= r_end) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int r = 4 * wave + j;
-            const long long e = r_beg + t * TK + r;
-            char* ra = lds + bb * BUF + r * PT;
-            if (e < r_end) {
-                if (lane < 32) {
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)(A + e * D + lane * 8), (lds_vptr)ra, 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds((gbl_vptr)(B + e * D + lane * 8), (lds_vptr)(ra + OPB), 16, 0, 0);
+            for (int j = 0; j < 2; ++j) {
+                const int r = 4 * wave + 2 * j + (lane >> 5);
+                const int c = (lane & 31) ^ (4 * (r & 3));
+                const long long e = t0 + r;
+                char* ra = lds + bb * BUF + (4 * wave + 2 * j) * PT;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)(A + e * D + c * 8), (lds_vptr)ra, 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gbl_vptr)(B + e * D + c * 8), (lds_vptr)(ra + OPB), 16, 0, 0);
+            }
+            n = 4;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = 4 * wave + j;
+                const long long e = t0 + r;
+                char* ra = lds + bb * BUF + r * PT;
+                if (e < r_end) {
+                    if (lane < 32) {
+                        const int c = lane ^ (4 * (r & 3));
+                        __builtin_amdgcn_global_load_lds((gbl_vptr)(A + e * D + c * 8), (lds_vptr)ra, 16, 0, 0);
+                        __builtin_amdgcn_global_load_lds((gbl_vptr)(B + e * D + c * 8), (lds_vptr)(ra + OPB), 16, 0, 0);
+                    }
+                    n += 2;
+                } else if (lane < 32) {
+                    st4(reinterpret_cast<float*>(ra) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                    st4(reinterpret_cast<float*>(ra + OPB) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
                 }
-                n += 2;
-            } else if (lane < 32) {
-                st4(reinterpret_cast<float*>(ra) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
-                st4(reinterpret_cast<float*>(ra + OPB) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
             }
         }
         return n;
     };
     auto wait_newest = [&](int n) __attribute__((always_inline)) { wait_vm(n); };
-    // this lane's transposed-read address: rows 8(l>>5) + ((l>>2)&3) (+4: second read), columns
-    // 16((l>>4)&1) + 4(l&3) of a 32-column block
-    const int roff = (8 * (lane >> 5) + ((lane >> 2) & 3)) * PT + 2 * (16 * ((lane >> 4) & 1) + 4 * (lane & 3));
+    // this lane's transposed-read address: rows 8(l>>5) + x (+4: second read), x = (l>>2)&3, logical columns
+    // 16((l>>4)&1) + 4(l&3) of the 32-column block blk, i.e. logical chunk 4 blk + 2((l>>4)&1) + ((l&3)>>1), at
+    // physical chunk 4(blk ^ x) + 2((l>>4)&1) + ((l&3)>>1) (the +4 row has the same r & 3)
+    const int xs = (lane >> 2) & 3;
+    const int roff = (8 * (lane >> 5) + xs) * PT + 2 * (16 * ((lane >> 4) & 1) + 4 * (lane & 3));
     auto mfma_tile = [&](int bb) __attribute__((always_inline)) {
 #pragma unroll
         for (int s = 0; s < TK / 16; ++s) {
             const char* base = lds + bb * BUF + 16 * s * PT + roff;
-            const bf16x8 a = tr_frag_bf(base + 64 * wave);
-            bf16x8 b = tr_frag_bf(base + OPB);
+            const bf16x8 a = tr_frag_bf(base + 64 * (wave ^ xs));
+            bf16x8 b = tr_frag_bf(base + OPB + 64 * xs);
 #pragma unroll
             for (int cj = 0; cj < 8; ++cj) {
                 bf16x8 nb = b;                              // column tile cj+1's fragment in flight
-                if (cj + 1 < 8) nb = tr_frag_bf(base + OPB + 64 * (cj + 1));
+                if (cj + 1 < 8) nb = tr_frag_bf(base + OPB + 64 * ((cj + 1) ^ xs));
                 acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[cj], 0, 0, 0);
                 b = nb;
             }
@@ -3755,7 +3788,9 @@ inline unsigned grid_for(long long rows, int lpr) {
 // on v_mfma_f32_16x16x32_bf16 with the weight / node-row side as operand A, so lane l ends with edge row l&15 of each
 // 16-row block at 4 consecutive columns: one 8-B bf16 store per 16 x 16 block, no LDS staging of the output.
 //   x S:     k-step q: A = S^T pieces (registers, 128 VGPRs: the wave's 32 columns x 256 k x hi / lo), B = 8
-//            consecutive k of an edge row straight from the LDS-DMA'd A tile (528-B row pitch: conflict-free b128).
+//            consecutive k of an edge row straight from the LDS-DMA'd A tile (512-B row slots, 16-B chunks XOR-
+//            swizzled by row, two rows per full-wave DMA; round 4: 528-B slots, one half-wave DMA per row; either
+//            way the b128 fragment reads are conflict-free).
 //   combine: the tile's distinct V rows ("slots": runs of equal v_idx; tail-sorted config-5 edges give 1-3 per
 //            64-row tile) are the k axis, k = 8 s + r for slot s < 4 of a block of four: A = V_r[slot s] at the lane's
 //            column (hi / lo), B = coef[e][r] where slot(e) = s, else 0 (hi / lo); three products (hi hi, hi lo,
@@ -3775,14 +3810,14 @@ inline unsigned grid_for(long long rows, int lpr) {
 namespace fg8 {
 constexpr int D = 256, R = 8, TR = 64, NW = 8, NBUF = 3;
 constexpr int RPW = TR / NW;                             // A rows each wave DMAs per tile
-constexpr int PITCH = 528;                               // bytes per bf16 A row slot (512 + 16)
-constexpr int ABUF = TR * PITCH;                         // 33,792 B per A buffer
+constexpr int PITCH = 512;                               // bytes per bf16 A row slot, 16-B chunks XOR-swizzled
+constexpr int ABUF = TR * PITCH;                         // 32,768 B per A buffer
 constexpr int CAPS = 4;                                  // slots staged in LDS per tile (one block of the k axis)
 constexpr int SLOTB = 1088;                              // bytes per slot: [8 relations][32 columns] fp32 + 64 pad
 // per wave: v_idx [64], slot -> V row [64], coefficients [64][8], slots
 constexpr int WIDX = 0, WTAIL = 256, WCOEF = 512, WV = WCOEF + TR * R * 4;
 constexpr int WREG = WV + CAPS * SLOTB;                  // 6,912 B per wave
-constexpr int LDSB = NBUF * ABUF + NW * WREG;            // 156,672 B
+constexpr int LDSB = NBUF * ABUF + NW * WREG;            // 153,600 B
 static_assert(LDSB <= 160 * 1024, "LDS budget");
 }  // namespace fg8
 
@@ -3834,15 +3869,19 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     // vector-memory ops this wave has issued (wave-uniform): a wait for "op k and everything older" is
     // s_waitcnt vmcnt(nops - k) (ops complete in issue order; LDS-DMA, loads and stores count alike)
     int nops = 0;
+    // A(t): the wave's 8 rows, two per full-wave DMA: lane i -> row r0 + (i >> 5), LDS chunk i & 31 of that row's slot,
+    // global chunk (i & 31) ^ (row & 15) (the swizzle that makes the fragment reads below conflict-free without a pad)
     auto dma_A = [&](long long t, int b) __attribute__((always_inline)) {
         const int lane = fresh_lane();
 #pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            const int r = wave * RPW + j;
-            const char* gp = reinterpret_cast<const char*>(p.A) + clampe(t * TR + r) * (D * 2) + (lane & 31) * 16;
-            if (lane < 32) __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(lds + b * ABUF + r * PITCH), 16, 0, 0);
+        for (int j = 0; j < RPW / 2; ++j) {
+            const int r0 = wave * RPW + 2 * j;
+            const int r = r0 + (lane >> 5);
+            const char* gp = reinterpret_cast<const char*>(p.A) + clampe(t * TR + r) * (D * 2) +
+                             ((lane & 31) ^ (r & 15)) * 16;
+            __builtin_amdgcn_global_load_lds((gbl_vptr)gp, (lds_vptr)(lds + b * ABUF + r0 * PITCH), 16, 0, 0);
         }
-        nops += RPW;
+        nops += RPW / 2;
     };
     auto dma_idx = [&](long long t) __attribute__((always_inline)) {
         const int lane = fresh_lane();
@@ -3971,19 +4010,22 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
         for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const char* ab = lds + b * ABUF + i16 * PITCH + 16 * g;
+        // row 16 rb + i16, logical chunk 4q + g at physical chunk (4q + g) ^ i16 = 4q ^ (g ^ i16): the 16 lanes of each
+        // ds_read_b128 group on 16 different 16-B bank groups
+        const char* ab = lds + b * ABUF + i16 * PITCH;
+        const int sv = 16 * (g ^ i16);
         // fragments of k-steps q and q+1 in alternating registers; one k-step per scheduling region (the fully
         // unrolled loop otherwise hoists all the fragment loads and takes the kernel past 256 VGPRs)
         bf16x8 x[2][4];
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb) x[0][rb] = *reinterpret_cast<const bf16x8*>(ab + 16 * rb * PITCH);
+        for (int rb = 0; rb < 4; ++rb) x[0][rb] = *reinterpret_cast<const bf16x8*>(ab + 16 * rb * PITCH + sv);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int cu = q & 1;
             if (q + 1 < 8) {
 #pragma unroll
                 for (int rb = 0; rb < 4; ++rb)
-                    x[cu ^ 1][rb] = *reinterpret_cast<const bf16x8*>(ab + 16 * rb * PITCH + 64 * (q + 1));
+                    x[cu ^ 1][rb] = *reinterpret_cast<const bf16x8*>(ab + 16 * rb * PITCH + ((64 * (q + 1)) ^ sv));
             }
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb)
