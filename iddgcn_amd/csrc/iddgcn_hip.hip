@@ -2710,28 +2710,59 @@ __global__ __launch_bounds__(256) void distmult_heads_kernel(int n_nodes, int R,
                 const f32x4 prod = a * rho[u] * b[u];
                 sc[u] = group_sum<LPR>(prod[0] + prod[1] + prod[2] + prod[3]);
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (e[u] < 0) continue;
-                const float p = sigmoidf_(sc[u]);
-                if (sub == 0) {
-                    if (p_out) p_out[e[u]] = p;
-                    if (s_out) s_out[e[u]] = sc[u];
-                }
-                float g, lterm;
+            // the per-edge scalar chain (sigmoid, Keras BCE seed and loss term: two logf, two IEEE divisions, expf)
+            auto scalar_chain = [&](float sv, float yv, float& p, float& ds, float& lterm) __attribute__((always_inline)) {
+                p = sigmoidf_(sv);
+                float g;
                 if (y) {        // Keras BCE seed
                     const float pc = fminf(fmaxf(p, EPS_BCE), 1.0f - EPS_BCE);
                     const bool pass = (p >= EPS_BCE) && (p <= 1.0f - EPS_BCE);
-                    g = pass ? scale * (-(yy[u] / (pc + EPS_BCE)) + (1.0f - yy[u]) / (1.0f - pc + EPS_BCE)) : 0.f;
-                    lterm = -(yy[u] * logf(pc + EPS_BCE) + (1.0f - yy[u]) * logf(1.0f - pc + EPS_BCE));
+                    g = pass ? scale * (-(yv / (pc + EPS_BCE)) + (1.0f - yv) / (1.0f - pc + EPS_BCE)) : 0.f;
+                    lterm = -(yv * logf(pc + EPS_BCE) + (1.0f - yv) * logf(1.0f - pc + EPS_BCE));
                 } else {        // prediction seed: gradient of scale * sum_e p_e
                     g = scale;
                     lterm = p;
                 }
-                const float ds = g * p * (1.0f - p);
-                if (sub == 0) {
-                    if (ds_out) ds_out[e[u]] = ds;
-                    lacc += lterm;
+                ds = g * p * (1.0f - p);
+            };
+            // one head per wave (LPR = 64): the group's U scores are wave-uniform, so lane u runs edge u's scalar chain
+            // and the results are broadcast (readlane) — one chain per group instead of U redundant ones; the same
+            // function of the same inputs, so p, s, ds and the loss terms are bitwise those of the redundant form
+            float ds_l = 0.f, lt_l = 0.f;
+            if constexpr (LPR == 64) {
+                float sv = sc[0], yv = yy[0];
+                long long el = e[0];
+#pragma unroll
+                for (int u = 1; u < U; ++u) {
+                    sv = sub == u ? sc[u] : sv;
+                    yv = sub == u ? yy[u] : yv;
+                    el = sub == u ? e[u] : el;
+                }
+                float p_l;
+                scalar_chain(sv, yv, p_l, ds_l, lt_l);
+                if (sub < U && el >= 0) {
+                    if (p_out) p_out[el] = p_l;
+                    if (s_out) s_out[el] = sv;
+                    if (ds_out) ds_out[el] = ds_l;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (e[u] < 0) continue;
+                float ds, lterm;
+                if constexpr (LPR == 64) {
+                    ds = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ds_l), u));
+                    lterm = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lt_l), u));
+                    if (sub == 0) lacc += lterm;
+                } else {
+                    float p;
+                    scalar_chain(sc[u], yy[u], p, ds, lterm);
+                    if (sub == 0) {
+                        if (p_out) p_out[e[u]] = p;
+                        if (s_out) s_out[e[u]] = sc[u];
+                        if (ds_out) ds_out[e[u]] = ds;
+                        lacc += lterm;
+                    }
                 }
                 f32x4 dx = (ds * rho[u]) * a;
                 dx = dx * (b[u] * (1.0f - b[u]));
