@@ -471,8 +471,16 @@ class Engine:
             S = P[f"S{l + 1}"]
             ops.alpha_fwd(ws.X[l - 1], P[f"Wa{l + 1}"], P[f"ba{l + 1}"], ws.Ssm[l], ws.W[l])
             ops.gather_rows(ws.W[l], ed.h, ws.Wedge[l])
-            ops.rowgemm(ws.X[l - 1], S, ws.X[l], coef=ws.W[l], V=ws.P[l], v_rel_stride=N * D,
-                        act=L.ACT_SIGMOID, **pr)
+            if R > 2 and D == 256:
+                # head chain at node level, many relations: X^{l-1}·S into ES1 (free once the layer-1 combines above
+                # have read it), then the row-aligned combine sigma(Y + sum_r W_r P_r) — every node row's own 8 V rows,
+                # which the fused GEMM's gathered-V epilogue (built for tail runs) stages through its capped slabs
+                # one row at a time: config 5 4.5 ms -> 0.6 + 1.9 ms
+                ops.rowgemm(ws.X[l - 1], S, ws.ES1, **pr)
+                ops.combine(ws.ES1, ws.W[l], ws.P[l], ws.X[l])
+            else:
+                ops.rowgemm(ws.X[l - 1], S, ws.X[l], coef=ws.W[l], V=ws.P[l], v_rel_stride=N * D,
+                            act=L.ACT_SIGMOID, **pr)
             with self._mark("tail_fwd_gemm"):
                 ops.rowgemm(ws.xt[l - 1], S, ws.xt[l], coef=ws.Wedge[l], V=ws.P[l], v_idx=ed.t,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID,

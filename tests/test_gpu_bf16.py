@@ -174,6 +174,28 @@ def test_rowgemm_bf16_backward_dsigmoid(precision, cuda):
     assert torch.equal(Xi, C)
 
 
+@pytest.mark.parametrize("precision", ["exact", "bf16"])
+def test_rowgemm_bf16_gathered_rows(precision, cuda):
+    """bf16 A rows gathered by a_idx (the v3 kernel's two-rows-per-DMA staging takes each half-wave's row from its own
+    index, round 5): random, repeated and ragged indices, plain and sigma' forms, within the output's bf16 rounding of
+    the fp64 reference on the same bf16 inputs (the weights rounded too for precision "bf16")."""
+    g = torch.Generator().manual_seed(21)
+    Msrc, M = 5000, 20_003
+    A = bf(torch.rand(Msrc, D, generator=g)).to(cuda)
+    idx = torch.randint(0, Msrc, (M,), generator=g).int().to(cuda)
+    idx[100:140] = 7                                   # a run of one repeated row
+    S = (torch.randn(D, D, generator=g, dtype=torch.float64) / 16).to(cuda)
+    Sd = rb(S) if precision == "bf16" else S.float().double()
+    X = bf(torch.rand(M, D, generator=g)).to(cuda)
+    Ag = A.double()[idx.long()]
+    for act, aux, ref in ((L.ACT_NONE, None, Ag @ Sd), (L.ACT_SIGMOID, None, torch.sigmoid(Ag @ Sd)),
+                          (L.ACT_DSIGMOID, X, (Ag @ Sd) * X.double() * (1 - X.double()))):
+        C = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
+        ops.rowgemm(A, S.float(), C, a_idx=idx, act=act, aux=aux, precision=precision)
+        err = (C.double() - ref).abs()
+        assert (err <= 2 ** -8 * ref.abs() + 1e-5 * ref.abs().max()).all(), (act, err.max().item())
+
+
 def test_rowgemm_bf16_precision_refused_on_fp32_tables(cuda):
     """IDDGCN_GEMM_BF16 is a bf16-table form: iddgcn_rowgemm_f32 refuses it (IDDGCN_E_BAD_ARG, nothing launched)."""
     A = torch.rand(64, D, device=cuda)

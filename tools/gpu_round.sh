@@ -8,7 +8,7 @@ TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="bench.py --no-cpu-baseline --no-other-mode --also none --steps 5 --warmup 2"
+BENCH="bench.py --no-cpu-baseline --no-other-mode --no-fold0-auc --also none --steps 5 --warmup 2"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${2:-} > "$OUT/gpu_tests.log" 2>&1 &&
 timeout -k 10 300 python -u bench.py > "$OUT/bench.json.log" 2>&1 &&
 timeout -k 10 120 python -u $BENCH > "$OUT/bench_profiled_cmd.json.log" 2>&1 &&
