@@ -72,6 +72,9 @@ def main():
                                                           scale=1.0 / (T * N)),
                            lambda: [ws.xt[0], ws.dOn_b, ws.loss_slab, ws.drel_slab]),
     }
+    x1 = torch.empty_like(ws.xt[0])
+    cases["layer-1 tail combine"] = (lambda: ops.combine(ws.ES1, ws.Wedge[0], ws.P[0], x1, y_idx=ed.t, v_idx=ed.t),
+                                     lambda: [x1])
     cases["gather_rows W[h]"] = (lambda: ops.gather_rows(ws.W[1], ed.h, ws.Wedge[0]), lambda: [ws.Wedge[0]])
     cases["head_dz"] = (lambda: ops.head_dz(ws.Ssm[1], ws.W[1], ed.hptr, ed.hperm, ws.dWedge, ws.dwh, ws.dz),
                         lambda: [ws.dz])
