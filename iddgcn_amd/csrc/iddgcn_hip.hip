@@ -3852,16 +3852,10 @@ constexpr int LDSB = NBUF * ABUF + NW * WREG;            // 153,600 B
 static_assert(LDSB <= 160 * 1024, "LDS budget");
 }  // namespace fg8
 
-// XS = false (round 5): the layer-1 tail combine of the same mode, x^1[e] = act(Y[v_idx[e]] + sum_r coef[e][r]
-// V_r[v_idx[e]]) with Y = E S^1 (p.aux, a node table gathered like V): no A tile, no x S MFMAs; the tile's Y rows
-// are DMA'd beside its V slots and added to the combine's accumulators (iddgcn_combine_bf16 at R = 8; it replaces
-// run_combine256_kernel's 2048 VALU FMAs per edge row).
-template <bool HL, bool XS = true>
+template <bool HL>
 __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     using namespace fg8;
-    constexpr int NB = XS ? NBUF : 0;                    // A buffers
-    constexpr int WR = XS ? WREG : WREG + CAPS * 128;    // per-wave region (+ the slots' Y rows: [slot][32] fp32)
-    __shared__ __attribute__((aligned(16))) char lds[NB * ABUF + NW * WR];
+    __shared__ __attribute__((aligned(16))) char lds[LDSB];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // per-lane index math inside the tile loop starts from an opaque copy of the lane id, so the compiler recomputes
@@ -3874,8 +3868,7 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     };
     const int i16 = lane & 15, g = lane >> 4;
     const int c0 = wave * 32;
-    char* wreg = lds + NB * ABUF + wave * WR;
-    char* ysl = wreg + WREG;                             // (XS = false) the staged slots' Y rows
+    char* wreg = lds + NBUF * ABUF + wave * WREG;
     int* idxw = reinterpret_cast<int*>(wreg + WIDX);
     int* tailw = reinterpret_cast<int*>(wreg + WTAIL);
     float* coefw = reinterpret_cast<float*>(wreg + WCOEF);
@@ -3891,20 +3884,18 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     auto clampe = [&](long long e) __attribute__((always_inline)) { return e > Mlast ? Mlast : e; };
 
     // weights: lane (g, i16), column block cb, k-step q: S[32q + 8g + j][c0 + 16cb + i16], j < 8, as bf16 hi + lo
-    bf16x8 wh[2][XS ? 8 : 1], wl[2][(HL && XS) ? 8 : 1];
-    if constexpr (XS) {
+    bf16x8 wh[2][8], wl[2][HL ? 8 : 1];
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
+    for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
+        for (int q = 0; q < 8; ++q)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float w = p.B[(32 * q + 8 * g + j) * D + c0 + 16 * cb + i16];
-                    const __bf16 hi = (__bf16)w;
-                    wh[cb][q][j] = hi;
-                    if constexpr (HL) wl[cb][q][j] = (__bf16)(w - (float)hi);
-                }
-    }
+            for (int j = 0; j < 8; ++j) {
+                const float w = p.B[(32 * q + 8 * g + j) * D + c0 + 16 * cb + i16];
+                const __bf16 hi = (__bf16)w;
+                wh[cb][q][j] = hi;
+                if constexpr (HL) wl[cb][q][j] = (__bf16)(w - (float)hi);
+            }
 
     // vector-memory ops this wave has issued (wave-uniform): a wait for "op k and everything older" is
     // s_waitcnt vmcnt(nops - k) (ops complete in issue order; LDS-DMA, loads and stores count alike)
@@ -3912,7 +3903,6 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     // A(t): the wave's 8 rows, two per full-wave DMA: lane i -> row r0 + (i >> 5), LDS chunk i & 31 of that row's slot,
     // global chunk (i & 31) ^ (row & 15) (the swizzle that makes the fragment reads below conflict-free without a pad)
     auto dma_A = [&](long long t, int b) __attribute__((always_inline)) {
-        if constexpr (!XS) return;
         const int lane = fresh_lane();
 #pragma unroll
         for (int j = 0; j < RPW / 2; ++j) {
@@ -3953,15 +3943,6 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
                                              16, 0, 0);
         }
         nops += un;
-        if constexpr (!XS) {
-            // the staged slots' Y rows (this wave's 32 columns): lane l -> slot l >> 3, 16-B group l & 7, one DMA
-            const int ys = lane >> 3;
-            const long long ytail = tailw[ys < un ? ys : 0];
-            if (lane < 8 * un)
-                __builtin_amdgcn_global_load_lds((gbl_vptr)(p.aux + ytail * D + c0 + 4 * (lane & 7)), (lds_vptr)ysl, 16, 0,
-                                                 0);
-            nops += 1;
-        }
         const long long clast = (long long)p.M * R - 4;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -3994,14 +3975,6 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
                     const int tail = __builtin_amdgcn_readfirstlane(tailw[b0 + k]);
                     __builtin_amdgcn_global_load_lds((gbl_vptr)(p.V + (long long)tail * D + loff),
                                                      (lds_vptr)(vsl + k * SLOTB), 16, 0, 0);
-                }
-                if constexpr (!XS) {
-                    const int nk = u - b0 < CAPS ? u - b0 : CAPS;
-                    const int ys = lane >> 3;
-                    const long long ytail = tailw[b0 + (ys < nk ? ys : 0)];
-                    if (lane < 8 * nk)
-                        __builtin_amdgcn_global_load_lds((gbl_vptr)(p.aux + ytail * D + c0 + 4 * (lane & 7)),
-                                                         (lds_vptr)ysl, 16, 0, 0);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
@@ -4040,20 +4013,6 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
                     }
                 }
             }
-            if constexpr (!XS) {
-                // + Y[tail] for the rows whose slot is in this block: lane (g, i16) holds row 16 rb + i16 at columns
-                // 16 cb + 4 g .. +3 of the wave's 32
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int rb = 0; rb < 4; ++rb) {
-                    const int sl = slot[rb] - b0;
-                    if (sl >= 0 && sl < CAPS) {
-#pragma unroll
-                        for (int cb = 0; cb < 2; ++cb)
-                            accP[rb][cb] += ld4(reinterpret_cast<const float*>(ysl + sl * 128) + 16 * cb + 4 * g);
-                    }
-                }
-            }
         }
     };
     // finish(t, q): block q = (rb, cb) of the previous tile t: activation, bf16, one 8-B store per lane
@@ -4082,12 +4041,6 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
         for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (!XS) {             // the combine alone: the previous tile's activation and stores
-            if (tprev >= 0) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) finish(tprev, q);
-            }
-        } else {
         // row 16 rb + i16, logical chunk 4q + g at physical chunk (4q + g) ^ i16 = 4q ^ (g ^ i16): the 16 lanes of each
         // ds_read_b128 group on 16 different 16-B bank groups
         const char* ab = lds + b * ABUF + i16 * PITCH;
@@ -4115,7 +4068,6 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
             // the previous tile's block q: its VALU and store issue in the shadow of this k-step's MFMAs
             if (tprev >= 0) finish(tprev, q);
             __builtin_amdgcn_sched_barrier(0);
-        }
         }
     };
 
@@ -4157,15 +4109,6 @@ __global__ __launch_bounds__(512) void fwd_gather8_bf16_kernel(RowGemmP p) {
     combine();
 #pragma unroll
     for (int q = 0; q < 8; ++q) finish(t_end - 1, q);
-}
-
-// the layer-1 tail combine of the bf16-feature mode at R = 8 (fwd_gather8_bf16_kernel<true, false>: Y = p.aux)
-void launch_combine8(hipStream_t st, RowGemmP p) {
-    const long long ntiles = ((long long)p.M + fg8::TR - 1) / fg8::TR;
-    long long nb = ntiles < 512 ? ntiles : 512;          // 99 VGPRs, 58 KiB of LDS: two workgroups per CU
-    p.tiles_per_block = (int)((ntiles + nb - 1) / nb);
-    nb = (ntiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    hipLaunchKernelGGL((fwd_gather8_bf16_kernel<true, false>), dim3((unsigned)nb), dim3(512), 0, st, p);
 }
 
 // config-5 forward form (R = 8, per-edge coefficients, gathered V rows, bf16 A / C): one persistent workgroup per CU
@@ -4821,26 +4764,6 @@ int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const v
 
 int iddgcn_combine_bf16(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,
                         const float* V, long long v_rel_stride, void* out) {
-    // R = 8, D = 256, 16-B aligned tables (the DMAs move 16-B pieces): the combine on MFMAs (fwd_gather8_bf16_kernel
-    // without its x S part, round 5); otherwise the VALU run combine
-    auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
-    if (d == 256 && R == 8 && M > 0 && Y && idx && coef && V && out && al16(Y) && al16(coef) && al16(V) && al16(out) &&
-        (v_rel_stride & 3) == 0) {
-        RowGemmP p{};
-        p.M = M;
-        p.R = 8;
-        p.coef = coef;
-        p.V = V;
-        p.v_idx = idx;
-        p.v_rel_stride = v_rel_stride;
-        p.v_row_stride = 256;
-        p.C = (float*)out;
-        p.act = IDDGCN_ACT_SIGMOID;
-        p.aux = Y;
-        p.precision = IDDGCN_GEMM_EXACT_F32;
-        launch_combine8((hipStream_t)stream, p);
-        return launch_status();
-    }
     return run_combine_out<true, false>(stream, M, d, R, Y, idx, coef, V, v_rel_stride, out);
 }
 
