@@ -662,7 +662,13 @@ class Engine:
             if b > a:
                 ops.alpha_fwd(ws.X[l - 1][a:b], P[f"Wa{l + 1}"], P[f"ba{l + 1}"], ws.Ssm[l][a:b], ws.W[l][a:b])
             sh.all_gather(ws.W[l])
-            if b > a:
+            if b > a and R > 2 and D == 256 and ws.train:
+                # as in forward(): the GEMM into a free N x D table (ES1 is still needed by the layer-1 tail combine
+                # below; the head-seed buffer dOn_b is free until the backward), then the row-aligned combine
+                tmp = ws.dOn_b[a:b]
+                ops.rowgemm(ws.X[l - 1][a:b], P[f"S{l + 1}"], tmp, **pr)
+                ops.combine(tmp, ws.W[l][a:b], ws.P[l], ws.X[l][a:b], v_idx=idx)
+            elif b > a:
                 ops.rowgemm(ws.X[l - 1][a:b], P[f"S{l + 1}"], ws.X[l][a:b], coef=ws.W[l][a:b], V=ws.P[l], v_idx=idx,
                             v_rel_stride=N * D, act=L.ACT_SIGMOID, **pr)
         x3 = sh.all_gather(ws.X[2], async_op=True)
