@@ -109,8 +109,12 @@ def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4, edge_mfma="hilo"):
     nbytes = {"tail_fwd_gemm": 2.0 * eb * D * T + 4.0 * R * T + 4.0 * T + 4.0 * R * N * D,
               "tail_bwd_gemm": 3.0 * eb * D * T,
               "tail_bwd_rec_gemm": 2.0 * eb * D * T + 4.0 * R * T + 4.0 * T + 4.0 * (R + 1) * N * D,
-              "tail_dS_tn": 2.0 * eb * D * T}[name]
-    if eb == 2:
+              "tail_dS_tn": 2.0 * eb * D * T,
+              "tail_bwd_sigma_tn": 3.0 * eb * D * T}[name]
+    if name == "tail_bwd_sigma_tn":
+        # one pass, both GEMMs (bf16 tables, hi + lo weights): sigma' 2 bf16 products per term, the TN 1
+        flops, hw_flops, peak_f = 2 * flops, 3 * flops, MFMA_F16_PEAK_TFLOPS
+    elif eb == 2:
         hw_flops, peak_f = (1 if edge_mfma == "bf16" else 2) * flops, MFMA_F16_PEAK_TFLOPS
     elif gemm == "bf16x3":
         hw_flops, peak_f = 6 * flops, MFMA_F16_PEAK_TFLOPS

@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
 # a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 10
+ABI_VERSION = 11
 ROWGEMM_BATCH = 25          # IDDGCN_ROWGEMM_BATCH: entries per iddgcn_rowgemm_batched_f32 call
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
@@ -80,6 +80,8 @@ SIGNATURES = {
     # bf16-feature mode
     "iddgcn_rowgemm_bf16": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
     "iddgcn_gemm_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
+    "iddgcn_sigma_tn_ranges": (ci, [cll]),
+    "iddgcn_sigma_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_combine_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_combine_planes_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_gemm_tn_planes_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),

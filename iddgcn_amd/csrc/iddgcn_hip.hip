@@ -1705,6 +1705,241 @@ __global__ __launch_bounds__(512) void gemm_tn256_bf16t_kernel(long long M, long
         }
 }
 
+// ---- sigma' backward + dS TN in one pass over the bf16 edge tables (round 5, config 5) --------------------------
+// A layer's edge backward reads do^l and x^{l-1} twice: dS^l = x^{l-1,T} do^l (gemm_tn256_bf16t_kernel, 51.2 GB per
+// config-5 launch) and dx^{l-1} = (do^l S^{l,T}) x^{l-1}(1 - x^{l-1}) written over x^{l-1} (the v3 sigma' kernel,
+// 76.8 GB); both run at the box's HBM ceiling.  This kernel reads each tile once: 76.8 GB for both.
+// Workgroup pair per row range (column half h = 0, 1; blockIdx 8 apart: the same XCD, so the pair's second read of a
+// do tile is an L2 hit).  Workgroup h reads do (all columns) and x[:, half h] only, and writes dx[:, half h] only (the
+// same bytes of x), so the in-place write never meets the other workgroup's reads:
+//   * dx[:, half h]: wave w owns columns c0 = 128h + 16w .. +15; the weights S[c][k] (S^T) as a bf16 hi + lo pair are
+//     operand A of v_mfma_f32_16x16x32_bf16 (64 VGPRs), the do rows operand B (ds_read_b128); lane l ends with row
+//     l & 15 (+16) at columns c0 + 4(l >> 4) .. +3; epilogue x(1 - x) from the x tile, bf16 8-B stores.  Per 32 k:
+//     hi then lo into one accumulator, as the v3 kernel's per-16-k pair.
+//   * dS[half h rows, :]: wave w owns dS rows 128h + 32(w & 3) .. +31 (x columns) x columns 128(w >> 2) .. +127 (four
+//     32 x 32 tiles, 64 VGPRs), v_mfma_f32_32x32x16_bf16 on ds_read_b64_tr_b16 fragments (8 rows of one column), as
+//     gemm_tn256_bf16t_kernel; per-range partials in slab[range] (rows of half h), summed by reduce_slabs.
+// Tiles of 32 rows, three buffers [do: 32 x 512 B | x half: 32 x 256 B], filled by full-wave LDS-DMAs (two do rows or
+// four x half rows per instruction, 3 per wave per tile).  16-B chunk c of row r sits at c ^ stn_sw(r): the sixteen
+// lanes of each ds_read_b128 group (rows l & 15, chunk 4q + (l >> 4)) hit 16 distinct chunks mod 16 (stn_sw maps rows
+// {0-3, 12-15} onto pairs {2m, 2m + 1}), and the four rows of a transposed read's 32-lane half land on the four
+// 64-B quarters of the bank row (stn_sw(r) >> 2 = r & 3).
+namespace stn {
+constexpr int D = 256, TR = 32, DPT = 512, XPT = 256, DOB = TR * DPT, XB = TR * XPT, BUF = DOB + XB,
+              PD = 2, NBUF = PD + 1;     // 3 / 4 tiles ahead: 21.2 / 21.5 vs 20.8 ms
+}  // namespace stn
+__device__ __forceinline__ int stn_sw(int r) { return (4 * (r & 3)) ^ ((0x1320 >> (4 * ((r >> 2) & 3))) & 15); }
+// ds_read_b64_tr_b16 issued in asm (the caller waits for it with an explicit lgkmcnt tied to the result)
+__device__ __forceinline__ void tr_read_asm(v4s16& d, const char* p) {
+    const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(d) : "v"(a) : "memory");
+}
+__global__ __launch_bounds__(512) void sigma_tn_bf16_kernel(long long M, int tiles_per_block, int n_ranges,
+                                                            const __bf16* __restrict__ dO, __bf16* __restrict__ X,
+                                                            const float* __restrict__ S, float* __restrict__ slab) {
+    using namespace stn;
+    static_assert(NBUF * BUF <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * BUF];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bx = blockIdx.x;
+    const int half = (bx >> 3) & 1;
+    const int range = ((bx >> 4) << 3) | (bx & 7);
+    if (range >= n_ranges) return;
+    const long long ntiles = (M + TR - 1) / TR;
+    const long long t_beg = (long long)range * tiles_per_block;
+    long long t_end = t_beg + tiles_per_block;
+    if (t_end > ntiles) t_end = ntiles;            // a range past the table still writes its (zero) partial
+    const int i16 = lane & 15, g = lane >> 4;
+    const int c0 = 128 * half + 16 * wave;
+    const int swi = stn_sw(i16);
+
+    // S^T as operand A: column c0 + i16, k = 32q + 8g + e; W = hi + lo, hi = bf16(W), lo = bf16(W - hi)
+    bf16x8 whi[8], wlo[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float w = S[(c0 + i16) * D + 32 * q + 8 * g + e];
+            whi[q][e] = (__bf16)w;
+            wlo[q][e] = (__bf16)(w - (float)whi[q][e]);
+        }
+    f32x16 tacc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) tacc[j][k] = 0.f;
+
+    // rows of tile t into buffer bb; returns the LDS-DMA count (wave-uniform).  Rows past M (the table's last tile)
+    // are zeros in both operands (0 x whatever-bits could be NaN in the TN).
+    auto stage = [&](long long t, int bb) __attribute__((always_inline)) -> int {
+        char* base = lds + bb * BUF;
+        const long long t0 = t * TR;
+        if (t0 + TR <= M) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = 4 * wave + 2 * j + (lane >> 5);
+                const int c = (lane & 31) ^ stn_sw(r);
+                __builtin_amdgcn_global_load_lds((gbl_vptr)(dO + (t0 + r) * D + c * 8),
+                                                 (lds_vptr)(base + (4 * wave + 2 * j) * DPT), 16, 0, 0);
+            }
+            const int r = 4 * wave + (lane >> 4);
+            const int c = (lane & 15) ^ stn_sw(r);
+            __builtin_amdgcn_global_load_lds((gbl_vptr)(X + (t0 + r) * D + 128 * half + c * 8),
+                                             (lds_vptr)(base + DOB + 4 * wave * XPT), 16, 0, 0);
+            return 3;
+        }
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = 4 * wave + j;
+            const long long e = t0 + r;
+            if (e < M) {
+                if (lane < 32)
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)(dO + e * D + (lane ^ stn_sw(r)) * 8),
+                                                     (lds_vptr)(base + r * DPT), 16, 0, 0);
+                if (lane < 16)
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)(X + e * D + 128 * half + (lane ^ stn_sw(r)) * 8),
+                                                     (lds_vptr)(base + DOB + r * XPT), 16, 0, 0);
+                n += 2;
+            } else {
+                if (lane < 32) st4(reinterpret_cast<float*>(base + r * DPT) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                if (lane < 16) st4(reinterpret_cast<float*>(base + DOB + r * XPT) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+            }
+        }
+        return n;
+    };
+    // transposed-read lane geometry (gemm_tn256_bf16t_kernel's): rows 8(l >> 5) + xs (+4: second read), logical chunk
+    // 4 blk + colq of the 32-column block blk, byte 8(l & 1) in it
+    const int xs = (lane >> 2) & 3;
+    const int colq = 2 * ((lane >> 4) & 1) + ((lane & 3) >> 1);
+    const int cb = 8 * (lane & 1);
+    const int wb = wave & 3, cbase = 4 * (wave >> 2);
+    auto mfma_tile = [&](int bb, f32x4 (&sacc)[2]) __attribute__((always_inline)) {
+        const char* dob = lds + bb * BUF;
+        const char* xb = dob + DOB;
+        // sigma': do rows x S^T, k-step q's fragments of both row blocks loaded one step ahead
+        sacc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        sacc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bf16x8 bv[2][2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+            bv[0][rb] = *reinterpret_cast<const bf16x8*>(dob + (16 * rb + i16) * DPT + 16 * (g ^ swi));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int cu = q & 1;
+            if (q + 1 < 8) {
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb)
+                    bv[cu ^ 1][rb] = *reinterpret_cast<const bf16x8*>(dob + (16 * rb + i16) * DPT +
+                                                                      16 * ((4 * (q + 1) + g) ^ swi));
+            }
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                sacc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[q], bv[cu][rb], sacc[rb], 0, 0, 0);
+                sacc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[q], bv[cu][rb], sacc[rb], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // dS: x[:, half]^T do, two 16-row k-steps x four column tiles.  The transposed reads are issued in asm with an
+        // explicit wait: hipcc guards the builtin form (no alias information) with a vmcnt(0), i.e. it drained the
+        // tile t + 2 DMAs issued at the top of the iteration
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int ra = 16 * s + 8 * (lane >> 5) + xs, rq = ra + 4;
+            v4s16 ta[2], tb[4][2];
+            tr_read_asm(ta[0], xb + ra * XPT + 16 * ((4 * wb + colq) ^ stn_sw(ra)) + cb);
+            tr_read_asm(ta[1], xb + rq * XPT + 16 * ((4 * wb + colq) ^ stn_sw(rq)) + cb);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int blk = cbase + j;
+                tr_read_asm(tb[j][0], dob + ra * DPT + 16 * ((4 * blk + colq) ^ stn_sw(ra)) + cb);
+                tr_read_asm(tb[j][1], dob + rq * DPT + 16 * ((4 * blk + colq) ^ stn_sw(rq)) + cb);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(ta[0]), "+v"(ta[1]), "+v"(tb[0][0]), "+v"(tb[0][1]), "+v"(tb[1][0]), "+v"(tb[1][1]),
+                           "+v"(tb[2][0]), "+v"(tb[2][1]), "+v"(tb[3][0]), "+v"(tb[3][1])::"memory");
+            const bf16x8 a = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ta[0], ta[1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                tacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    a, __builtin_bit_cast(bf16x8, __builtin_shufflevector(tb[j][0], tb[j][1], 0, 1, 2, 3, 4, 5, 6, 7)),
+                    tacc[j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // epilogue: dx = acc x(1 - x) (the v3 kernel's order), bf16 over the x rows of this half; rows past M dropped by the
+    // buffer range.  Returns its store count.
+    auto epilogue = [&](long long t, int bb, const f32x4 (&sacc)[2]) __attribute__((always_inline)) -> int {
+        const char* xb = lds + bb * BUF + DOB;
+        const long long row0 = t * TR;
+        const long long left = M - row0;
+        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 2);
+        const __amdgpu_buffer_rsrc_t rc =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(X) + row0 * D * 2, (short)0, nbytes, 0x00020000);
+        const int xc = (2 * wave + (g >> 1)) ^ swi;          // x half chunk of columns 16w + 4g .. +3 (row & 15 = i16)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const int r = 16 * rb + i16;
+            const f32x4 x = bf4_to_f32(*reinterpret_cast<const bf16x4*>(xb + r * XPT + 16 * xc + 8 * (g & 1)));
+            f32x4 v = sacc[rb];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = v[q] * (x[q] * (1.0f - x[q]));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, f32_to_bf4(v)), rc, (r * D + c0 + 4 * g) * 2,
+                                                  0, 0);
+        }
+        return 2;
+    };
+
+    // PD tiles in flight ahead of the one computed; per iteration it = t - t_beg the wave issues the DMAs of tile t + PD
+    // and then the stores of tile t (the prologue counts as iterations -PD .. -1, DMAs only), so the ops younger than
+    // tile t + 1's DMAs are the stores of their iteration and everything of the PD - 1 iterations after it
+    if (t_beg < t_end) {
+        int dc[PD], sc[PD];
+#pragma unroll
+        for (int k = 0; k < PD; ++k) {
+            dc[k] = t_beg + k < t_end ? stage(t_beg + k, k) : 0;
+            sc[k] = 0;
+        }
+        int younger = 0;
+#pragma unroll
+        for (int k = 1; k < PD; ++k) younger += dc[k];
+        wait_vm(younger);                          // tile t_beg landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        f32x4 sacc[2];
+        int b = 0;
+        for (long long t = t_beg; t < t_end; ++t) {
+            const int it = (int)(t - t_beg);
+            const int slot = it % PD;               // iteration it - PD's entries, no longer needed
+            dc[slot] = t + PD < t_end ? stage(t + PD, (b + PD) % NBUF) : 0;
+            mfma_tile(b, sacc);
+            sc[slot] = epilogue(t, b, sacc);
+            int y = sc[(it + 1) % PD];              // iteration it + 1 - PD: issued tile t + 1's DMAs, then stores
+#pragma unroll
+            for (int j = 2; j <= PD; ++j) {
+                const int s2 = (it + j) % PD;       // iterations it + 2 - PD .. it
+                y += dc[s2] + sc[s2];
+            }
+            wait_vm(y);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            b = (b + 1) % NBUF;
+        }
+    }
+    float* out = slab + (long long)range * D * D;
+    const int i = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int row = 128 * half + 32 * wb + (k & 3) + 8 * (k >> 2) + 4 * h;
+            out[row * D + 32 * (cbase + j) + i] = tacc[j][k];
+        }
+}
+
 // ---------------------------------------------------------------------------
 // bf16x3 operands (IDDGCN_GEMM_BF16X3), D = 256.  Every fp32 operand value x is the EXACT sum of three
 // bf16 values:  b0 = bf16_rne(x), b1 = bf16_rne(x - b0), b2 = (x - b0) - b1.  Each difference is exact in
@@ -4759,6 +4994,34 @@ int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const v
     if (rc) return rc;
     const long long n = (long long)d * d;
     launch_reduce_slabs(st, n_blocks, n, slab, C, accumulate, 1.0f);
+    return launch_status();
+}
+
+int iddgcn_sigma_tn_ranges(long long M) {
+    const long long nt = (M + stn::TR - 1) / stn::TR;
+    long long nr = nt < 128 ? nt : 128;
+    if (nr < 1) nr = 1;
+    const long long tpb = (nt + nr - 1) / nr > 0 ? (nt + nr - 1) / nr : 1;
+    nr = (nt + tpb - 1) / tpb;
+    return (int)((nr + 7) / 8 * 8 > 0 ? (nr + 7) / 8 * 8 : 8);
+}
+
+int iddgcn_sigma_tn_bf16(void* stream, long long M, int d, const void* dO, void* X, const float* S, float* slab,
+                         long long slab_floats, float* dS) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (M < 0 || !S || !slab || !dS || (M > 0 && (!dO || !X))) return IDDGCN_E_BAD_ARG;
+    if (((uintptr_t)dO & 15) || ((uintptr_t)X & 15)) return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const long long nt = (M + stn::TR - 1) / stn::TR;
+    const int nr = iddgcn_sigma_tn_ranges(M);
+    const long long tpb = nt > 0 ? (nt + nr - 1) / nr : 1;
+    const long long n = (long long)d * d;
+    if (slab_floats < nr * n) return IDDGCN_E_BAD_ARG;
+    hipLaunchKernelGGL(sigma_tn_bf16_kernel, dim3((unsigned)(2 * nr)), dim3(512), 0, st, M, (int)tpb, nr,
+                       (const __bf16*)dO, (__bf16*)X, S, slab);
+    int rc = launch_status();
+    if (rc) return rc;
+    launch_reduce_slabs(st, nr, n, slab, dS, 0, 1.0f);
     return launch_status();
 }
 

@@ -248,7 +248,8 @@ class Workspace:
         self.drel_slab = e(self.nb_dm * R * D)
         self.loss_slab = e(self.nb_dm)
         # partials of the edge TN, or of one batched launch of up to L.TN_BATCH node-level TNs
-        tn = max(ops.tn_blocks(T, D), min(256, L.TN_BATCH * ops.tn_blocks(N, D)), ops.tn_blocks(N, D))
+        tn = max(ops.tn_blocks(T, D), min(256, L.TN_BATCH * ops.tn_blocks(N, D)), ops.tn_blocks(N, D),
+                 ops.sigma_tn_slab_floats(T, D) // (D * D) if D == 256 else 1)
         self.tn_slab = e(tn * D * D)
         self.narrow_slab = e((ops.tn_narrow_blocks(N) + 1) * (D + 1) * R)
 
@@ -293,6 +294,7 @@ class Engine:
         if edge_mfma == "bf16" and features != "bf16":
             raise L.IddgcnError("edge_mfma='bf16' needs features='bf16' (bf16 edge tables)")
         self.edge_mfma = edge_mfma
+        self.fuse_sigma_tn = True
         if not 1 <= num_relations <= 8:
             raise L.IddgcnError("num_relations must be in [1, 8]")
         if gemm not in GEMM_MODES:
@@ -365,6 +367,13 @@ class Engine:
         """Precision of the edge-level row GEMMs (the tail chain's forward and sigma' backward): "bf16" with
         edge_mfma="bf16" (bf16 edge tables), else ``row_gemm``."""
         return "bf16" if self.edge_mfma == "bf16" else self.row_gemm
+
+    @property
+    def sigma_tn_fused(self):
+        """bf16 edge tables with hi + lo edge weights at D = 256 (config 5's mode): a layer's dS TN and sigma' backward
+        GEMM run as one pass over do^l and x^{l-1} (ops.sigma_tn, ABI 11) instead of two (``fuse_sigma_tn`` = False
+        keeps the two kernels, for A/B)."""
+        return self.fuse_sigma_tn and self.features == "bf16" and self.D == 256 and self.edge_mfma == "hilo"
 
     @property
     def use_planes(self):
@@ -544,7 +553,10 @@ class Engine:
             else:
                 ops.tail_seg_reduce(ed.tptr, None, ws.Wedge[l], do, Pl, ws.dP, ws.dWedge,
                                     dsum=ws.dES if l == 0 else None)
-            if l > 0:
+            if l > 0 and self.sigma_tn_fused:
+                with self._mark("tail_bwd_sigma_tn"):
+                    ops.sigma_tn(do, ws.xt[l - 1], Sl, G[f"S{l + 1}"], ws.tn_slab)
+            elif l > 0:
                 # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x), written over x^{l}
                 with self._mark("tail_dS_tn"):
                     ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)
@@ -725,7 +737,10 @@ class Engine:
             elif b > a:
                 ops.tail_seg_reduce(tptr, None, ws.Wedge[l], do, Pl[:, a:b], ws.dP[:, a:b], ws.dWedge,
                                     dsum=ws.dES[a:b] if l == 0 else None)
-            if l > 0:
+            if l > 0 and self.sigma_tn_fused:
+                with self._mark("tail_bwd_sigma_tn"):
+                    ops.sigma_tn(do, ws.xt[l - 1], Sl, G[f"S{l + 1}"], ws.tn_slab)
+            elif l > 0:
                 with self._mark("tail_dS_tn"):
                     ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)
                 with self._mark("tail_bwd_gemm"):

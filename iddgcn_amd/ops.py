@@ -199,6 +199,22 @@ def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False, precision="exact"):
     L.check(rc, "gemm_tn")
 
 
+def sigma_tn(dO, X, S, dS, slab):
+    """A layer's edge backward GEMM pair over bf16 tables in one pass (iddgcn_sigma_tn_bf16, ABI 11):
+    dS = X^T dO (overwritten) and X = (dO S^T) * X (1 - X) in place, hi + lo bf16 weights."""
+    M, D = X.shape
+    _req(X, _BF16, (M, D), "X")
+    _req(dO, _BF16, (M, D), "dO")
+    _req(S, _F32, (D, D), "S")
+    _req(dS, _F32, (D, D), "dS")
+    L.check(L.lib().iddgcn_sigma_tn_bf16(_stream(), M, D, _ptr(dO), _ptr(X), _ptr(S), _ptr(slab), slab.numel(),
+                                         _ptr(dS)), "sigma_tn")
+
+
+def sigma_tn_slab_floats(M, D=256):
+    return int(L.lib().iddgcn_sigma_tn_ranges(M)) * D * D
+
+
 def gemm_tn_batched(entries, slab, precision="exact"):
     """Up to L.TN_BATCH independent C (+)= A^T B, entries = [(A, B, C, accumulate), ...] (fp32, same D), in one
     launch (iddgcn_gemm_tn_batched_f32, ABI 5; one launch at D = 256 in the split and bf16x3 modes); slab holds

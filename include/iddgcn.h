@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 10
+#define IDDGCN_ABI_VERSION 11
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -316,6 +316,16 @@ int iddgcn_rowgemm_bf16(void* stream, const iddgcn_rowgemm_t* args);
 /* iddgcn_gemm_tn_f32 with bf16 A and B (slab / blocks / C as there). */
 int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const void* B, float* slab, int n_blocks,
                         float* C, int accumulate);
+
+/* ABI 11: a layer's whole edge backward GEMM pair in one pass over the bf16 tables (replaces iddgcn_gemm_tn_bf16 +
+ * iddgcn_rowgemm_bf16 with act DSIGMOID, the autodiff of IDDGCN.py:62-63,79 for x_t^{l-1} S^l):
+ *   dS = X^T dO  (dS[k][c] = sum_e X[e][k] dO[e][c]; overwritten)
+ *   X  = (dO S^T) * X (1 - X)  (in place: dx^{l-1} over x^{l-1}; hi + lo bf16 weights, fp32 accumulation)
+ * X and dO are M x 256 bf16 (16-B aligned), S 256 x 256 fp32; slab holds iddgcn_sigma_tn_ranges(M) * 256 * 256
+ * floats of partials (slab_floats is checked).  D = 256 only. */
+int iddgcn_sigma_tn_ranges(long long M);
+int iddgcn_sigma_tn_bf16(void* stream, long long M, int d, const void* dO, void* X, const float* S, float* slab,
+                         long long slab_floats, float* dS);
 
 /* The run form of iddgcn_combine_f32 (y_idx == v_idx = idx, coefficients per row) writing bf16 out. */
 int iddgcn_combine_bf16(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,
