@@ -81,7 +81,7 @@ SIGNATURES = {
     "iddgcn_rowgemm_bf16": (ci, [vp, ctypes.POINTER(RowGemmArgs)]),
     "iddgcn_gemm_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
     "iddgcn_sigma_tn_ranges": (ci, [cll]),
-    "iddgcn_sigma_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, vp, cll, vp]),
+    "iddgcn_sigma_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, vp, cll, vp, ci]),
     "iddgcn_combine_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_combine_planes_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_gemm_tn_planes_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),

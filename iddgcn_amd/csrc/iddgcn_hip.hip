@@ -1734,6 +1734,7 @@ __device__ __forceinline__ void tr_read_asm(v4s16& d, const char* p) {
     const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(d) : "v"(a) : "memory");
 }
+template <bool W1>
 __global__ __launch_bounds__(512) void sigma_tn_bf16_kernel(long long M, int tiles_per_block, int n_ranges,
                                                             const __bf16* __restrict__ dO, __bf16* __restrict__ X,
                                                             const float* __restrict__ S, float* __restrict__ slab) {
@@ -1762,7 +1763,7 @@ __global__ __launch_bounds__(512) void sigma_tn_bf16_kernel(long long M, int til
         for (int e = 0; e < 8; ++e) {
             const float w = S[(c0 + i16) * D + 32 * q + 8 * g + e];
             whi[q][e] = (__bf16)w;
-            wlo[q][e] = (__bf16)(w - (float)whi[q][e]);
+            wlo[q][e] = W1 ? (__bf16)0.f : (__bf16)(w - (float)whi[q][e]);
         }
     f32x16 tacc[4];
 #pragma unroll
@@ -1837,7 +1838,8 @@ __global__ __launch_bounds__(512) void sigma_tn_bf16_kernel(long long M, int til
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
                 sacc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(whi[q], bv[cu][rb], sacc[rb], 0, 0, 0);
-                sacc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[q], bv[cu][rb], sacc[rb], 0, 0, 0);
+                if constexpr (!W1)
+                    sacc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[q], bv[cu][rb], sacc[rb], 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -5007,7 +5009,7 @@ int iddgcn_sigma_tn_ranges(long long M) {
 }
 
 int iddgcn_sigma_tn_bf16(void* stream, long long M, int d, const void* dO, void* X, const float* S, float* slab,
-                         long long slab_floats, float* dS) {
+                         long long slab_floats, float* dS, int precision) {
     if (d != 256) return IDDGCN_E_BAD_DIM;
     if (M < 0 || !S || !slab || !dS || (M > 0 && (!dO || !X))) return IDDGCN_E_BAD_ARG;
     if (((uintptr_t)dO & 15) || ((uintptr_t)X & 15)) return IDDGCN_E_BAD_ARG;
@@ -5017,8 +5019,12 @@ int iddgcn_sigma_tn_bf16(void* stream, long long M, int d, const void* dO, void*
     const long long tpb = nt > 0 ? (nt + nr - 1) / nr : 1;
     const long long n = (long long)d * d;
     if (slab_floats < nr * n) return IDDGCN_E_BAD_ARG;
-    hipLaunchKernelGGL(sigma_tn_bf16_kernel, dim3((unsigned)(2 * nr)), dim3(512), 0, st, M, (int)tpb, nr,
-                       (const __bf16*)dO, (__bf16*)X, S, slab);
+    if (precision == IDDGCN_GEMM_BF16)
+        hipLaunchKernelGGL(sigma_tn_bf16_kernel<true>, dim3((unsigned)(2 * nr)), dim3(512), 0, st, M, (int)tpb, nr,
+                           (const __bf16*)dO, (__bf16*)X, S, slab);
+    else
+        hipLaunchKernelGGL(sigma_tn_bf16_kernel<false>, dim3((unsigned)(2 * nr)), dim3(512), 0, st, M, (int)tpb, nr,
+                           (const __bf16*)dO, (__bf16*)X, S, slab);
     int rc = launch_status();
     if (rc) return rc;
     launch_reduce_slabs(st, nr, n, slab, dS, 0, 1.0f);

@@ -370,10 +370,10 @@ class Engine:
 
     @property
     def sigma_tn_fused(self):
-        """bf16 edge tables with hi + lo edge weights at D = 256 (config 5's mode): a layer's dS TN and sigma' backward
-        GEMM run as one pass over do^l and x^{l-1} (ops.sigma_tn, ABI 11) instead of two (``fuse_sigma_tn`` = False
-        keeps the two kernels, for A/B)."""
-        return self.fuse_sigma_tn and self.features == "bf16" and self.D == 256 and self.edge_mfma == "hilo"
+        """bf16 edge tables at D = 256 (config 5's mode): a layer's dS TN and sigma' backward GEMM run as one pass over
+        do^l and x^{l-1} (ops.sigma_tn, ABI 11; the sigma' weights as ``edge_gemm`` takes them) instead of two
+        (``fuse_sigma_tn`` = False keeps the two kernels, for A/B)."""
+        return self.fuse_sigma_tn and self.features == "bf16" and self.D == 256
 
     @property
     def use_planes(self):
@@ -555,7 +555,7 @@ class Engine:
                                     dsum=ws.dES if l == 0 else None)
             if l > 0 and self.sigma_tn_fused:
                 with self._mark("tail_bwd_sigma_tn"):
-                    ops.sigma_tn(do, ws.xt[l - 1], Sl, G[f"S{l + 1}"], ws.tn_slab)
+                    ops.sigma_tn(do, ws.xt[l - 1], Sl, G[f"S{l + 1}"], ws.tn_slab, precision=self.edge_gemm)
             elif l > 0:
                 # dS^{l+1} (edge part) = x_t^{l}^T do ; do^{l} = (do S^T) * x(1-x), written over x^{l}
                 with self._mark("tail_dS_tn"):
@@ -739,7 +739,7 @@ class Engine:
                                     dsum=ws.dES[a:b] if l == 0 else None)
             if l > 0 and self.sigma_tn_fused:
                 with self._mark("tail_bwd_sigma_tn"):
-                    ops.sigma_tn(do, ws.xt[l - 1], Sl, G[f"S{l + 1}"], ws.tn_slab)
+                    ops.sigma_tn(do, ws.xt[l - 1], Sl, G[f"S{l + 1}"], ws.tn_slab, precision=self.edge_gemm)
             elif l > 0:
                 with self._mark("tail_dS_tn"):
                     ops.gemm_tn(ws.xt[l - 1], do, G[f"S{l + 1}"], ws.tn_slab, a_planes=pl, **pk)

@@ -199,16 +199,17 @@ def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False, precision="exact"):
     L.check(rc, "gemm_tn")
 
 
-def sigma_tn(dO, X, S, dS, slab):
+def sigma_tn(dO, X, S, dS, slab, precision="exact"):
     """A layer's edge backward GEMM pair over bf16 tables in one pass (iddgcn_sigma_tn_bf16, ABI 11):
-    dS = X^T dO (overwritten) and X = (dO S^T) * X (1 - X) in place, hi + lo bf16 weights."""
+    dS = X^T dO (overwritten) and X = (dO S^T) * X (1 - X) in place; the weights as a bf16 hi + lo pair, or with
+    precision "bf16" rounded to bf16 (as rowgemm's bf16 form)."""
     M, D = X.shape
     _req(X, _BF16, (M, D), "X")
     _req(dO, _BF16, (M, D), "dO")
     _req(S, _F32, (D, D), "S")
     _req(dS, _F32, (D, D), "dS")
     L.check(L.lib().iddgcn_sigma_tn_bf16(_stream(), M, D, _ptr(dO), _ptr(X), _ptr(S), _ptr(slab), slab.numel(),
-                                         _ptr(dS)), "sigma_tn")
+                                         _ptr(dS), L.GEMM_BF16 if precision == "bf16" else L.GEMM_EXACT_F32), "sigma_tn")
 
 
 def sigma_tn_slab_floats(M, D=256):

@@ -320,12 +320,13 @@ int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const v
 /* ABI 11: a layer's whole edge backward GEMM pair in one pass over the bf16 tables (replaces iddgcn_gemm_tn_bf16 +
  * iddgcn_rowgemm_bf16 with act DSIGMOID, the autodiff of IDDGCN.py:62-63,79 for x_t^{l-1} S^l):
  *   dS = X^T dO  (dS[k][c] = sum_e X[e][k] dO[e][c]; overwritten)
- *   X  = (dO S^T) * X (1 - X)  (in place: dx^{l-1} over x^{l-1}; hi + lo bf16 weights, fp32 accumulation)
+ *   X  = (dO S^T) * X (1 - X)  (in place: dx^{l-1} over x^{l-1}; bf16 hi + lo weights, or with precision
+ *        IDDGCN_GEMM_BF16 the weights rounded to bf16 as iddgcn_rowgemm_bf16 takes them; fp32 accumulation)
  * X and dO are M x 256 bf16 (16-B aligned), S 256 x 256 fp32; slab holds iddgcn_sigma_tn_ranges(M) * 256 * 256
  * floats of partials (slab_floats is checked).  D = 256 only. */
 int iddgcn_sigma_tn_ranges(long long M);
 int iddgcn_sigma_tn_bf16(void* stream, long long M, int d, const void* dO, void* X, const float* S, float* slab,
-                         long long slab_floats, float* dS);
+                         long long slab_floats, float* dS, int precision);
 
 /* The run form of iddgcn_combine_f32 (y_idx == v_idx = idx, coefficients per row) writing bf16 out. */
 int iddgcn_combine_bf16(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,

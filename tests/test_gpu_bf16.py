@@ -216,22 +216,25 @@ def test_gemm_tn_bf16(M, cuda):
     assert maxrel(C, ref) <= 1e-5
 
 
+@pytest.mark.parametrize("precision", ["exact", "bf16"])
 @pytest.mark.parametrize("M", [0, 31, 5003, 300_017])
-def test_sigma_tn_bf16_fused(M, cuda):
+def test_sigma_tn_bf16_fused(M, precision, cuda):
     """iddgcn_sigma_tn_bf16 (ABI 11): dS = X^T dO and X = (dO S^T) X (1 - X) in place, in one pass — the bars of the two
     kernels it replaces (dS within 1e-5 of max|ref| of the fp64 product of the same bf16 tables; every dx element within
-    the output's bf16 rounding plus 1e-5 of max|ref|, hi + lo weights), on full tiles, a ragged last tile, a table
-    shorter than one tile and an empty one; dS is overwritten (a stale slab / output never leaks in)."""
+    the output's bf16 rounding plus 1e-5 of max|ref| of the fp64 reference with the weights as the kernel takes them:
+    hi + lo, or rounded to bf16 for precision "bf16"), on full tiles, a ragged last tile, a table shorter than one
+    tile and an empty one; dS is overwritten (a stale slab / output never leaks in)."""
     g = torch.Generator().manual_seed(M + 1)
     dO = bf(torch.randn(M, D, generator=g) * 1e-3).to(cuda)
     X = bf(torch.rand(M, D, generator=g)).to(cuda)
     S = (torch.randn(D, D, generator=g, dtype=torch.float64) / 16).to(cuda)
+    Sd = rb(S) if precision == "bf16" else S.float().double()
     ref_S = X.double().t() @ dO.double()
-    ref_x = (dO.double() @ S.float().double().t()) * X.double() * (1 - X.double())
+    ref_x = (dO.double() @ Sd.t()) * X.double() * (1 - X.double())
     slab = torch.full((ops.sigma_tn_slab_floats(M),), float("nan"), device=cuda)
     dS = torch.full((D, D), float("nan"), device=cuda)
     Xi = X.clone()
-    ops.sigma_tn(dO, Xi, S.float(), dS, slab)
+    ops.sigma_tn(dO, Xi, S.float(), dS, slab, precision=precision)
     torch.cuda.synchronize()
     if M == 0:
         assert torch.equal(dS, torch.zeros_like(dS))
@@ -242,7 +245,7 @@ def test_sigma_tn_bf16_fused(M, cuda):
     # the same dx as the sigma' kernel it replaces, up to the fp32 accumulation order (one bf16 rounding step apart
     # at most)
     C = torch.empty(M, D, dtype=torch.bfloat16, device=cuda)
-    ops.rowgemm(dO, S.float(), C, b_trans=True, act=L.ACT_DSIGMOID, aux=X)
+    ops.rowgemm(dO, S.float(), C, b_trans=True, act=L.ACT_DSIGMOID, aux=X, precision=precision)
     diff = (Xi.double() - C.double()).abs()
     assert (diff <= 2 ** -7 * C.double().abs() + 1e-6 * ref_x.abs().max()).all(), diff.max().item()
 
