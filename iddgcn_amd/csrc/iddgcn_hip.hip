@@ -1580,6 +1580,11 @@ __device__ __forceinline__ void wait_vm(int n) {
 // 256-B bank row.  Wave w owns output rows 32w..32w+31 (columns of A) x all 256 columns (8 accumulator tiles); one
 // v_mfma_f32_32x32x16_bf16 per (k-step, column tile), rows 16s..16s+15 of the tile in k-step s with the same lane
 // k-order as before, so the partials are bitwise the round-4 kernel's.  One barrier per tile.
+// ds_read_b64_tr_b16 issued in asm (the caller waits for it with an explicit lgkmcnt tied to the result)
+__device__ __forceinline__ void tr_read_asm(v4s16& d, const char* p) {
+    const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(d) : "v"(a) : "memory");
+}
 namespace tbf {
 constexpr int D = 256, TK = 32, PT = 512, OPB = TK * PT, BUF = 2 * OPB, NBUF = 3, PD = NBUF - 1;   // 4 buffers: 10.1 vs 9.8 ms
 }  // namespace tbf
@@ -1652,19 +1657,32 @@ __global__ __launch_bounds__(512) void gemm_tn256_bf16t_kernel(long long M, long
     // physical chunk 4(blk ^ x) + 2((l>>4)&1) + ((l&3)>>1) (the +4 row has the same r & 3)
     const int xs = (lane >> 2) & 3;
     const int roff = (8 * (lane >> 5) + xs) * PT + 2 * (16 * ((lane >> 4) & 1) + 4 * (lane & 3));
+    // per 16-row k-step: the A fragment and all eight B fragments read (in asm) before one tied wait, then the eight
+    // MFMAs; hipcc guards the builtin transposed read (no alias information) with a vmcnt(0), which drained the DMAs
+    // of the tiles in flight every k-step (round 5; same MFMA order, bitwise the same partials)
     auto mfma_tile = [&](int bb) __attribute__((always_inline)) {
 #pragma unroll
         for (int s = 0; s < TK / 16; ++s) {
             const char* base = lds + bb * BUF + 16 * s * PT + roff;
-            const bf16x8 a = tr_frag_bf(base + 64 * (wave ^ xs));
-            bf16x8 b = tr_frag_bf(base + OPB + 64 * xs);
+            v4s16 ta[2], tb[8][2];
+            tr_read_asm(ta[0], base + 64 * (wave ^ xs));
+            tr_read_asm(ta[1], base + 64 * (wave ^ xs) + 4 * PT);
 #pragma unroll
             for (int cj = 0; cj < 8; ++cj) {
-                bf16x8 nb = b;                              // column tile cj+1's fragment in flight
-                if (cj + 1 < 8) nb = tr_frag_bf(base + OPB + 64 * ((cj + 1) ^ xs));
-                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[cj], 0, 0, 0);
-                b = nb;
+                tr_read_asm(tb[cj][0], base + OPB + 64 * (cj ^ xs));
+                tr_read_asm(tb[cj][1], base + OPB + 64 * (cj ^ xs) + 4 * PT);
             }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(ta[0]), "+v"(ta[1]), "+v"(tb[0][0]), "+v"(tb[0][1]), "+v"(tb[1][0]), "+v"(tb[1][1]),
+                           "+v"(tb[2][0]), "+v"(tb[2][1]), "+v"(tb[3][0]), "+v"(tb[3][1]), "+v"(tb[4][0]),
+                           "+v"(tb[4][1]), "+v"(tb[5][0]), "+v"(tb[5][1]), "+v"(tb[6][0]), "+v"(tb[6][1]),
+                           "+v"(tb[7][0]), "+v"(tb[7][1])::"memory");
+            const bf16x8 a = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ta[0], ta[1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+            for (int cj = 0; cj < 8; ++cj)
+                acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    a, __builtin_bit_cast(bf16x8, __builtin_shufflevector(tb[cj][0], tb[cj][1], 0, 1, 2, 3, 4, 5, 6, 7)),
+                    acc[cj], 0, 0, 0);
         }
     };
     // cnt[k]: the LDS-DMA count of the tile in buffer k (the waits below let the younger tiles' DMAs fly)
@@ -1729,11 +1747,6 @@ constexpr int D = 256, TR = 32, DPT = 512, XPT = 256, DOB = TR * DPT, XB = TR * 
               PD = 2, NBUF = PD + 1;     // 3 / 4 tiles ahead: 21.2 / 21.5 vs 20.8 ms
 }  // namespace stn
 __device__ __forceinline__ int stn_sw(int r) { return (4 * (r & 3)) ^ ((0x1320 >> (4 * ((r >> 2) & 3))) & 15); }
-// ds_read_b64_tr_b16 issued in asm (the caller waits for it with an explicit lgkmcnt tied to the result)
-__device__ __forceinline__ void tr_read_asm(v4s16& d, const char* p) {
-    const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(d) : "v"(a) : "memory");
-}
 template <bool W1>
 __global__ __launch_bounds__(512) void sigma_tn_bf16_kernel(long long M, int tiles_per_block, int n_ranges,
                                                             const __bf16* __restrict__ dO, __bf16* __restrict__ X,
@@ -2416,25 +2429,45 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
     // this lane's transposed-read address: rows 8(l>>5) + ((l>>2)&3) (+4: second read), columns
     // 16((l>>4)&1) + 4(l&3) of a 32-column block
     const int roff = (8 * (lane >> 5) + ((lane >> 2) & 3)) * PT + 2 * (16 * ((lane >> 4) & 1) + 4 * (lane & 3));
+    // fragments by transposed reads issued in asm with tied lgkmcnt waits (round 5): hipcc guards the builtin form (no
+    // alias information) with a vmcnt(0) before the first one, a drain of the tile t+2 DMAs every tile
+    auto tie6 = [&](v4s16 (&f)[3][2]) __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(f[0][0]), "+v"(f[0][1]), "+v"(f[1][0]), "+v"(f[1][1]), "+v"(f[2][0]), "+v"(f[2][1])::"memory");
+    };
+    auto frag = [&](const v4s16 (&f)[2]) __attribute__((always_inline)) {
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(f[0], f[1], 0, 1, 2, 3, 4, 5, 6, 7));
+    };
     auto mfma_tile = [&](int bb) __attribute__((always_inline)) {
         const char* pa = lds + bb * BUF + roff + 64 * wave;
-        const bf16x8 a0 = tr_frag_b3(pa), a1 = tr_frag_b3(pa + 512), a2 = tr_frag_b3(pa + 1024);
+        const char* pb0 = lds + bb * BUF + OPB + roff;
+        v4s16 fa[3][2], fb[3][2], fn[3][2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            tr_read_asm(fa[k][0], pa + 512 * k);
+            tr_read_asm(fa[k][1], pa + 512 * k + 4 * PT);
+            tr_read_asm(fb[k][0], pb0 + 512 * k);
+            tr_read_asm(fb[k][1], pb0 + 512 * k + 4 * PT);
+        }
+        tie6(fa);
+        tie6(fb);
+        const bf16x8 a0 = frag(fa[0]), a1 = frag(fa[1]), a2 = frag(fa[2]);
         // B fragments of column tile cj+1 in flight during tile cj's MFMAs (two register sets: the 128
         // accumulator VGPRs leave no room for all eight tiles' fragments)
-        const char* pb0 = lds + bb * BUF + OPB + roff;
-        bf16x8 b0 = tr_frag_b3(pb0), b1 = tr_frag_b3(pb0 + 512), b2 = tr_frag_b3(pb0 + 1024);
         // per tile the five smaller products start from zero and join the running sum with one fp32 add
         // (v_add_f32, round-to-nearest-even) in front of the a0 b0 MFMA: all six MFMAs chained on the running sum
         // over a block's 16k rows gave 1.46x the exact mode's fmaf-chain error (tools/bench_gemm.py)
 #pragma unroll
         for (int cj = 0; cj < 8; ++cj) {
-            bf16x8 n0 = b0, n1 = b1, n2 = b2;          // column tile cj+1's fragments in flight
             if (cj + 1 < 8) {
                 const char* pb = pb0 + 64 * (cj + 1);
-                n0 = tr_frag_b3(pb);
-                n1 = tr_frag_b3(pb + 512);
-                n2 = tr_frag_b3(pb + 1024);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    tr_read_asm(fn[k][0], pb + 512 * k);
+                    tr_read_asm(fn[k][1], pb + 512 * k + 4 * PT);
+                }
             }
+            const bf16x8 b0 = frag(fb[0]), b1 = frag(fb[1]), b2 = frag(fb[2]);
             f32x16 c;
 #pragma unroll
             for (int j = 0; j < 16; ++j) c[j] = 0.f;
@@ -2445,9 +2478,14 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
             acc[cj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[cj] + c, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            b0 = n0;
-            b1 = n1;
-            b2 = n2;
+            if (cj + 1 < 8) {
+                tie6(fn);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    fb[k][0] = fn[k][0];
+                    fb[k][1] = fn[k][1];
+                }
+            }
         }
     };
 
