@@ -1542,7 +1542,11 @@ __global__ __launch_bounds__(512) void gemm_tn256_x3_kernel(long long M_, long l
         if (t + 2 < nt) stage(t + 2, b);
         if (t + 1 < nt) {
             convert(b ^ 1);
-            __syncthreads();
+            // the converted tile visible to every wave: LDS only (a __syncthreads here also waited for tile t+2's DMA
+            // just issued, so it never overlapped tile t+1's MFMAs)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
         }
     }
     float* out = slab + (long long)blockIdx.x * D * D;
