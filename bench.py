@@ -111,9 +111,13 @@ def kernel_roofline(name, N, R, D, T, gemm, avg_ms, eb=4, edge_mfma="hilo"):
               "tail_bwd_rec_gemm": 2.0 * eb * D * T + 4.0 * R * T + 4.0 * T + 4.0 * (R + 1) * N * D,
               "tail_dS_tn": 2.0 * eb * D * T,
               "tail_bwd_sigma_tn": 3.0 * eb * D * T}[name]
-    if name == "tail_bwd_sigma_tn":
-        # one pass, both GEMMs (bf16 tables, hi + lo weights): sigma' 2 bf16 products per term, the TN 1
-        flops, hw_flops, peak_f = 2 * flops, 3 * flops, MFMA_F16_PEAK_TFLOPS
+    if name == "tail_bwd_sigma_tn" and eb == 2:
+        # one pass, both GEMMs over bf16 tables: sigma' 2 bf16 products per term with hi + lo weights (1 with bf16
+        # weights, edge_mfma "bf16"), the TN 1
+        flops, hw_flops, peak_f = 2 * flops, (2 if edge_mfma == "bf16" else 3) * flops, MFMA_F16_PEAK_TFLOPS
+    elif name == "tail_bwd_sigma_tn":
+        # one pass, both GEMMs over fp32 tables in the bf16x3 mode (round 6): six bf16 products per term in each
+        flops, hw_flops, peak_f = 2 * flops, 12 * flops, MFMA_F16_PEAK_TFLOPS
     elif eb == 2:
         hw_flops, peak_f = (1 if edge_mfma == "bf16" else 2) * flops, MFMA_F16_PEAK_TFLOPS
     elif gemm == "bf16x3":
@@ -160,18 +164,23 @@ def stream_probe(torch, dev, T, D, reps=3):
     return out
 
 
-def pmc_traffic(kernel, gemm, workload, world):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of the same bench
-    command (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x2 per the gfx950
-    correction + WRITE_SIZE, separate --pmc passes), or None when no such profile exists."""
+def pmc_record(key):
+    """An entry of the NEWEST committed rocprofv3 PMC summary (profiles/rNN/pmc_traffic.json of the latest round,
+    written by tools/pmc_traffic.py / tools/pmc_step.py: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE,
+    separate --pmc passes), or (None, None).  Older rounds' files are not consulted: their kernels may have changed."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
-        with open(path) as f:
-            rec = json.load(f)
-        key = f"{workload}/{gemm}/n{world}/{kernel}"
-        if key in rec:
-            return rec[key]["bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "pmc_traffic.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        rec = json.load(f)
+    return rec.get(key), os.path.relpath(paths[-1], ROOT)
+
+
+def pmc_traffic(kernel, gemm, workload, world):
+    """HBM bytes per launch of `kernel` of the same bench command (pmc_record), or None."""
+    r, path = pmc_record(f"{workload}/{gemm}/n{world}/{kernel}")
+    return (r["bytes_per_launch"], path) if r else (None, None)
 
 
 def workload_bytes(cid, world, features):
@@ -349,28 +358,51 @@ def cpu_baseline(cfg, frac=0.05, min_steps=3, budget_s=60.0):
                        f"{os.cpu_count()}-CPU host ({cpu_model()})")}
 
 
-def step_roofline(N, R, D, T, M, gemm, features, ms_per_step, edge_mfma="hilo"):
-    """Whole-step roofline (T_roof = W_gemm / P_mfma + Q_hbm / BW, fraction =
-    T_roof / T_measured), for one rank's step.  Two forms: the BASELINE formula as written (W_gemm on the f32 MFMA
-    peak), and the same work on the peak of the MFMAs this mode issues (bf16x3: 6 bf16 products per fp32 product on
-    the 2.5 PF peak; split: 3 f16 products; the bf16-feature mode: 2 bf16 MFMAs per k-step, bf16 edge tables)."""
-    from iddgcn_amd.engine import step_bytes, step_flops
+def step_roofline(N, R, D, T, M, gemm, features, ms_per_step, edge_mfma="hilo", fused_sigma_tn=True,
+                  fused_tail_head=False):
+    """Whole-step roofline of one rank's step (round 6: a lower bound of THIS formulation).
+
+    impl: engine.step_bytes_impl's parts (the compulsory HBM bytes and D x D GEMM work of each stage of the
+      implemented step: tail-sorted gathers read each distinct node row once, SpMM gathers from tables beyond the
+      256 MiB Infinity Cache once per stored entry, small random-order rows one 128-B line each); each part priced at
+      the larger of its MFMA time (the MFMA products this mode issues per flop, on that MFMA's dense peak) and its
+      HBM time at 8 TB/s, summed over the parts.  T_roof <= the measured step by construction, frac = T_roof / T.
+    survey_formula: SURVEY §8(d)'s W_gemm / P + Q_hbm / BW as written (Q_hbm charges every scored edge R gathered
+      P_r rows per layer, 8·L·R·T·D; W_gemm on the f32 peak) and with W_gemm on this mode's MFMA peak: kept for
+      comparison, NOT a lower bound of this formulation (its ratio to the measured step can exceed 1)."""
+    from iddgcn_amd.engine import step_bytes, step_bytes_impl, step_flops
     W = float(step_flops(N, R, D, T, M))
     Q = float(step_bytes(N, R, D, T, M))
     if features == "bf16":          # BASELINE.md: "for bf16, use 2.5 PFLOP/s and halve the D-terms"
         Q = Q - 0.5 * (40.0 * T * D + 8.0 * 3 * R * T * D)
-    hw, peak = {"exact": (1, MFMA_F32_PEAK_TFLOPS), "split": (3, MFMA_F16_PEAK_TFLOPS),
-                "bf16x3": (6, MFMA_F16_PEAK_TFLOPS)}[gemm]
-    if features == "bf16":
-        hw, peak = (1 if edge_mfma == "bf16" else 2), MFMA_F16_PEAK_TFLOPS
+    # MFMA products per algorithmic flop and their peak, for the edge-level and the node-level GEMMs of this mode
+    node = {"exact": (1, MFMA_F32_PEAK_TFLOPS), "split": (3, MFMA_F16_PEAK_TFLOPS),
+            "bf16x3": (6, MFMA_F16_PEAK_TFLOPS)}[gemm]
+    edge = node
+    if features == "bf16":          # bf16 tables: x·S and sigma' 2 products (hi + lo weights) or 1, the dS TN 1
+        edge = ((1.0 if edge_mfma == "bf16" else 1.5), MFMA_F16_PEAK_TFLOPS)
+    Qi, parts = step_bytes_impl(N, R, D, T, M, eb=2 if features == "bf16" else 4, fused_sigma_tn=fused_sigma_tn,
+                                fused_tail_head=fused_tail_head)
+    t_parts = {}
+    for name, (nbytes, flop, kind) in parts.items():
+        hw, peak = {"edge": edge, "node": node}.get(kind, (0, 1.0))
+        t_parts[name] = max(hw * flop / (peak * 1e12), nbytes / (HBM_PEAK_GBS * 1e9)) * 1e3
+    t_impl = sum(t_parts.values())
     t_hbm = Q / (HBM_PEAK_GBS * 1e9) * 1e3
     t_f32 = W / (MFMA_F32_PEAK_TFLOPS * 1e12) * 1e3
-    t_mode = hw * W / (peak * 1e12) * 1e3
-    return {"W_gemm_flop": W, "Q_hbm_bytes": Q, "t_hbm_ms": t_hbm,
-            "baseline_formula": {"t_mfma_ms": t_f32, "t_roof_ms": t_f32 + t_hbm, "frac": (t_f32 + t_hbm) / ms_per_step,
-                                 "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS},
-            "mode": {"gemm": gemm, "features": features, "mfma_products_per_flop": hw, "peak_TFLOPs": peak,
-                     "t_mfma_ms": t_mode, "t_roof_ms": t_mode + t_hbm, "frac": (t_mode + t_hbm) / ms_per_step}}
+    hw_mode = node[0] if features != "bf16" else edge[0]
+    t_mode = hw_mode * W / (node[1] * 1e12) * 1e3
+    return {"impl": {"Q_hbm_bytes": Qi, "W_gemm_flop": sum(v[1] for v in parts.values()), "t_roof_ms": t_impl,
+                     "frac": t_impl / ms_per_step, "t_hbm_ms": Qi / (HBM_PEAK_GBS * 1e9) * 1e3,
+                     "parts_ms": {k: round(v, 4) for k, v in t_parts.items()},
+                     "parts_GB": {k: round(v[0] / 1e9, 3) for k, v in parts.items()},
+                     "fused_sigma_tn": bool(fused_sigma_tn), "fused_tail_head": bool(fused_tail_head)},
+            "survey_formula": {"W_gemm_flop": W, "Q_hbm_bytes": Q, "t_hbm_ms": t_hbm,
+                               "f32_peak": {"t_mfma_ms": t_f32, "t_roof_ms": t_f32 + t_hbm,
+                                            "ratio_to_measured": (t_f32 + t_hbm) / ms_per_step},
+                               "mode_peak": {"mfma_products_per_flop": hw_mode, "t_mfma_ms": t_mode,
+                                             "t_roof_ms": t_mode + t_hbm, "ratio_to_measured": (t_mode + t_hbm) / ms_per_step},
+                               "note": "SURVEY §8(d) as written; not a lower bound of this formulation"}}
 
 
 def rank_consistency(buf):
@@ -444,6 +476,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
     if cuts is not None:
         from iddgcn_amd.parallel import NodeShard
         eng.row_shard = NodeShard(cuts)          # node rows split over the ranks, scored edges by tail
+        eng.overlap_e_gather = True              # the E all-gather travels into the next step (finished below)
     elif shard == "relation" and world > 1:
         eng.node_shard = RelationShard(R, N)     # SURVEY §8(e) alternative: node tables split by relation
     elif shard == "spmm" and world > 1:
@@ -491,8 +524,14 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
                       + ("+row-partitioned-spmm" if eng.spmm_shard else ""),
                       "gemm": gemm, "features": feat, **({"edge_mfma": emfma} if feat == "bf16" else {})},
            "scored_edges_per_s": T / (elapsed / steps), "loss": loss_val, "steps": steps, "warmup": warmup,
-           "step_roofline": step_roofline(N, R, D, ed.T, M, gemm, feat,
-                                          elapsed / steps * 1e3, edge_mfma=emfma)}
+           "step_roofline": step_roofline(N, R, D, ed.T, M, gemm, feat, elapsed / steps * 1e3, edge_mfma=emfma,
+                                          fused_sigma_tn=eng.sigma_tn_fused,
+                                          fused_tail_head=eng.fuse_tail_head and feat == "bf16" and R == 8 and D == 256)}
+    step_pmc, step_pmc_src = pmc_record(f"{cfg['name']}/{gemm}/n{world}/step")
+    if step_pmc:        # the measured HBM bytes of a whole step (tools/pmc_step.py) beside the compulsory count
+        out["step_roofline"]["impl"].update({"pmc_step_bytes": step_pmc["bytes"], "pmc_source": step_pmc_src,
+                                             "impl_over_pmc": out["step_roofline"]["impl"]["Q_hbm_bytes"] /
+                                             step_pmc["bytes"]})
     if world > 1:
         out["ranks_consistent"] = consist == 0.0
         out["params_max_abs_diff_vs_rank0"] = consist

@@ -1,18 +1,23 @@
 """ctypes binding of libiddgcn_hip.so (C-ABI declared in include/iddgcn.h, iddgcn_graph.h,
 iddgcn_similarity.h and iddgcn_sampling.h).
 
-The product path has no CPU fallback: if the shared library is missing or was
-built for another ABI version, :func:`lib` raises immediately.
+The product path has no CPU fallback: if the shared library is missing, was
+built for another ABI version or from other sources than the tree beside it
+(the source digest compiled into it, _srchash.py), :func:`lib` raises immediately.
 """
 import ctypes
 import os
 
+from . import _srchash
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libiddgcn_hip.so")
-# a build variant of the same source (tools/ A/B timing); the product loads LIB_PATH
+PRODUCT_LIB = os.path.join(_HERE, "libiddgcn_hip.so")
+LIB_PATH = PRODUCT_LIB
+# a build variant of the same source (tools/ A/B timing, built with extra -D flags: no source digest check); the
+# product loads PRODUCT_LIB
 if os.environ.get("IDDGCN_LIB"):
     LIB_PATH = os.environ["IDDGCN_LIB"]
-ABI_VERSION = 11
+ABI_VERSION = 12
 ROWGEMM_BATCH = 25          # IDDGCN_ROWGEMM_BATCH: entries per iddgcn_rowgemm_batched_f32 call
 
 ACT_NONE, ACT_SIGMOID, ACT_DSIGMOID = 0, 1, 2
@@ -82,6 +87,7 @@ SIGNATURES = {
     "iddgcn_gemm_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
     "iddgcn_sigma_tn_ranges": (ci, [cll]),
     "iddgcn_sigma_tn_bf16": (ci, [vp, cll, ci, vp, vp, vp, vp, cll, vp, ci]),
+    "iddgcn_sigma_tn_f32": (ci, [vp, cll, ci, vp, vp, vp, vp, cll, vp, ci]),
     "iddgcn_combine_bf16": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_combine_planes_f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, cll, vp]),
     "iddgcn_gemm_tn_planes_f32": (ci, [vp, cll, ci, vp, vp, vp, ci, vp, ci]),
@@ -123,21 +129,47 @@ def exported_symbols():
     return list(SIGNATURES)
 
 
-def load(path=LIB_PATH):
-    """Load the library and bind every symbol of include/*.h (no GPU call)."""
+class StaleLibraryError(IddgcnError):
+    pass
+
+
+def library_source_sha256(lib):
+    """The source digest compiled into a loaded library (iddgcn_source_sha256), or None if it exports none."""
+    try:
+        fn = lib.iddgcn_source_sha256
+    except AttributeError:
+        return None
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    return fn().decode()
+
+
+def load(path=LIB_PATH, check_source=None):
+    """Load the library and bind every symbol of include/*.h (no GPU call).  ``check_source`` (default: for the
+    product library) compares the digest of the sources the library was built from with the tree's (_srchash) and
+    raises StaleLibraryError on a mismatch."""
     if not os.path.exists(path):
         raise IddgcnError(
             f"libiddgcn_hip.so not found at {path}: build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950). "
             "There is no CPU fallback for the IDDGCN hot path.")
     lib = ctypes.CDLL(path)
+    lib.iddgcn_abi_version.restype = ci
+    v = lib.iddgcn_abi_version()
+    if v != ABI_VERSION:
+        raise IddgcnError(f"libiddgcn_hip ABI version {v}, expected {ABI_VERSION}")
+    if check_source is None:
+        check_source = os.path.abspath(path) == PRODUCT_LIB and not os.environ.get("IDDGCN_LIB")
+    if check_source:
+        built, tree = library_source_sha256(lib), _srchash.source_sha256()
+        if built != tree:
+            raise StaleLibraryError(
+                f"{path} was built from other sources (digest {built}) than this tree's ({tree}): rebuild it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'`")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    v = lib.iddgcn_abi_version()
-    if v != ABI_VERSION:
-        raise IddgcnError(f"libiddgcn_hip ABI version {v}, expected {ABI_VERSION}")
     return lib
 
 

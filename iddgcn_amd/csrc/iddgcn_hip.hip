@@ -2247,8 +2247,8 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
         asm volatile("ds_read_b128 %0, %6 offset:%7\n\tds_read_b128 %1, %6 offset:%8\n\t"                 \
                      "ds_read_b128 %2, %6 offset:%9\n\tds_read_b128 %3, %6 offset:%10\n\t"                \
                      "ds_read_b128 %4, %6 offset:%11\n\tds_read_b128 %5, %6 offset:%12"                   \
-                     : "=v"(fx[S][0]), "=v"(fx[S][1]), "=v"(fx[S][2]), "=v"(fy[S][0]), "=v"(fy[S][1]),     \
-                       "=v"(fy[S][2])                                                                   \
+                     : "=&v"(fx[S][0]), "=&v"(fx[S][1]), "=&v"(fx[S][2]), "=&v"(fy[S][0]), "=&v"(fy[S][1]),     \
+                       "=&v"(fy[S][2])                                                                   \
                      : "v"(ab), "i"(64 * (Q)), "i"(64 * (Q) + 512), "i"(64 * (Q) + 1024),                \
                        "i"(64 * (Q) + 16 * PITCH), "i"(64 * (Q) + 16 * PITCH + 512),                      \
                        "i"(64 * (Q) + 16 * PITCH + 1024)                                                 \
@@ -2534,6 +2534,371 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
             const int row = 32 * wave + (j & 3) + 8 * (j >> 2) + 4 * h;
             out[row * D + 32 * cj + i] = acc[cj][j];
         }
+}
+
+// ---- sigma' backward + dS TN in one pass over the fp32 edge tables, bf16x3 operands (round 6, configs 3 / 4) ------
+// The headline mode's layer-2/3 edge backward (the autodiff of IDDGCN.py:62-63,79 for x_t^{l-1} S^l):
+//   dS = X^T dO (per-range partials, summed by reduce_slabs)  and  X = (dO S^T) X (1 - X) in place.
+// rowgemm256_b3_kernel<0, true> (sigma') and gemm_tn256_b3_kernel (TN) ran it as two passes: both read dO and X
+// (20.5 GB per config-3 layer) and each converted its operands to bf16 planes on its own.  One pass here reads each
+// tile once (12.3 GB) and converts each row once per workgroup.
+// Workgroup pair per row range (column half h = 0, 1; blockIdx 8 apart: the same XCD, so the pair's second read of a
+// dO tile is an L2 hit), as sigma_tn_bf16_kernel: workgroup h reads dO (all columns) and X[:, half h], and writes
+// dX[:, half h] over the same bytes, so the in-place write never meets the other workgroup's reads.
+//   * sigma': wave w owns output columns c0 = 128h + 16w .. +15; S^T as three bf16 planes is operand A of
+//     v_mfma_f32_16x16x32_bf16 (96 VGPRs), the dO planes operand B (ds_read_b128): rowgemm256_b3_kernel's six
+//     products in its order, so dX is bitwise that kernel's.  Epilogue x(1 - x) with x = p0 + p1 + p2 rebuilt (exactly:
+//     the pieces are an exact split) from the X planes in LDS.
+//   * dS[half h rows, :]: wave w owns X columns 128h + 32(w & 3) .. +31 x dO columns 128(w >> 2) .. +127 as 2 x 8
+//     16x16 tiles (64 VGPRs); v_mfma_f32_16x16x32_bf16 over the tile's 32 rows (one k-step) on ds_read_b64_tr_b16
+//     fragments (T10 geometry: lane l supplies row 8(l >> 4) + ((l >> 2) & 3) (+4), columns 4(l & 3) .. +3 of a
+//     16-column block); per 16x16 tile the five smaller products start from zero and join the running sum by one fp32
+//     add in front of the a0 b0 MFMA (gemm_tn256_b3_kernel's accuracy form, 32 rows per join).
+// LDS: two buffers of [dO: 32 x 1536 B | X half: 32 x 768 B] (147,456 B).  An fp32 dO row arrives by one full-wave
+// LDS-DMA at the start of its 1536-B slot, a pair of X-half rows by one full-wave DMA across their two 768-B slots; the
+// wave that DMA'd them converts them in place (all six reads before any write) to three bf16 planes (plane j at byte
+// 512 j / 256 j of the slot) with 16-B chunk c of row r at c ^ stn_sw(r).  Every slot starts at bank 0, so the
+// conflict analysis of sigma_tn_bf16_kernel's 512 / 256-B slots holds for the ds_read_b128 row fragments and the
+// transposed reads alike.  Tile t + 1 is DMA'd while tile t computes and converted after its MFMAs; one barrier per
+// tile.  Every LDS read of the loop is issued in asm with a tied lgkmcnt wait (no compiler vmcnt drain of the DMAs).
+namespace st3 {
+constexpr int D = 256, TR = 32, DP = 1536, XP = 768, DOB = TR * DP, XB = TR * XP, BUF = DOB + XB, NBUF = 2;
+}  // namespace st3
+__device__ __forceinline__ unsigned lds_u32(const void* p) {
+    return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+// three transposed reads at a, a + PS, a + 2 PS (the three planes of one 4-row block).  Every multi-instruction asm
+// read here marks its outputs early-clobber ("=&v"): without it the compiler may give an output the input address
+// register, which the first read then overwrites (asynchronously) while the later reads still use it as address
+// (tests/test_host.py::test_asm_transposed_reads_are_waited_for caught exactly that in this kernel's first build)
+template <int PS>
+__device__ __forceinline__ void tr_read3(v4s16 (&d)[3], unsigned a) {
+    asm volatile("ds_read_b64_tr_b16 %0, %3\n\tds_read_b64_tr_b16 %1, %3 offset:%4\n\tds_read_b64_tr_b16 %2, %3 offset:%5"
+                 : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2])
+                 : "v"(a), "i"(PS), "i"(2 * PS)
+                 : "memory");
+}
+__device__ __forceinline__ bf16x8 cat_tr(const v4s16& a, const v4s16& b) {
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// bf16 element q of a packed 4-element u32x2, as fp32
+__device__ __forceinline__ float bf_at(const u32x2& v, int q) {
+    const unsigned w = v[q >> 1];
+    return __builtin_bit_cast(float, (q & 1) ? (w & 0xffff0000u) : (w << 16));
+}
+__global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles_per_block, int n_ranges,
+                                                          const float* __restrict__ dO, float* __restrict__ X,
+                                                          const float* __restrict__ S, float* __restrict__ slab) {
+    using namespace st3;
+    static_assert(NBUF * BUF <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char lds[NBUF * BUF];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bx = blockIdx.x;
+    const int half = (bx >> 3) & 1;
+    const int range = ((bx >> 4) << 3) | (bx & 7);
+    if (range >= n_ranges) return;
+    const long long ntiles = (M + TR - 1) / TR;
+    const long long t_beg = (long long)range * tiles_per_block;
+    long long t_end = t_beg + tiles_per_block;
+    if (t_end > ntiles) t_end = ntiles;            // a range past the table still writes its (zero) partial
+    const int i16 = lane & 15, g = lane >> 4;
+    const int c0 = 128 * half + 16 * wave;
+    const unsigned lds0 = lds_u32(lds);
+    // a lane index the compiler cannot hoist out of the loop: the per-lane LDS offsets of every phase are recomputed
+    // from it there (a few VALU each) instead of being kept live across the loop, where they spilled (23 VGPRs)
+    auto fresh_lane = [&]() __attribute__((always_inline)) {
+        int l = lane;
+        asm volatile("" : "+v"(l));
+        return l;
+    };
+
+    // S^T as operand A: column c0 + i16, k = 32q + 8g + e, split exactly into three bf16 pieces
+    bf16x8 w0[8], w1[8], w2[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            __bf16 a, b, c;
+            split3(S[(c0 + i16) * D + 32 * q + 8 * g + e], a, b, c);
+            w0[q][e] = a;
+            w1[q][e] = b;
+            w2[q][e] = c;
+        }
+    f32x4 tacc[2][8];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb) tacc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // fp32 rows of tile t into buffer bb: dO rows 4w .. 4w+3 (one full-wave DMA each), X-half rows 4w .. 4w+3 (a pair
+    // per full-wave DMA); rows past M as fp32 zeros (0 x whatever-bits could be NaN in the TN).  Returns the DMA count.
+    auto stage = [&](long long t, int bb) __attribute__((always_inline)) -> int {
+        const int lane = fresh_lane();
+        char* base = lds + bb * BUF;
+        const long long t0 = t * TR;
+        if (t0 + TR <= M) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = 4 * wave + j;
+                __builtin_amdgcn_global_load_lds((gbl_vptr)(dO + (t0 + r) * D + lane * 4), (lds_vptr)(base + r * DP), 16,
+                                                 0, 0);
+            }
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int r = 4 * wave + 2 * p;
+                __builtin_amdgcn_global_load_lds(
+                    (gbl_vptr)(X + (t0 + r + (lane >> 5)) * D + 128 * half + (lane & 31) * 4),
+                    (lds_vptr)(base + DOB + r * XP), 16, 0, 0);
+            }
+            return 6;
+        }
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = 4 * wave + j;
+            const long long e = t0 + r;
+            char* xr = base + DOB + (r & ~1) * XP + 512 * (r & 1);     // where the pair DMA would put row r
+            if (e < M) {
+                __builtin_amdgcn_global_load_lds((gbl_vptr)(dO + e * D + lane * 4), (lds_vptr)(base + r * DP), 16, 0, 0);
+                if (lane < 32)
+                    __builtin_amdgcn_global_load_lds((gbl_vptr)(X + e * D + 128 * half + lane * 4), (lds_vptr)xr, 16, 0,
+                                                     0);
+                n += 2;
+            } else {
+                st4(reinterpret_cast<float*>(base + r * DP) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+                if (lane < 32) st4(reinterpret_cast<float*>(xr) + lane * 4, f32x4{0.f, 0.f, 0.f, 0.f});
+            }
+        }
+        return n;
+    };
+    // row j of this wave's share of buffer bb, fp32 -> three bf16 planes in place: j < 4 the dO row 4w + j, j = 4, 5 the
+    // X-half pair 4w + 2(j - 4), +1 (the 1-KiB read completes before the writes, which overwrite its bytes and, for a
+    // pair, the second row's)
+    auto convert_row = [&](int bb, int j) __attribute__((always_inline)) {
+        char* base = lds + bb * BUF;
+        const int lane = fresh_lane();
+        u32x4 v;
+        const bool dor = j < 4;
+        const int r0 = dor ? 4 * wave + j : 4 * wave + 2 * (j - 4);
+        char* src = dor ? base + r0 * DP : base + DOB + r0 * XP;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_u32(src) + 16 * lane) : "memory");
+        bf16x4 p0, p1, p2;
+        split3x4(__builtin_bit_cast(f32x4, v), p0, p1, p2);
+        char* row;
+        int ps;
+        if (dor) {
+            row = base + r0 * DP + 16 * ((lane >> 1) ^ stn_sw(r0)) + 8 * (lane & 1);
+            ps = 512;
+        } else {
+            const int r = r0 + (lane >> 5);
+            row = base + DOB + r * XP + 16 * (((lane & 31) >> 1) ^ stn_sw(r)) + 8 * (lane & 1);
+            ps = 256;
+        }
+        *reinterpret_cast<bf16x4*>(row) = p0;
+        *reinterpret_cast<bf16x4*>(row + ps) = p1;
+        *reinterpret_cast<bf16x4*>(row + 2 * ps) = p2;
+    };
+    auto convert = [&](int bb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) convert_row(bb, j);
+    };
+    // sigma': row fragment of row i16 (+16 rb) at k-step q, plane j: chunk (4q + g) ^ swi = 4(q ^ sa) + (g ^ sl)
+    auto mfma_sigma = [&](int bb, f32x4 (&acc)[2]) __attribute__((always_inline)) {
+        const int lane = fresh_lane();
+        const int i16 = lane & 15, g = lane >> 4, swi = stn_sw(i16), sa = swi >> 2, sl = swi & 3;
+        const unsigned rb0 = lds0 + bb * BUF + i16 * DP + 16 * (g ^ sl);
+        const unsigned ad0 = rb0 + 64 * (0 ^ sa), ad1 = rb0 + 64 * (1 ^ sa), ad2 = rb0 + 64 * (2 ^ sa),
+                       ad3 = rb0 + 64 * (3 ^ sa);
+        f32x4 hi0 = {0.f, 0.f, 0.f, 0.f}, lo0 = hi0, hi1 = hi0, lo1 = hi0;
+        u32x4 fx[2][3], fy[2][3];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#define ST3_LOADQ(Q, S_, AD)                                                                              \
+        asm volatile("ds_read_b128 %0, %6 offset:%7\n\tds_read_b128 %1, %6 offset:%8\n\t"                 \
+                     "ds_read_b128 %2, %6 offset:%9\n\tds_read_b128 %3, %6 offset:%10\n\t"                \
+                     "ds_read_b128 %4, %6 offset:%11\n\tds_read_b128 %5, %6 offset:%12"                   \
+                     : "=&v"(fx[S_][0]), "=&v"(fx[S_][1]), "=&v"(fx[S_][2]), "=&v"(fy[S_][0]), "=&v"(fy[S_][1]),  \
+                       "=&v"(fy[S_][2])                                                                  \
+                     : "v"(AD), "i"(256 * ((Q) >> 2)), "i"(256 * ((Q) >> 2) + 512),                       \
+                       "i"(256 * ((Q) >> 2) + 1024), "i"(256 * ((Q) >> 2) + 16 * DP),                     \
+                       "i"(256 * ((Q) >> 2) + 16 * DP + 512), "i"(256 * ((Q) >> 2) + 16 * DP + 1024)      \
+                     : "memory")
+        ST3_LOADQ(0, 0, ad0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int S_ = q & 1;
+            if (q + 1 < 8) {
+                switch (q) {      // the offsets are immediates: one asm per k-step
+                    case 0: ST3_LOADQ(1, 1, ad1); break;
+                    case 1: ST3_LOADQ(2, 0, ad2); break;
+                    case 2: ST3_LOADQ(3, 1, ad3); break;
+                    case 3: ST3_LOADQ(4, 0, ad0); break;
+                    case 4: ST3_LOADQ(5, 1, ad1); break;
+                    case 5: ST3_LOADQ(6, 0, ad2); break;
+                    default: ST3_LOADQ(7, 1, ad3); break;
+                }
+                asm volatile("s_waitcnt lgkmcnt(6)"
+                             : "+v"(fx[S_][0]), "+v"(fx[S_][1]), "+v"(fx[S_][2]), "+v"(fy[S_][0]), "+v"(fy[S_][1]),
+                               "+v"(fy[S_][2])::"memory");
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(fx[S_][0]), "+v"(fx[S_][1]), "+v"(fx[S_][2]), "+v"(fy[S_][0]), "+v"(fy[S_][1]),
+                               "+v"(fy[S_][2])::"memory");
+            }
+            const bf16x8 x0 = __builtin_bit_cast(bf16x8, fx[S_][0]), x1 = __builtin_bit_cast(bf16x8, fx[S_][1]),
+                         x2 = __builtin_bit_cast(bf16x8, fx[S_][2]);
+            const bf16x8 y0 = __builtin_bit_cast(bf16x8, fy[S_][0]), y1 = __builtin_bit_cast(bf16x8, fy[S_][1]),
+                         y2 = __builtin_bit_cast(bf16x8, fy[S_][2]);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], x2, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], y2, lo1, 0, 0, 0);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2[q], x0, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2[q], y0, lo1, 0, 0, 0);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[q], x1, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[q], y1, lo1, 0, 0, 0);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], x1, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], y1, lo1, 0, 0, 0);
+            lo0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[q], x0, lo0, 0, 0, 0);
+            lo1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[q], y0, lo1, 0, 0, 0);
+            hi0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], x0, hi0, 0, 0, 0);
+            hi1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[q], y0, hi1, 0, 0, 0);
+        }
+#undef ST3_LOADQ
+        acc[0] = hi0 + lo0;
+        acc[1] = hi1 + lo1;
+    };
+    // hook(nb): VALU / LDS work issued right behind column block nb's twelve MFMAs (it runs in their shadow)
+    auto mfma_tn = [&](int bb, auto&& hook) __attribute__((always_inline)) {
+        // transposed-read rows of this lane (first / second read of a fragment) and their swizzles; the byte of the
+        // lane's 4 columns in a row of 16-column block blk is 16 ((2 blk) ^ (sw & 14)) + 16 (tb ^ (sw & 1)) + 8 (l & 1)
+        const int lane = fresh_lane();
+        const int tra = 8 * (lane >> 4) + ((lane >> 2) & 3), trq = tra + 4;
+        const int swa = stn_sw(tra), swq = stn_sw(trq);
+        const int tb = (lane & 3) >> 1;
+        const unsigned xoa = tra * XP + 16 * (tb ^ (swa & 1)) + 8 * (lane & 1),
+                       xoq = trq * XP + 16 * (tb ^ (swq & 1)) + 8 * (lane & 1);
+        const unsigned doa = tra * DP + 16 * (tb ^ (swa & 1)) + 8 * (lane & 1) + 256 * (wave >> 2),
+                       doq = trq * DP + 16 * (tb ^ (swq & 1)) + 8 * (lane & 1) + 256 * (wave >> 2);
+        const int swa_e = swa & 14, swq_e = swq & 14;
+        const unsigned db = lds0 + bb * BUF, xb = db + DOB;
+        v4s16 xa[2][2][3], fb[2][2][3];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const int cx = 4 * (wave & 3) + 2 * mb;
+            tr_read3<256>(xa[mb][0], xb + xoa + 16 * (cx ^ swa_e));
+            tr_read3<256>(xa[mb][1], xb + xoq + 16 * (cx ^ swq_e));
+        }
+        tr_read3<512>(fb[0][0], db + doa + 16 * (0 ^ swa_e));
+        tr_read3<512>(fb[0][1], db + doq + 16 * (0 ^ swq_e));
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(xa[0][0][0]), "+v"(xa[0][0][1]), "+v"(xa[0][0][2]), "+v"(xa[0][1][0]), "+v"(xa[0][1][1]),
+                       "+v"(xa[0][1][2]), "+v"(xa[1][0][0]), "+v"(xa[1][0][1]), "+v"(xa[1][0][2]), "+v"(xa[1][1][0]),
+                       "+v"(xa[1][1][1]), "+v"(xa[1][1][2]), "+v"(fb[0][0][0]), "+v"(fb[0][0][1]), "+v"(fb[0][0][2]),
+                       "+v"(fb[0][1][0]), "+v"(fb[0][1][1]), "+v"(fb[0][1][2])::"memory");
+        bf16x8 a[2][3];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) a[mb][j] = cat_tr(xa[mb][0][j], xa[mb][1][j]);
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb) {
+            const int s = nb & 1;
+            if (nb + 1 < 8) {
+                tr_read3<512>(fb[s ^ 1][0], db + doa + 16 * ((2 * (nb + 1)) ^ swa_e));
+                tr_read3<512>(fb[s ^ 1][1], db + doq + 16 * ((2 * (nb + 1)) ^ swq_e));
+            }
+            const bf16x8 b0 = cat_tr(fb[s][0][0], fb[s][1][0]), b1 = cat_tr(fb[s][0][1], fb[s][1][1]),
+                         b2 = cat_tr(fb[s][0][2], fb[s][1][2]);
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            f32x4 e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][0], b2, z, 0, 0, 0);
+            f32x4 e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][0], b2, z, 0, 0, 0);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][2], b0, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][2], b0, e1, 0, 0, 0);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][1], b1, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][1], b1, e1, 0, 0, 0);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][0], b1, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][0], b1, e1, 0, 0, 0);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][1], b0, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][1], b0, e1, 0, 0, 0);
+            tacc[0][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][0], b0, tacc[0][nb] + e0, 0, 0, 0);
+            tacc[1][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][0], b0, tacc[1][nb] + e1, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            hook(nb);
+            __builtin_amdgcn_sched_barrier(0);
+            if (nb + 1 < 8)
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(fb[s ^ 1][0][0]), "+v"(fb[s ^ 1][0][1]), "+v"(fb[s ^ 1][0][2]), "+v"(fb[s ^ 1][1][0]),
+                               "+v"(fb[s ^ 1][1][1]), "+v"(fb[s ^ 1][1][2])::"memory");
+        }
+    };
+    // epilogue of row block rb (rows 16 rb + i16): dX = acc x(1 - x) (rowgemm256_b3_kernel's order), x rebuilt from the
+    // planes of columns 16w + 4g .. +3; one fp32 16-B store per lane over the X rows of this half, rows past M dropped
+    // by the buffer range
+    auto epilogue_rb = [&](long long t, int bb, const f32x4& acc, int rb) __attribute__((always_inline)) {
+        const int lane = fresh_lane();
+        const int i16 = lane & 15, g = lane >> 4, swi = stn_sw(i16);
+        const int r = 16 * rb + i16;
+        const unsigned xb = lds0 + bb * BUF + DOB + r * XP + 16 * ((2 * wave + (g >> 1)) ^ swi) + 8 * (g & 1);
+        u32x2 xr[3];
+        asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %3 offset:256\n\tds_read_b64 %2, %3 offset:512\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(xr[0]), "=&v"(xr[1]), "=&v"(xr[2])
+                     : "v"(xb)
+                     : "memory");
+        const long long row0 = t * TR;
+        const long long left = M - row0;
+        const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
+        const __amdgpu_buffer_rsrc_t rc =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(X) + row0 * D * 4, (short)0, nbytes, 0x00020000);
+        f32x4 v = acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float x = (bf_at(xr[0], q) + bf_at(xr[1], q)) + bf_at(xr[2], q);
+            v[q] = v[q] * (x * (1.0f - x));
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v, rc, (r * D + 128 * half + 16 * wave + 4 * g) * 4, 0, 0);
+    };
+
+    if (t_beg < t_end) {
+        stage(t_beg, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        convert(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        // per iteration: the DMA of tile t + 1, the sigma' MFMAs of tile t, then its TN MFMAs with the rest of the
+        // iteration's work issued behind them, one piece per 16-column block: the two epilogue row blocks of tile t,
+        // then (its DMA landed: only those two stores are younger) tile t + 1's six row conversions; one barrier
+        {
+            int b = 0;
+            for (long long t = t_beg; t < t_end; ++t) {
+                const bool more = t + 1 < t_end;
+                if (more) stage(t + 1, b ^ 1);
+                f32x4 acc[2];
+                mfma_sigma(b, acc);
+                mfma_tn(b, [&](int nb) __attribute__((always_inline)) {
+                    if (nb < 2) {
+                        epilogue_rb(t, b, acc[nb], nb);
+                    } else if (more) {
+                        if (nb == 2) wait_vm(2);
+                        convert_row(b ^ 1, nb - 2);
+                    }
+                });
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                b ^= 1;
+            }
+        }
+    }
+    float* out = slab + (long long)range * D * D;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = 128 * half + 32 * (wave & 3) + 16 * mb + 4 * g + j;
+                out[row * D + 128 * (wave >> 2) + 16 * nb + i16] = tacc[mb][nb][j];
+            }
 }
 
 // out[D][R] partial of A^T dz and colsum(dz) per block; slab row layout [(D+1)][R]
@@ -5062,6 +5427,10 @@ int iddgcn_sigma_tn_ranges(long long M) {
 int iddgcn_sigma_tn_bf16(void* stream, long long M, int d, const void* dO, void* X, const float* S, float* slab,
                          long long slab_floats, float* dS, int precision) {
     if (d != 256) return IDDGCN_E_BAD_DIM;
+    // the weights as a bf16 hi + lo pair for the fp32-operand modes, rounded to bf16 for IDDGCN_GEMM_BF16; nothing else
+    if (precision != IDDGCN_GEMM_EXACT_F32 && precision != IDDGCN_GEMM_SPLIT_F16 && precision != IDDGCN_GEMM_BF16X3 &&
+        precision != IDDGCN_GEMM_BF16)
+        return IDDGCN_E_BAD_ARG;
     if (M < 0 || !S || !slab || !dS || (M > 0 && (!dO || !X))) return IDDGCN_E_BAD_ARG;
     if (((uintptr_t)dO & 15) || ((uintptr_t)X & 15)) return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;
@@ -5076,6 +5445,25 @@ int iddgcn_sigma_tn_bf16(void* stream, long long M, int d, const void* dO, void*
     else
         hipLaunchKernelGGL(sigma_tn_bf16_kernel<false>, dim3((unsigned)(2 * nr)), dim3(512), 0, st, M, (int)tpb, nr,
                            (const __bf16*)dO, (__bf16*)X, S, slab);
+    int rc = launch_status();
+    if (rc) return rc;
+    launch_reduce_slabs(st, nr, n, slab, dS, 0, 1.0f);
+    return launch_status();
+}
+
+int iddgcn_sigma_tn_f32(void* stream, long long M, int d, const float* dO, float* X, const float* S, float* slab,
+                        long long slab_floats, float* dS, int precision) {
+    if (d != 256) return IDDGCN_E_BAD_DIM;
+    if (precision != IDDGCN_GEMM_BF16X3) return IDDGCN_E_BAD_ARG;
+    if (M < 0 || !S || !slab || !dS || (M > 0 && (!dO || !X))) return IDDGCN_E_BAD_ARG;
+    if (((uintptr_t)dO & 15) || ((uintptr_t)X & 15)) return IDDGCN_E_BAD_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const long long nt = (M + st3::TR - 1) / st3::TR;
+    const int nr = iddgcn_sigma_tn_ranges(M);
+    const long long tpb = nt > 0 ? (nt + nr - 1) / nr : 1;
+    const long long n = (long long)d * d;
+    if (slab_floats < nr * n) return IDDGCN_E_BAD_ARG;
+    hipLaunchKernelGGL(sigma_tn_b3_kernel, dim3((unsigned)(2 * nr)), dim3(512), 0, st, M, (int)tpb, nr, dO, X, S, slab);
     int rc = launch_status();
     if (rc) return rc;
     launch_reduce_slabs(st, nr, n, slab, dS, 0, 1.0f);

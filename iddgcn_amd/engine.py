@@ -86,6 +86,7 @@ class KerasAdam:
         self.lr, self.b1, self.b2, self.eps = learning_rate, beta_1, beta_2, epsilon
         self.m = torch.zeros_like(params.flat)
         self.v = torch.zeros_like(params.flat)
+        self._n_e = params["E"].numel()
         self.iterations = 0
 
     def alpha_at(self, t):
@@ -155,6 +156,14 @@ class KerasAdam:
         rs_e.wait()
         if e_hi > e_lo:
             self._apply_range(params, grads, e_lo, e_hi, alpha)
+
+    def gather_owned_state(self, shard):
+        """After apply_owned steps the Adam moments of E are partitioned by rows: each rank's m / v hold its own rows
+        [shard.a, shard.b) only (the others stay at their last all-reduced state).  All-gather them so every rank holds
+        the whole optimizer state (a checkpoint, or a switch back to a replicated update); the rows are the owners'
+        bitwise."""
+        for t in (self.m, self.v):
+            shard.all_gather(t[:self._n_e].view(shard.N, -1))
 
     def apply_table(self, params, grads, alpha_table, step):
         """apply() with alpha = alpha_table[step] read on the device (HIP-graph replay); the caller
@@ -295,6 +304,9 @@ class Engine:
             raise L.IddgcnError("edge_mfma='bf16' needs features='bf16' (bf16 edge tables)")
         self.edge_mfma = edge_mfma
         self.fuse_sigma_tn = True
+        # bf16 edge tables at R = 8, D = 256: the tail reduction adds the head chain's node terms (tail_seg_reduce_head)
+        # and head_dz finishes the head side; False runs the plain tail reduction + head_bwd_node (A/B, tests)
+        self.fuse_tail_head = True
         if not 1 <= num_relations <= 8:
             raise L.IddgcnError("num_relations must be in [1, 8]")
         if gemm not in GEMM_MODES:
@@ -370,10 +382,13 @@ class Engine:
 
     @property
     def sigma_tn_fused(self):
-        """bf16 edge tables at D = 256 (config 5's mode): a layer's dS TN and sigma' backward GEMM run as one pass over
-        do^l and x^{l-1} (ops.sigma_tn, ABI 11; the sigma' weights as ``edge_gemm`` takes them) instead of two
-        (``fuse_sigma_tn`` = False keeps the two kernels, for A/B)."""
-        return self.fuse_sigma_tn and self.features == "bf16" and self.D == 256
+        """A layer's dS TN and sigma' backward GEMM run as one pass over do^l and x^{l-1} (ops.sigma_tn) instead of two:
+        bf16 edge tables at D = 256 (config 5's mode, ABI 11; the sigma' weights as ``edge_gemm`` takes them), and fp32
+        tables in the bf16x3 mode at D = 256 (the headline, ABI 12).  ``fuse_sigma_tn`` = False keeps the two kernels,
+        for A/B."""
+        if not (self.fuse_sigma_tn and self.D == 256):
+            return False
+        return self.features == "bf16" or (self.edge_gemm == "bf16x3" and self._gemm == "bf16x3")
 
     @property
     def use_planes(self):
@@ -539,7 +554,7 @@ class Engine:
             side = self._side_stream() if (self.overlap and l > 0) else None
             # bf16 edge tables at R = 8, D = 256 (config 5): the tail reduction on MFMAs adds the head chain's node terms
             # (Wl[n] dO[n] into dP, dO[n] into dES) before its store, so the head backward below skips them
-            fused = self.features == "bf16" and R == 8 and D == 256 and self.node_shard is None
+            fused = self.fuse_tail_head and self.features == "bf16" and R == 8 and D == 256 and self.node_shard is None
             if side is not None:
                 side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(side):
@@ -631,6 +646,11 @@ class Engine:
         return float(self._pred_seed), False
 
     _e_pending = None      # the asynchronous all-gather of E after an owner-row Adam (node-partitioned train_step)
+    # node-partitioned train_step with E owned by rows: False (default) completes the all-gather of E before train_step
+    # returns, so params are whole for any reader (to_numpy, a checkpoint, predict) or writer (load); True leaves it in
+    # flight for the next forward to complete after its owner-local work (bench.py's timed loop) — until then the other
+    # ranks' rows of params["E"] are stale and must be neither read nor written (finish_pending() completes it)
+    overlap_e_gather = False
 
     def finish_pending(self):
         """Complete the all-gather of E a node-partitioned train_step left in flight (the next forward does it
@@ -726,7 +746,7 @@ class Engine:
         # bf16 edge tables at R = 8, D = 256 (config 5): layers 2 and 1 take the fused tail + head-term reduction (their
         # head seeds dO[a:b] are final: the node level of the layer above), then head_dz over the owned rows with the
         # reduce-scattered dWedge head sums; layer 3's head seeds are still on the wire during its tail reduction
-        fuse = self.features == "bf16" and R == 8 and D == 256
+        fuse = self.fuse_tail_head and self.features == "bf16" and R == 8 and D == 256
         for l in (2, 1, 0):
             Wl, Pl, Sl = ws.W[l], ws.P[l], P[f"S{l + 1}"]
             do = ws.xt[l]
@@ -811,6 +831,8 @@ class Engine:
             D = self.D
             opt.apply_owned(params, grads, comm, rs, sh.a * D, sh.b * D)
             self._e_pending = sh.all_gather(params["E"], async_op=True)
+            if not self.overlap_e_gather:
+                self.finish_pending()
             return grads.loss
         self.backward(params, grads, adj, ed, ws, comm)
         if comm is not None and hasattr(comm, "finish_each") and hasattr(opt, "apply_overlapped"):
@@ -824,6 +846,7 @@ class Engine:
     def predict(self, params, adj, ed, logits=False):
         """Probabilities p = sigmoid(s) of the scored edges (caller's order); with ``logits=True``
         also the pre-sigmoid DistMult scores s (IDDGCN.py:108)."""
+        self.finish_pending()
         ws = self.workspace(ed.T, False)
         self.forward(params, adj, ed, ws, False)
         return (ed.unsort(ws.p), ed.unsort(ws.s)) if logits else ed.unsort(ws.p)
@@ -843,6 +866,7 @@ class Engine:
     def loss_and_grads(self, params, grads, adj, ed, t_global=None, logits=False):
         """Forward + backward without the optimizer step: (loss sum, p) or, with ``logits=True``,
         (loss sum, p, s) — s the pre-sigmoid DistMult scores — all per edge in the caller's order."""
+        self.finish_pending()
         ws = self.workspace(ed.T, True)
         self._t_global = t_global
         self._want_p = True
@@ -896,3 +920,59 @@ def step_flops(N, R, D, T, M):
 def step_bytes(N, R, D, T, M, L=NUM_LAYERS):
     """Algorithmic HBM bytes of one training step (Q_hbm, fp32)."""
     return 40 * T * D + 8 * L * R * T * D + 24 * T + 16 * M + 16 * L * (R + 1) * N * D
+
+
+MALL_BYTES = 256 * 2 ** 20          # the Infinity Cache (MI355X_MICROARCH.md): a gathered table this small is read once
+LINE = 128                          # bytes an HBM access moves for a row gathered in random order (an L2 line)
+
+
+def step_bytes_impl(N, R, D, T, M, eb=4, fused_sigma_tn=True, fused_tail_head=False):
+    """Compulsory HBM bytes and GEMM work of one training step of THIS formulation (round 6), part by part (one part =
+    the launches of one Engine.forward / backward stage): every table a kernel needs read once and every table it
+    produces written once, where
+
+      * gathers of tail-sorted rows (P_r^l[t], ES1[t]) read each distinct node row once per kernel (the rows of a tail
+        run are consecutive edges: the distinct-row count, not R rows per scored edge as SURVEY §8(d)'s 8·L·R·T·D);
+      * the SpMMs' column gathers read the gathered table once if it fits the 256 MiB Infinity Cache, else one row per
+        stored entry (E at configs 4 / 5 is 1 GB: 4·M·D per SpMM);
+      * rows of fewer than 128 B gathered or scattered in random (head) order move one 128-B line each (W^l[h_e] into
+        the per-edge table, the dWedge head sums), the HBM access granularity.
+
+    eb: bytes per edge-table element (4 fp32, 2 in the bf16-feature mode).  fused_sigma_tn: the layer-2/3 dS TN and
+    sigma' backward as one pass (do^l, x^{l-1} read once) rather than two.  fused_tail_head: the R = 8 bf16 tail
+    reduction that adds the head chain's node terms (its head side reads only the dWedge head sums).
+    Returns (total bytes, {part: (bytes, algorithmic GEMM flop, "edge" | "node" | None)}); the flop sum is SURVEY
+    §8(d)'s W_gemm less the SpMMs.  bench.py step_roofline "impl" prices each part at the larger of its MFMA and HBM
+    time (a lower bound of a step whose parts run one after another); the PMC step totals of profiles/r06 show how
+    close the kernels come to the bytes."""
+    f = 4.0
+    NDf, RNDf, TDe = N * D * f, R * N * D * f, T * D * eb
+    G = 2.0 * D * D                                                           # flop per row of a D x D GEMM
+    small_row = lambda nbytes: max(float(nbytes), LINE)          # noqa: E731
+    gath_E = NDf if NDf <= MALL_BYTES else M * D * f
+    gath_dAE = RNDf if RNDf <= MALL_BYTES else M * D * f
+    L_ = NUM_LAYERS
+    p = {}
+    # forward
+    p["spmm_fwd"] = (4.0 * M + 4.0 * R * (N + 1) + gath_E + RNDf, 0.0, None)
+    p["projections"] = (RNDf + NDf + (L_ * RNDf + NDf), (L_ * R + 1) * G * N, "node")   # AE_r, E -> P_r^l, ES1
+    p["alpha"] = (L_ * (NDf + 2 * N * R * f), 0.0, None)
+    p["gather_W"] = (L_ * (4.0 * T + T * small_row(R * f)), 0.0, None)               # h_e, W^l[h_e] -> Wedge
+    p["head_chain"] = (L_ * (2 * NDf + RNDf + N * R * f), (L_ - 1) * G * N, "node")  # X^{l-1}|ES1, P^l, W^l -> X^l
+    p["tail_l1_combine"] = (NDf + RNDf + T * R * f + 4.0 * T + TDe, 0.0, None)       # ES1[t], P^1[t], Wedge -> x^1
+    p["tail_fwd_gemm"] = ((L_ - 1) * (2 * TDe + T * R * f + 4.0 * T + RNDf), (L_ - 1) * G * T, "edge")
+    p["distmult"] = (NDf + 2 * TDe + 16.0 * T + NDf, 0.0, None)                      # X^3[h], x^3 -> do^3, dO^3
+    # backward, per layer
+    if fused_tail_head:     # do, Wedge, P[t], dO, W -> dP, dWedge, <dO, P>; head side: dWedge[hperm] -> dz
+        p["tail_reduce"] = (L_ * (TDe + 2 * T * R * f + 2 * RNDf + NDf) + NDf, 0.0, None)
+        p["head_bwd"] = (L_ * (4.0 * T + T * small_row(R * f)), 0.0, None)
+    else:                   # do, Wedge, P[t] -> dP, dWedge (+dES); head side: dO, P, dP (rw), dWedge[hperm] -> dz
+        p["tail_reduce"] = (L_ * (TDe + 2 * T * R * f + 2 * RNDf) + NDf, 0.0, None)
+        p["head_bwd"] = (L_ * (NDf + 3 * RNDf + 4.0 * T + T * small_row(R * f)), 0.0, None)
+    p["edge_sigma_tn"] = ((L_ - 1) * (3 * TDe if fused_sigma_tn else 5 * TDe), 2 * (L_ - 1) * G * T, "edge")
+    p["node_tn"] = (L_ * (2 * NDf + 2 * RNDf + NDf + N * R * f), L_ * (R + 1) * G * N, "node")  # dS head, dK_r, dW_a
+    p["head_chain_bwd"] = (L_ * 3 * NDf, L_ * G * N, "node")                        # dO, X (dES) -> dO' (dE)
+    p["dAE"] = (L_ * 2 * RNDf + (L_ - 1) * RNDf, L_ * R * G * N, "node")             # dP (+ dAE) -> dAE
+    p["spmm_bwd"] = (4.0 * M + 4.0 * R * (N + 1) + gath_dAE + 2 * NDf, 0.0, None)
+    p["adam"] = (7 * NDf, 0.0, None)                                                 # E: var, m, v, g -> var, m, v
+    return sum(v[0] for v in p.values()), p

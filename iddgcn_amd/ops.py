@@ -200,16 +200,31 @@ def gemm_tn(A, B, C, slab, accumulate=False, a_planes=False, precision="exact"):
 
 
 def sigma_tn(dO, X, S, dS, slab, precision="exact"):
-    """A layer's edge backward GEMM pair over bf16 tables in one pass (iddgcn_sigma_tn_bf16, ABI 11):
-    dS = X^T dO (overwritten) and X = (dO S^T) * X (1 - X) in place; the weights as a bf16 hi + lo pair, or with
-    precision "bf16" rounded to bf16 (as rowgemm's bf16 form)."""
+    """A layer's edge backward GEMM pair in one pass (the autodiff of IDDGCN.py:62-63,79): dS = X^T dO (overwritten)
+    and X = (dO S^T) * X (1 - X) in place.
+      * bf16 tables (iddgcn_sigma_tn_bf16, ABI 11): the weights as a bf16 hi + lo pair ("exact", "split", "bf16x3"),
+        or rounded to bf16 ("bf16", as rowgemm's bf16 form);
+      * fp32 tables (iddgcn_sigma_tn_f32, ABI 12): precision "bf16x3" only (every operand split exactly into three
+        bf16 pieces; X bitwise the bf16x3 row GEMM's sigma' output)."""
     M, D = X.shape
-    _req(X, _BF16, (M, D), "X")
-    _req(dO, _BF16, (M, D), "dO")
+    prec = _prec(precision)
+    et = _BF16 if X.dtype == _BF16 else _F32
+    _req(X, et, (M, D), "X")
+    _req(dO, et, (M, D), "dO")
     _req(S, _F32, (D, D), "S")
     _req(dS, _F32, (D, D), "dS")
-    L.check(L.lib().iddgcn_sigma_tn_bf16(_stream(), M, D, _ptr(dO), _ptr(X), _ptr(S), _ptr(slab), slab.numel(),
-                                         _ptr(dS), L.GEMM_BF16 if precision == "bf16" else L.GEMM_EXACT_F32), "sigma_tn")
+    _req(slab, _F32, None, "slab")
+    if et == _BF16:
+        if prec not in (L.GEMM_EXACT_F32, L.GEMM_SPLIT_F16, L.GEMM_BF16X3, L.GEMM_BF16):
+            raise L.IddgcnError(f"sigma_tn: precision {precision!r} is not a form of the bf16 pass")
+        rc = L.lib().iddgcn_sigma_tn_bf16(_stream(), M, D, _ptr(dO), _ptr(X), _ptr(S), _ptr(slab), slab.numel(),
+                                          _ptr(dS), prec)
+    else:
+        if prec != L.GEMM_BF16X3:
+            raise L.IddgcnError(f"sigma_tn: fp32 tables take precision 'bf16x3' only, got {precision!r}")
+        rc = L.lib().iddgcn_sigma_tn_f32(_stream(), M, D, _ptr(dO), _ptr(X), _ptr(S), _ptr(slab), slab.numel(),
+                                         _ptr(dS), prec)
+    L.check(rc, "sigma_tn")
 
 
 def sigma_tn_slab_floats(M, D=256):

@@ -1,17 +1,20 @@
-"""Data parallelism for the full-batch step (one process per GPU, RCCL over xGMI).
+"""Data parallelism for the full-batch step (one process per GPU, RCCL over xGMI; SURVEY §8(e)).
 
-Two partitions of the step.  Node-row partitioning (NodeShard below, bench.py's default with more
-than one GPU) splits the node rows and takes the scored edges by tail.  Edge partitioning (``--shard edge``; the
-default of IDDGCN_Model.fit's multi-rank branch; described in the rest of this paragraph): the scored edges of a
-full-batch step are independent given the node tables, so each rank takes a contiguous slice of them; the graph (CSR
-of every A_r) and all parameters are replicated.  Every gradient of the step is a sum over scored
-edges, so the per-rank gradients — already normalised by the GLOBAL edge count — are summed by an
-all-reduce of the flat gradient buffer IN PLACE (FlatParams.buf = [E | rel | layer params | loss]),
-after which Adam runs identically on every rank.  There is no other collective on the data path.
+The default with more than one GPU is node-row partitioning (NodeShard below; bench.py --shard node).  Rank k owns
+a contiguous range of node rows, balanced by tail edges plus node work (node_ranges / node_row_weight), and takes the
+scored edges whose TAIL it owns, so every tail-side quantity is local.  The node tables of the owned rows are
+computed locally.  What crosses ranks is the head side (W^l and X^3 all-gathered, the head seeds reduce-scattered),
+the small weight gradients (all-reduced) and E: dE is reduce-scattered to the row owners, each owner runs Keras Adam
+over its rows, and E is all-gathered in per-owner pieces that the next forward consumes as they land
+(Engine.forward's owner-split SpMM).
 
-The all-reduce is bucketed and overlapped with the end of the backward (BucketedAllReduce): the
-small gradients + loss go out as soon as the layer loop ends, then dE in row chunks as the
-transposed SpMM finishes each chunk (engine.Engine.backward).
+Two alternatives are kept as flags:
+  * edge partitioning (``--shard edge``; also IDDGCN_Model.fit's multi-rank branch): each rank takes a contiguous
+    slice of the scored edges, the graph and parameters are replicated, and the flat gradient buffer
+    [E | rel | layer params | loss] is all-reduced IN PLACE in buckets (BucketedAllReduce) overlapped with the end
+    of the backward, after which Adam runs identically on every rank;
+  * relation-sharded node tables (RelationShard, ``--shard relation``): the (relation, row) rows of A_r E and P_r^l
+    split over the ranks, P^l all-gathered, dP^l reduce-scattered.
 """
 import numpy as np
 import torch.distributed as dist

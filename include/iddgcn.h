@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define IDDGCN_ABI_VERSION 11
+#define IDDGCN_ABI_VERSION 12
 
 #define IDDGCN_E_BAD_DIM   (-1)   /* D not in {32,64,128,256} */
 #define IDDGCN_E_BAD_REL   (-2)   /* R < 0 or R > 8 */
@@ -87,6 +87,10 @@ extern "C" {
 #define IDDGCN_PLANES_AUX  4      /* the sigma' operand aux is planes rows (act DSIGMOID) */
 
 int iddgcn_abi_version(void);
+/* ABI 12: sha256 (hex) of the sources the library was built from (the .hip sources and device_flags.txt of
+ * iddgcn_amd/csrc, the headers in include/; iddgcn_amd/_srchash.py), written into the library by the build; the
+ * Python loader refuses a library whose digest is not the tree's. */
+const char* iddgcn_source_sha256(void);
 
 /* Y[s][n][:] = (accumulate ? Y[s][n][:] : 0) + sum_{k=ptr[s*(n_rows+1)+n]}^{..+1} (vals ? vals[k] : 1) * X[col[k]][:]
  * for s in [0, n_seg).  One CSR per relation, row_ptr holds absolute offsets into col/vals.
@@ -323,10 +327,20 @@ int iddgcn_gemm_tn_bf16(void* stream, long long M, int d, const void* A, const v
  *   X  = (dO S^T) * X (1 - X)  (in place: dx^{l-1} over x^{l-1}; bf16 hi + lo weights, or with precision
  *        IDDGCN_GEMM_BF16 the weights rounded to bf16 as iddgcn_rowgemm_bf16 takes them; fp32 accumulation)
  * X and dO are M x 256 bf16 (16-B aligned), S 256 x 256 fp32; slab holds iddgcn_sigma_tn_ranges(M) * 256 * 256
- * floats of partials (slab_floats is checked).  D = 256 only. */
+ * floats of partials (slab_floats is checked); precision: IDDGCN_GEMM_EXACT_F32, _SPLIT_F16 or _BF16X3 (the hi + lo
+ * weights) or IDDGCN_GEMM_BF16, anything else IDDGCN_E_BAD_ARG.  D = 256 only. */
 int iddgcn_sigma_tn_ranges(long long M);
 int iddgcn_sigma_tn_bf16(void* stream, long long M, int d, const void* dO, void* X, const float* S, float* slab,
                          long long slab_floats, float* dS, int precision);
+
+/* ABI 12: the same pass over fp32 tables in the bf16x3 operand mode (the headline's layer-2/3 edge backward, configs
+ * 3 / 4; replaces iddgcn_gemm_tn_f32 + iddgcn_rowgemm_f32 with act DSIGMOID at precision IDDGCN_GEMM_BF16X3):
+ *   dS = X^T dO (overwritten) and X = (dO S^T) * X (1 - X) in place, every operand split exactly into three bf16
+ *   pieces (six products, fp32 accumulation); X is bitwise the row GEMM's sigma' output.
+ * X and dO are M x 256 fp32 (16-B aligned); slab holds iddgcn_sigma_tn_ranges(M) * 256 * 256 floats; precision must
+ * be IDDGCN_GEMM_BF16X3 (anything else: IDDGCN_E_BAD_ARG).  D = 256 only. */
+int iddgcn_sigma_tn_f32(void* stream, long long M, int d, const float* dO, float* X, const float* S, float* slab,
+                        long long slab_floats, float* dS, int precision);
 
 /* The run form of iddgcn_combine_f32 (y_idx == v_idx = idx, coefficients per row) writing bf16 out. */
 int iddgcn_combine_bf16(void* stream, int M, int d, int R, const float* Y, const int* idx, const float* coef,

@@ -120,7 +120,7 @@ def test_fit_world2_gloo_one_gpu_equals_single_process(cuda):
         assert np.abs(g0[k] - g).max() <= 2e-4 * np.abs(g).max() + 1e-30, k
 
 
-def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact", features="f32"):
+def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact", features="f32", ab_fuse=False):
     """One data-parallel step (forward + backward + bucketed all-reduce, no Adam) on this rank's shard of
     the scored edges, edge-partitioned or with relation-sharded node tables.  "edge_device": the
     bucketed all-reduce on its device branch (asynchronous, in place on the GPU buckets, ordered after
@@ -159,7 +159,17 @@ def _step_worker(rank, world, port, q, mode, N, R, D, gemm="exact", features="f3
         eng.backward(P, G, adj, ed, ws, comm)
         comm.finish()
         torch.cuda.synchronize()
-        q.put((rank, float(G.loss.item()), G.to_numpy()))
+        if not ab_fuse:
+            q.put((rank, float(G.loss.item()), G.to_numpy()))
+            return
+        # the same step with the fused R = 8 tail + head-term reduction switched off (Engine.fuse_tail_head)
+        fused = G.to_numpy()
+        eng.fuse_tail_head = False
+        eng.forward(P, adj, ed, ws, True)
+        eng.backward(P, G, adj, ed, ws, comm)
+        comm.finish()
+        torch.cuda.synchronize()
+        q.put((rank, fused, G.to_numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -273,6 +283,32 @@ def test_node_sharded_step_equals_full_batch(world, N, R, D, gemm, mode, feature
     assert abs(l - full_loss) <= bl * full_loss
     for k, v in full.items():
         assert np.abs(g[k] - v).max() <= bg * np.abs(v).max() + 1e-30, k
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_node_sharded_fused_tail_head_ab(world, cuda):
+    """the node-row backward of config 5's mode (R = 8, bf16 edge tables) takes the fused tail + head-term
+    reduction (tail_seg_reduce_head on the owned tail segments, head_dz over the reduce-scattered dWedge head sums)
+    for layers 1-2.  The same sharded step with the fusion off (plain tail reduction + head_bwd_node, the path the
+    fp32 R = 8 case pins at 1e-5) reads the same bf16 edge tables and differs only in fp32 summation order: every
+    gradient within 1e-5 of max|g| (a missing or doubled small term would not be), bitwise equal across ranks."""
+    N, R, D = 800, 8, 256
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q, "node_device", N, R, D, "split", "bf16", True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for o in out[1:]:
+        assert all(np.array_equal(o[1][k], out[0][1][k]) for k in o[1])
+    fused, plain = out[0][1], out[0][2]
+    for k, v in plain.items():
+        assert np.abs(fused[k] - v).max() <= 1e-5 * np.abs(v).max() + 1e-30, (k, np.abs(fused[k] - v).max())
 
 
 def _adam_worker(rank, world, port, q, mode):

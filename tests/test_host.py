@@ -30,10 +30,112 @@ def test_library_exports_every_header_symbol():
     assert lib.iddgcn_abi_version() == _lib.ABI_VERSION
 
 
+def test_library_is_tied_to_its_sources(tmp_path):
+    """The product library carries the digest of the sources it was built from (iddgcn_source_sha256, ABI 12) and
+    it is this tree's; a library whose digest differs (a stale build at the same ABI) is refused by the loader."""
+    import subprocess
+    from iddgcn_amd import _srchash
+    lib = _lib.load()
+    assert _lib.library_source_sha256(lib) == _srchash.source_sha256()
+    files = _srchash.source_files()
+    assert "iddgcn_amd/csrc/iddgcn_hip.hip" in files and "include/iddgcn.h" in files
+    assert "iddgcn_amd/csrc/device_flags.txt" in files
+    # a stand-in library at the right ABI but built from other sources
+    src = tmp_path / "stale.c"
+    src.write_text(f'int iddgcn_abi_version(void) {{ return {_lib.ABI_VERSION}; }}\n'
+                   f'const char* iddgcn_source_sha256(void) {{ return "{"0" * 64}"; }}\n')
+    so = tmp_path / "libstale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    with pytest.raises(_lib.StaleLibraryError):
+        _lib.load(str(so), check_source=True)
+    # one without any digest is refused as well
+    src.write_text(f'int iddgcn_abi_version(void) {{ return {_lib.ABI_VERSION}; }}\n')
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    with pytest.raises(_lib.StaleLibraryError):
+        _lib.load(str(so), check_source=True)
+
+
+_ASM = None
+
+
+def _library_asm():
+    """The gfx950 disassembly of every code object in libiddgcn_hip.so (cached)."""
+    global _ASM
+    if _ASM is None:
+        _ASM = _disassemble()
+    return _ASM
+
+
 def test_library_has_no_packed_fp32_valu():
     """The product library is built without packed-fp32 VALU (iddgcn_amd/csrc/device_flags.txt; DESIGN.md
     §Determinism): disassemble the gfx950 code object of libiddgcn_hip.so and find no v_pk_fma_f32 / v_pk_mul_f32 /
     v_pk_add_f32 / v_pk_mov_b32."""
+    asm = _library_asm()
+    assert "radix" in asm and "tail_seg_reduce" in asm     # every translation unit's kernels were disassembled
+    assert asm.count("s_endpgm") > 50          # the kernels really were disassembled
+    bad = sorted(set(re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", asm)))
+    assert not bad, f"packed-fp32 VALU in the product library: {bad}"
+
+
+def _kernel_bodies(asm, pattern):
+    """{symbol: [instruction lines]} of the kernels whose symbol matches ``pattern`` (llvm-objdump -d layout: a
+    `<symbol>:` header, then one instruction per line)."""
+    out, cur = {}, None
+    for line in asm.split("\n"):
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+        if m:
+            cur = m.group(1) if re.search(pattern, m.group(1)) else None
+            if cur:
+                out[cur] = []
+            continue
+        if cur and line.strip():
+            ins = line.split("//")[0].strip()
+            if ins:
+                out[cur].append(ins)
+    return out
+
+
+def _regs(text):
+    """VGPR numbers named in an operand list (v7, v[4:7])."""
+    regs = set()
+    for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", text):
+        regs.update(range(int(a), int(b) + 1))
+    regs.update(int(x) for x in re.findall(r"\bv(\d+)\b", text))
+    return regs
+
+
+def test_asm_transposed_reads_are_waited_for():
+    """the TN kernels issue ds_read_b64_tr_b16 from inline asm (hipcc guards the builtin with a vmcnt(0)
+    drain), so the compiler does not know the result arrives late; correctness rests on nothing touching a
+    destination register before the tied `s_waitcnt lgkmcnt(0)`.  Walk the machine code of every such kernel: between
+    a transposed read and the next lgkmcnt(0) no instruction names one of its destination VGPRs (read, copied, spilled
+    or overwritten), and the kernels use no scratch."""
+    asm = _library_asm()
+    kernels = _kernel_bodies(asm, r"gemm_tn256_b3_kernel|gemm_tn256_bf16t_kernel|sigma_tn_bf16_kernel|sigma_tn_b3_kernel")
+    assert len(kernels) >= 5, sorted(kernels)       # both sigma_tn_bf16 forms, the two TNs, the fused bf16x3 pass
+    for name, body in kernels.items():
+        assert not any(i.startswith("scratch_") for i in body), f"{name}: scratch spill"
+        pending, n_tr = {}, 0
+        for k, ins in enumerate(body):
+            op, _, args = ins.partition(" ")
+            if op == "s_waitcnt" and "lgkmcnt(0)" in args:
+                pending = {}
+                continue
+            if op == "ds_read_b64_tr_b16":
+                n_tr += 1
+                dst, _, addr = args.partition(",")
+                hit = _regs(args) & set(pending)
+                assert not hit, f"{name}: {ins!r} names pending v{sorted(hit)} (line {k})"
+                for r in _regs(dst):
+                    pending[r] = k
+                continue
+            hit = _regs(args) & set(pending)
+            assert not hit, f"{name}: {ins!r} at line {k} names v{sorted(hit)} before the lgkmcnt(0) of the transposed " \
+                            f"read at line {min(pending[r] for r in hit)}"
+        assert n_tr > 0, name
+
+
+def _disassemble():
     import subprocess
     import tempfile
     llvm = "/opt/rocm/lib/llvm/bin"
@@ -56,10 +158,7 @@ def test_library_has_no_packed_fp32_valu():
                            capture_output=True)
             asm += subprocess.run([os.path.join(llvm, "llvm-objdump"), "-d", dev], check=True, capture_output=True,
                                   text=True).stdout
-    assert "radix" in asm and "tail_seg_reduce" in asm     # every translation unit's kernels were disassembled
-    assert asm.count("s_endpgm") > 50          # the kernels really were disassembled
-    bad = sorted(set(re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", asm)))
-    assert not bad, f"packed-fp32 VALU in the product library: {bad}"
+    return asm
 
 
 def test_block_helpers_are_pure_host():
@@ -75,6 +174,12 @@ def test_invalid_args_rejected_before_launch():
     assert lib.iddgcn_spmm_csr_f32(None, 1, 4, 48, None, None, None, None, None, 0) == -1
     assert lib.iddgcn_alpha_fwd_f32(None, 4, 64, 9, None, None, None, None, None, None) == -2
     assert lib.iddgcn_adam_f32(None, 4, None, None, None, None, 1.0, .9, .999, 1e-7, 0) == -3
+    # the fused sigma' + TN passes accept only their documented operand forms (checked before anything else)
+    assert lib.iddgcn_sigma_tn_f32(None, 0, 256, None, None, None, None, 0, None, _lib.GEMM_EXACT_F32) == -3
+    assert lib.iddgcn_sigma_tn_f32(None, 0, 256, None, None, None, None, 0, None, 7) == -3
+    assert lib.iddgcn_sigma_tn_f32(None, 0, 128, None, None, None, None, 0, None, _lib.GEMM_BF16X3) == -1
+    assert lib.iddgcn_sigma_tn_bf16(None, 0, 256, None, None, None, None, 0, None, 7) == -3
+    assert lib.iddgcn_sigma_tn_bf16(None, 0, 256, None, None, None, None, 0, None, _lib.GEMM_F32_4CHAIN) == -3
 
 
 @pytest.mark.parametrize("k", [0, 3])
@@ -292,3 +397,19 @@ def test_bf16x3_kernel_selection_is_pure_host():
         assert kid(**kw) == exact(**kw) < 500, kw
     # the TN entry accepts the mode (invalid arguments still refused before any launch)
     assert lib.iddgcn_gemm_tn_f32(None, 32, 256, None, None, None, 1, None, 0, _lib.GEMM_BF16X3) == -3
+
+
+def test_step_bytes_impl_is_a_lower_bound_of_the_measured_step():
+    """engine.step_bytes_impl (round 6, bench.py step_roofline "impl"): the compulsory HBM bytes of the implemented step
+    stay below the PMC-measured step they model — config 5 before the fused sigma' + TN pass (profiles/r05/cfg5/
+    step_pmc_bytes_r05c5pmc.txt: read 717.6 GB + write 261.8 GB = 979 GB) — and within 10% of it; its GEMM work is
+    SURVEY §8(d)'s W_gemm less the SpMMs; the fused pass saves exactly one read of do^l and x^{l-1} per layer 2-3."""
+    from iddgcn_amd.engine import step_bytes_impl, step_flops
+    N, R, D, M = 1_000_000, 8, 256, 40_000_000
+    T = M + M // 4
+    q, parts = step_bytes_impl(N, R, D, T, M, eb=2, fused_sigma_tn=False, fused_tail_head=True)
+    measured = 717.6e9 + 261.8e9
+    assert 0.9 * measured <= q <= measured, q / measured
+    assert abs(sum(v[1] for v in parts.values()) - (step_flops(N, R, D, T, M) - 4 * M * D)) < 1e-6 * q
+    qf, _ = step_bytes_impl(N, R, D, T, M, eb=2, fused_sigma_tn=True, fused_tail_head=True)
+    assert q - qf == 2 * 2 * T * D * 2

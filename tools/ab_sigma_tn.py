@@ -1,11 +1,12 @@
-"""A/B of the fused sigma' backward + dS TN pass (ops.sigma_tn, ABI 11) against the two kernels it replaces
-(gemm_tn256_bf16t_kernel + the v3 sigma' kernel) on config 5's real buffers (N = 1M, R = 8, T = 50M, bf16 edge
-tables; the engine built as bench.py builds it, one training step first): per-launch times (HIP events, the x table
-restored before each launch, not timed), the two results compared, then whole training steps with
-Engine.fuse_sigma_tn on and off, alternated.
+"""A/B of the fused sigma' backward + dS TN pass (ops.sigma_tn) against the two kernels it replaces, on a bench
+config's real buffers (the engine built as bench.py builds it, one training step first): per-launch times (HIP
+events, the x table restored before each launch, not timed), the two results compared, then whole training steps
+with Engine.fuse_sigma_tn on and off, alternated.
+  config 5 (N = 1M, R = 8, T = 50M, bf16 edge tables; ABI 11): gemm_tn256_bf16t_kernel + the v3 sigma' kernel;
+  config 3 (N = 100k, R = 2, T = 4M, fp32 tables, bf16x3; ABI 12): gemm_tn256_b3_kernel + rowgemm256_b3_kernel<0, 1>.
 
-usage: python tools/ab_sigma_tn.py [reps] [lib.so ...]   (libraries: the fused kernel and the step timed per build,
-dx of each compared with the first build's)
+usage: python tools/ab_sigma_tn.py [reps] [--config 3|5] [lib.so ...]   (libraries: the fused kernel and the step
+timed per build, dx of each compared with the first build's)
 """
 import sys
 import time
@@ -24,16 +25,19 @@ from iddgcn_amd.utils import synthetic_graph  # noqa: E402
 from tools.bench_mem import load_lenient  # noqa: E402
 
 
-def main(reps=5):
-    cfg = CONFIGS[5]
+def main(reps=5, config=5, libs=()):
+    cfg = CONFIGS[config]
     N, R, D, M = cfg["N"], cfg["R"], cfg["D"], cfg["M"]
     dev = torch.device("cuda", 0)
-    pos, _ = synthetic_graph(N, R, M, seed=0)
-    neg = negative_samples(pos[::cfg["neg_every"]], N, 89, device=dev)
+    pos, neg0 = synthetic_graph(N, R, M, seed=0)
+    neg = negative_samples(pos[::cfg["neg_every"]], N, 89, device=dev) if "neg_every" in cfg else neg0
     tri = np.concatenate([pos, neg])
     lab = np.concatenate([np.ones(len(pos), np.float32), np.zeros(len(neg), np.float32)])
     T = len(tri)
-    eng = Engine(N, R, D, dev, gemm=cfg["gemm"], features="bf16")
+    feat = cfg.get("features", "f32")
+    gemm = cfg.get("gemm", "bf16x3")
+    prec = "bf16x3" if feat == "f32" else "exact"
+    eng = Engine(N, R, D, dev, gemm=gemm, features=feat)
     adj = get_adj_mats(pos, N, R, device=dev)
     ed = eng.edges(tri, lab)
     P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
@@ -48,13 +52,13 @@ def main(reps=5):
     dS_a, dS_b = torch.empty(D, D, device=dev), torch.empty(D, D, device=dev)
 
     def two():
-        ops.gemm_tn(xs, do, dS_a, ws.tn_slab)
-        ops.rowgemm(do, S, xs, b_trans=True, act=L.ACT_DSIGMOID, aux=xs)
+        ops.gemm_tn(xs, do, dS_a, ws.tn_slab, precision=prec)
+        ops.rowgemm(do, S, xs, b_trans=True, act=L.ACT_DSIGMOID, aux=xs, precision=prec)
 
     def fused():
-        ops.sigma_tn(do, xs, S, dS_b, ws.tn_slab)
+        ops.sigma_tn(do, xs, S, dS_b, ws.tn_slab, precision=prec)
 
-    libs = sys.argv[2:] or [None]
+    libs = list(libs) or [None]
 
     def timed(fn, label):
         ts = []
@@ -104,4 +108,9 @@ def main(reps=5):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 5)
+    args = sys.argv[1:]
+    reps = int(args.pop(0)) if args and args[0].lstrip("-").isdigit() else 5
+    config = 5
+    if args[:1] == ["--config"]:
+        config, args = int(args[1]), args[2:]
+    main(reps, config, args)

@@ -28,7 +28,8 @@ SYMBOLS = {
     # bf16x3 operands (ABI 7): the column-half row GEMM and the transposed-read TN
     "bf16x3": {"tail_fwd_gemm": "rowgemm256_b3_kernel<2, false, false>",
                "tail_bwd_gemm": "rowgemm256_b3_kernel<0, true, false>",
-               "tail_dS_tn": "gemm_tn256_b3_kernel"},
+               "tail_dS_tn": "gemm_tn256_b3_kernel",
+               "tail_bwd_sigma_tn": "sigma_tn_b3_kernel"},           # round 6: the fused pass (ABI 12)
     "exact": {"tail_fwd_gemm": "rowgemm256_v3_kernel<2, false, true, false, false, false, false, false>",
               "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, false, false, false, false, false>",
               "tail_dS_tn": "gemm_tn256_dma_kernel"},
@@ -36,7 +37,8 @@ SYMBOLS = {
     # bench's gemm key with `python tools/pmc_traffic.py ... exact synthetic-5 1 profiles/r03 bf16`
     "bf16": {"tail_fwd_gemm": "fwd_gather8_bf16_kernel",
              "tail_bwd_gemm": "rowgemm256_v3_kernel<0, true, false, true, false, true, false, false>",
-             "tail_dS_tn": "gemm_tn256_bf16t_kernel"},
+             "tail_dS_tn": "gemm_tn256_bf16t_kernel",
+             "tail_bwd_sigma_tn": "sigma_tn_bf16_kernel"},         # round 5: the fused pass (ABI 11)
 }
 
 
