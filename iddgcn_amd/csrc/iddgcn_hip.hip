@@ -2037,6 +2037,9 @@ __device__ __forceinline__ void row_to_planes3(char* row, int lane) {
 //   * epilogue as the v3 kernel: gathered P_r[t] rows (the tile's distinct tails), per-edge coefficients
 //     and sigma' rows (or, accumulating, the old C rows) DMA'd into wave-private slabs ([32][16] fp32, XOR-swizzled 16-B groups); waves 4-7 run
 //     the epilogue of tile t-1 while waves 0-3 run tile t's MFMAs on the same SIMDs; one barrier per tile.
+__device__ __forceinline__ unsigned lds_u32(const void* p) {
+    return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
 namespace rb3 {
 constexpr int D = 256, NW = 8, TR = 32, CWG = 128, CWV = 16;
 constexpr int PITCH = 1568;                 // A row slot: three 512-B planes + 32 B
@@ -2233,6 +2236,9 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
         }
         return 2;
     };
+    // Measured and not kept (round 6, profiles/r06/ab_gemm_fwd_interleave_r06c.txt): the next tile's four rows converted
+    // inside this tile's MFMA phase (each row's read issued with a k-step's fragment reads, its split and stores behind
+    // that k-step's MFMAs): bitwise the same, forward 3.333 vs 3.278 ms, sigma' 3.334 vs 3.274, plain 2.925 vs 2.930
     auto mfma_tile = [&](int bb, f32x4 (&acc)[2]) __attribute__((always_inline)) {
         f32x4 hi0 = {0.f, 0.f, 0.f, 0.f}, lo0 = hi0, hi1 = hi0, lo1 = hi0;
         // Fragment reads in inline asm, one k-step ahead of the MFMAs that use them, each k-step's MFMAs behind an
@@ -2564,9 +2570,6 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
 namespace st3 {
 constexpr int D = 256, TR = 32, DP = 1536, XP = 768, DOB = TR * DP, XB = TR * XP, BUF = DOB + XB, NBUF = 2;
 }  // namespace st3
-__device__ __forceinline__ unsigned lds_u32(const void* p) {
-    return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
-}
 // three transposed reads at a, a + PS, a + 2 PS (the three planes of one 4-row block).  Every multi-instruction asm
 // read here marks its outputs early-clobber ("=&v"): without it the compiler may give an output the input address
 // register, which the first read then overwrites (asynchronously) while the later reads still use it as address
@@ -2672,36 +2675,42 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
         }
         return n;
     };
-    // row j of this wave's share of buffer bb, fp32 -> three bf16 planes in place: j < 4 the dO row 4w + j, j = 4, 5 the
-    // X-half pair 4w + 2(j - 4), +1 (the 1-KiB read completes before the writes, which overwrite its bytes and, for a
-    // pair, the second row's)
-    auto convert_row = [&](int bb, int j) __attribute__((always_inline)) {
+    // this wave's rows of buffer bb, fp32 -> three bf16 planes in place: the six 1-KiB reads first (one wait), then the
+    // writes (a row's planes overwrite its own fp32 bytes and, for an X pair, the second row's)
+    auto convert = [&](int bb) __attribute__((always_inline)) {
         char* base = lds + bb * BUF;
         const int lane = fresh_lane();
-        u32x4 v;
-        const bool dor = j < 4;
-        const int r0 = dor ? 4 * wave + j : 4 * wave + 2 * (j - 4);
-        char* src = dor ? base + r0 * DP : base + DOB + r0 * XP;
-        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_u32(src) + 16 * lane) : "memory");
-        bf16x4 p0, p1, p2;
-        split3x4(__builtin_bit_cast(f32x4, v), p0, p1, p2);
-        char* row;
-        int ps;
-        if (dor) {
-            row = base + r0 * DP + 16 * ((lane >> 1) ^ stn_sw(r0)) + 8 * (lane & 1);
-            ps = 512;
-        } else {
-            const int r = r0 + (lane >> 5);
-            row = base + DOB + r * XP + 16 * (((lane & 31) >> 1) ^ stn_sw(r)) + 8 * (lane & 1);
-            ps = 256;
-        }
-        *reinterpret_cast<bf16x4*>(row) = p0;
-        *reinterpret_cast<bf16x4*>(row + ps) = p1;
-        *reinterpret_cast<bf16x4*>(row + 2 * ps) = p2;
-    };
-    auto convert = [&](int bb) __attribute__((always_inline)) {
+        u32x4 v[6];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) convert_row(bb, j);
+        for (int j = 0; j < 4; ++j)
+            asm volatile("ds_read_b128 %0, %1" : "=v"(v[j]) : "v"(lds_u32(base + (4 * wave + j) * DP) + 16 * lane) : "memory");
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+            asm volatile("ds_read_b128 %0, %1"
+                         : "=v"(v[4 + p])
+                         : "v"(lds_u32(base + DOB + (4 * wave + 2 * p) * XP) + 16 * lane)
+                         : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5])::"memory");
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = 4 * wave + j;
+            char* row = base + r * DP + 16 * ((lane >> 1) ^ stn_sw(r)) + 8 * (lane & 1);
+            bf16x4 p0, p1, p2;
+            split3x4(__builtin_bit_cast(f32x4, v[j]), p0, p1, p2);
+            *reinterpret_cast<bf16x4*>(row) = p0;
+            *reinterpret_cast<bf16x4*>(row + 512) = p1;
+            *reinterpret_cast<bf16x4*>(row + 1024) = p2;
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int r = 4 * wave + 2 * p + (lane >> 5);
+            char* row = base + DOB + r * XP + 16 * (((lane & 31) >> 1) ^ stn_sw(r)) + 8 * (lane & 1);
+            bf16x4 p0, p1, p2;
+            split3x4(__builtin_bit_cast(f32x4, v[4 + p]), p0, p1, p2);
+            *reinterpret_cast<bf16x4*>(row) = p0;
+            *reinterpret_cast<bf16x4*>(row + 256) = p1;
+            *reinterpret_cast<bf16x4*>(row + 512) = p2;
+        }
     };
     // sigma': row fragment of row i16 (+16 rb) at k-step q, plane j: chunk (4q + g) ^ swi = 4(q ^ sa) + (g ^ sl)
     auto mfma_sigma = [&](int bb, f32x4 (&acc)[2]) __attribute__((always_inline)) {
@@ -2766,8 +2775,7 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
         acc[0] = hi0 + lo0;
         acc[1] = hi1 + lo1;
     };
-    // hook(nb): VALU / LDS work issued right behind column block nb's twelve MFMAs (it runs in their shadow)
-    auto mfma_tn = [&](int bb, auto&& hook) __attribute__((always_inline)) {
+    auto mfma_tn = [&](int bb) __attribute__((always_inline)) {
         // transposed-read rows of this lane (first / second read of a fragment) and their swizzles; the byte of the
         // lane's 4 columns in a row of 16-column block blk is 16 ((2 blk) ^ (sw & 14)) + 16 (tb ^ (sw & 1)) + 8 (l & 1)
         const int lane = fresh_lane();
@@ -2822,40 +2830,44 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
             tacc[0][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][0], b0, tacc[0][nb] + e0, 0, 0, 0);
             tacc[1][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][0], b0, tacc[1][nb] + e1, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            hook(nb);
-            __builtin_amdgcn_sched_barrier(0);
             if (nb + 1 < 8)
                 asm volatile("s_waitcnt lgkmcnt(0)"
                              : "+v"(fb[s ^ 1][0][0]), "+v"(fb[s ^ 1][0][1]), "+v"(fb[s ^ 1][0][2]), "+v"(fb[s ^ 1][1][0]),
                                "+v"(fb[s ^ 1][1][1]), "+v"(fb[s ^ 1][1][2])::"memory");
         }
     };
-    // epilogue of row block rb (rows 16 rb + i16): dX = acc x(1 - x) (rowgemm256_b3_kernel's order), x rebuilt from the
-    // planes of columns 16w + 4g .. +3; one fp32 16-B store per lane over the X rows of this half, rows past M dropped
-    // by the buffer range
-    auto epilogue_rb = [&](long long t, int bb, const f32x4& acc, int rb) __attribute__((always_inline)) {
+    // epilogue: dX = acc x(1 - x) (rowgemm256_b3_kernel's order), x rebuilt from the planes of columns 16w + 4g .. +3;
+    // fp32 16-B stores over the X rows of this half, rows past M dropped by the buffer range.  Returns its store count.
+    auto epilogue = [&](long long t, int bb, const f32x4 (&acc)[2]) __attribute__((always_inline)) -> int {
         const int lane = fresh_lane();
         const int i16 = lane & 15, g = lane >> 4, swi = stn_sw(i16);
-        const int r = 16 * rb + i16;
-        const unsigned xb = lds0 + bb * BUF + DOB + r * XP + 16 * ((2 * wave + (g >> 1)) ^ swi) + 8 * (g & 1);
-        u32x2 xr[3];
-        asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %3 offset:256\n\tds_read_b64 %2, %3 offset:512\n\t"
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=&v"(xr[0]), "=&v"(xr[1]), "=&v"(xr[2])
-                     : "v"(xb)
-                     : "memory");
+        const unsigned xb = lds0 + bb * BUF + DOB + 16 * ((2 * wave + (g >> 1)) ^ swi) + 8 * (g & 1);
+        u32x2 xr[2][3];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+            asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %3 offset:256\n\tds_read_b64 %2, %3 offset:512"
+                         : "=&v"(xr[rb][0]), "=&v"(xr[rb][1]), "=&v"(xr[rb][2])
+                         : "v"(xb + (16 * rb + i16) * XP)
+                         : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(xr[0][0]), "+v"(xr[0][1]), "+v"(xr[0][2]), "+v"(xr[1][0]), "+v"(xr[1][1]), "+v"(xr[1][2])::"memory");
         const long long row0 = t * TR;
         const long long left = M - row0;
         const unsigned nbytes = (unsigned)((left < TR ? left : TR) * D * 4);
         const __amdgpu_buffer_rsrc_t rc =
             __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(X) + row0 * D * 4, (short)0, nbytes, 0x00020000);
-        f32x4 v = acc;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float x = (bf_at(xr[0], q) + bf_at(xr[1], q)) + bf_at(xr[2], q);
-            v[q] = v[q] * (x * (1.0f - x));
+        for (int rb = 0; rb < 2; ++rb) {
+            const int r = 16 * rb + i16;
+            f32x4 v = acc[rb];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float x = (bf_at(xr[rb][0], q) + bf_at(xr[rb][1], q)) + bf_at(xr[rb][2], q);
+                v[q] = v[q] * (x * (1.0f - x));
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v, rc, (r * D + 128 * half + 16 * wave + 4 * g) * 4, 0, 0);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(v, rc, (r * D + 128 * half + 16 * wave + 4 * g) * 4, 0, 0);
+        return 2;
     };
 
     if (t_beg < t_end) {
@@ -2864,9 +2876,11 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
         convert(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();
-        // per iteration: the DMA of tile t + 1, the sigma' MFMAs of tile t, then its TN MFMAs with the rest of the
-        // iteration's work issued behind them, one piece per 16-column block: the two epilogue row blocks of tile t,
-        // then (its DMA landed: only those two stores are younger) tile t + 1's six row conversions; one barrier
+        // per iteration: the DMA of tile t + 1, the sigma' MFMAs of tile t, its epilogue, its TN MFMAs, then tile t + 1's
+        // conversion once its DMA has landed (only the epilogue's stores younger); one barrier.  Measured and not kept
+        // (round 6, profiles/r06/ab_sigma_tn_b3_r06b.txt): the epilogue and the conversion issued behind the TN MFMAs,
+        // one piece per column block (5.24 vs 4.99 ms per config-3 launch), and s_setprio 1 for waves 4-7 of that form
+        // (5.25-5.32); waves 4-7 running TN before sigma' (profiles/r06/ab_sigma_tn_b3_r06a.txt: 4.99-5.02 vs 4.78-4.89)
         {
             int b = 0;
             for (long long t = t_beg; t < t_end; ++t) {
@@ -2874,14 +2888,12 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
                 if (more) stage(t + 1, b ^ 1);
                 f32x4 acc[2];
                 mfma_sigma(b, acc);
-                mfma_tn(b, [&](int nb) __attribute__((always_inline)) {
-                    if (nb < 2) {
-                        epilogue_rb(t, b, acc[nb], nb);
-                    } else if (more) {
-                        if (nb == 2) wait_vm(2);
-                        convert_row(b ^ 1, nb - 2);
-                    }
-                });
+                const int ns = epilogue(t, b, acc);
+                mfma_tn(b);
+                if (more) {
+                    wait_vm(ns);
+                    convert(b ^ 1);
+                }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
