@@ -414,9 +414,11 @@ def _owner_worker(rank, world, port, q, staged, N, R, D, gemm):
                     eng.finish_pending()
                     P1 = P.buf.cpu().numpy()               # the weights after the first step
             eng.finish_pending()
+            if owner:           # the row-partitioned Adam moments of E, gathered whole (a checkpoint)
+                opt.gather_owned_state(eng.row_shard)
             torch.cuda.synchronize()
             res[owner] = (P.buf.cpu().numpy(), opt.m[a * D:b * D].cpu().numpy(), opt.v[a * D:b * D].cpu().numpy(), dE0,
-                          P1)
+                          P1, opt.m[:N * D].cpu().numpy(), opt.v[:N * D].cpu().numpy())
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -448,6 +450,9 @@ def test_node_sharded_owner_e_adam(world, staged, cuda):
     nE = N * D
     for _, res in out:
         own, ar = res[True], res[False]
+        # KerasAdam.gather_owned_state: every rank holds the whole E moments, the owners' rows
+        assert all(np.array_equal(res[True][5], o[1][True][5]) and np.array_equal(res[True][6], o[1][True][6])
+                   for o in out)
         if world == 2:
             assert all(np.array_equal(x, y) for x, y in zip(own, ar))
         else:
@@ -456,6 +461,7 @@ def test_node_sharded_owner_e_adam(world, staged, cuda):
             # consistency above.)
             assert np.array_equal(own[4][nE:], ar[4][nE:])
             assert np.abs(own[4][:nE] - ar[4][:nE]).max() <= 1e-6 * np.abs(ar[4][:nE]).max()
+            assert np.abs(own[5] - ar[5]).max() <= 1e-5 * np.abs(ar[5]).max()      # gathered m vs replicated m
     # the first step's dE, owned rows assembled, against the full batch at the same (initial) parameters
     pos, neg = synthetic_graph(N, R, 9000, seed=77)
     tri = np.concatenate([pos, neg])

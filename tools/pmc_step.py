@@ -18,7 +18,7 @@ from tools.pmc_traffic import load  # noqa: E402
 
 def steps(df):
     df = df.sort_values("Dispatch_Id").reset_index(drop=True)
-    adam = df.index[df["Kernel_Name"].str.startswith("adam_kernel")].tolist()
+    adam = df.index[df["Kernel_Name"].str.contains("adam_kernel", regex=False)].tolist()
     ends = adam[1::2]                        # the dense-segment Adam closes a step
     cuts = [-1] + ends
     return [df.iloc[cuts[i] + 1:cuts[i + 1] + 1] for i in range(len(ends))]
