@@ -2014,13 +2014,15 @@ __device__ __forceinline__ void split3x4(const f32x4& v, bf16x4& p0, bf16x4& p1,
 // a staged fp32 row of 256 values (bytes [0, 1024) of `row`) -> its three bf16 planes in place: plane j at
 // bytes [512 j, 512 j + 512), column k at byte 2k of its plane.  The wave's one ds_read_b128 of the whole row
 // precedes (data dependence) the stores that overwrite it.
-__device__ __forceinline__ void row_to_planes3(char* row, int lane) {
-    const f32x4 x = ld4(reinterpret_cast<const float*>(row) + lane * 4);
+__device__ __forceinline__ void planes_from3(const f32x4& x, char* row, int lane) {
     bf16x4 p0, p1, p2;
     split3x4(x, p0, p1, p2);
     *reinterpret_cast<bf16x4*>(row + lane * 8) = p0;
     *reinterpret_cast<bf16x4*>(row + 512 + lane * 8) = p1;
     *reinterpret_cast<bf16x4*>(row + 1024 + lane * 8) = p2;
+}
+__device__ __forceinline__ void row_to_planes3(char* row, int lane) {
+    planes_from3(ld4(reinterpret_cast<const float*>(row) + lane * 4), row, lane);
 }
 
 // ---- row GEMM, bf16x3 operands: C = epilogue(A B) over T rows --------------------------------------------
@@ -2046,7 +2048,6 @@ constexpr int PITCH = 1568;                 // A row slot: three 512-B planes + 
 constexpr int ABYTES = TR * PITCH;          // 50,176 B per A buffer (two buffers)
 constexpr int RPW = TR / NW;                // A rows each wave stages and converts
 constexpr int SLAB = TR * CWV;              // floats of a [32 rows][16 columns] slab
-constexpr int PF = 2;                       // L2 prefetch of the A tile this many tiles beyond the one being DMA'd
 }  // namespace rb3
 // float offset of (slot, 16-B column group g) in a [32][16] slab: groups XOR (-(slot / 4)) & 3, so the
 // epilogue's ds_read_b128 (slot l&15 [+16], group l>>4) is conflict-free in each of its four lane groups
@@ -2058,7 +2059,7 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
     static_assert(NV >= 0 && NV <= 2 && !(NV > 0 && AUX), "b3: gathered forward (NV = R = 1, 2), sigma' backward, plain");
     static_assert(!BC || NV == 0, "BC: one broadcast V row per relation (R <= 2), e.g. dz W_a^T");
     constexpr int NSL = NV + (AUX ? 1 : 0);
-    constexpr int WF = NSL * SLAB + 64 + 64 + 32 + 256;         // slabs, coef [32][R], idx [64], cmp [32], prefetch KiB
+    constexpr int WF = NSL * SLAB + 64 + 64 + 32;               // slabs, coef [32][R], idx [64], cmp [32]
     constexpr int LDSB = 2 * ABYTES + NW * WF * 4;
     static_assert(LDSB <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(16))) char lds[LDSB];
@@ -2074,7 +2075,6 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
     float* coefw = slabw + NSL * SLAB;
     int* idxw = reinterpret_cast<int*>(coefw + 64);
     int* cmpw = idxw + 64;
-    float* pfw = reinterpret_cast<float*>(cmpw + 32);          // L2-prefetch landing KiB (never read)
 
     const long long ntiles = ((long long)p.M + TR - 1) / TR;
     const long long t_beg = (long long)range * p.tiles_per_block;
@@ -2114,6 +2114,11 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
         __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)idxw, 4, 0, 0);
         return 1;
     };
+    // Measured and not kept (round 6, profiles/r06/ab_gemm_rega_r06j.txt): the A rows through registers
+    // (global_load_dwordx4, converted from there, no fp32 copy in LDS) instead of LDS-DMA: forward 3.216 vs 3.145 ms,
+    // sigma' 3.212 vs 3.136, only the plain form faster (2.770 vs 2.843).  And the L2 prefetch of the A tile two tiles
+    // ahead that this loop had through round 6 is gone: forward 3.277 -> 3.119 ms, sigma' 3.289 -> 3.120, plain 2.933
+    // -> 2.834 (profiles/r06/ab_gemm_nopf_r06i.txt): its DMA cost the issuing waves more than the L2 hits saved.
     auto dma_A = [&](long long t, int bb) __attribute__((always_inline)) -> int {
         if (t >= t_end) return 0;
 #pragma unroll
@@ -2123,14 +2128,6 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
             __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)(lds + bb * ABYTES + r * PITCH), 16, 0, 0);
         }
         return RPW;
-    };
-    // L2 prefetch of this wave's 4 A rows of tile t: one DMA, a 16-B read per 64 B (16 lanes per row) into a
-    // wave-private scratch KiB of LDS that nothing reads; the later A DMA of the tile then hits L2
-    auto prefetch = [&](long long t) __attribute__((always_inline)) -> int {
-        if (t >= t_end) return 0;
-        const float* src = p.A + clampe(t * TR + wave * RPW + (lane >> 4)) * D + (lane & 15) * 16;
-        __builtin_amdgcn_global_load_lds((gbl_vptr)src, (lds_vptr)pfw, 16, 0, 0);
-        return 1;
     };
     auto convert = [&](int bb) __attribute__((always_inline)) {
 #pragma unroll
@@ -2303,7 +2300,7 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
         acc[1] = hi1 + lo1;
     };
 
-    // prologue: indices, A and slabs of t_beg; A converted; indices of t_beg + 1; L2 prefetch of the first tiles
+    // prologue: indices, A and slabs of t_beg; A converted; indices of t_beg + 1
     dma_idx(t_beg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     dma_A(t_beg, 0);
@@ -2312,10 +2309,9 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
     convert(0);
     dma_idx(t_beg + 1);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    for (int k = 1; k <= PF; ++k) prefetch(t_beg + k);
     __syncthreads();
 
-    // per iteration t: A(t+1) DMA, then the L2 prefetch of A(t+1+PF); waves 4-7 run epilogue(t-1) and the slab /
+    // per iteration t: A(t+1) loads; waves 4-7 run epilogue(t-1) and the slab /
     // index DMAs of t, t+1 before MFMA(t), waves 0-3 epilogue(t) and those of t+1, t+2 after it
 #define B3_MAIN_LOOP(LATE)                                                                           \
     {                                                                                                \
@@ -2324,10 +2320,9 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
         for (long long t = t_beg; t < t_end; ++t) {                                                  \
             const bool more = t + 1 < t_end;                                                         \
             const int nA = dma_A(t + 1, b ^ 1);                                                      \
-            const int npf = prefetch(t + 1 + PF);                                                 \
-            int after_A = npf;                      /* ops issued after A(t+1) */                    \
+            int after_A = 0;                        /* ops issued after A(t+1) */                    \
             if (LATE && t > t_beg) {                                                                 \
-                wait_vm(nA + npf);                  /* slabs(t-1), idx(t) */                         \
+                wait_vm(nA);                        /* slabs(t-1), idx(t) */                         \
                 after_A += epilogue(t - 1, acc);                                                     \
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
                 after_A += dma_slabs(t);                                                             \
@@ -2341,7 +2336,7 @@ __global__ __launch_bounds__(512) void rowgemm256_b3_kernel(RowGemmP p, int n_ra
                     convert(b ^ 1);                                                                  \
                 }                                                                                    \
             } else {                                                                                 \
-                wait_vm(nA + npf);                  /* slabs(t), idx(t+1) */                         \
+                wait_vm(nA);                        /* slabs(t), idx(t+1) */                         \
                 after_A += epilogue(t, acc);                                                         \
                 if (more) {                                                                          \
                     wait_vm(after_A);               /* A(t+1) */                                     \
@@ -2569,6 +2564,10 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
 // tile.  Every LDS read of the loop is issued in asm with a tied lgkmcnt wait (no compiler vmcnt drain of the DMAs).
 namespace st3 {
 constexpr int D = 256, TR = 32, DP = 1536, XP = 768, DOB = TR * DP, XB = TR * XP, BUF = DOB + XB, NBUF = 2;
+#ifndef ST3_ROLES
+#define ST3_ROLES 1
+#endif
+constexpr int ROLES = ST3_ROLES;
 }  // namespace st3
 // three transposed reads at a, a + PS, a + 2 PS (the three planes of one 4-row block).  Every multi-instruction asm
 // read here marks its outputs early-clobber ("=&v"): without it the compiler may give an output the input address
@@ -2636,7 +2635,7 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
 
     // fp32 rows of tile t into buffer bb: dO rows 4w .. 4w+3 (one full-wave DMA each), X-half rows 4w .. 4w+3 (a pair
     // per full-wave DMA); rows past M as fp32 zeros (0 x whatever-bits could be NaN in the TN).  Returns the DMA count.
-    auto stage = [&](long long t, int bb) __attribute__((always_inline)) -> int {
+    auto stage = [&](long long t, int bb, int wave) __attribute__((always_inline)) -> int {
         const int lane = fresh_lane();
         char* base = lds + bb * BUF;
         const long long t0 = t * TR;
@@ -2677,7 +2676,7 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
     };
     // this wave's rows of buffer bb, fp32 -> three bf16 planes in place: the six 1-KiB reads first (one wait), then the
     // writes (a row's planes overwrite its own fp32 bytes and, for an X pair, the second row's)
-    auto convert = [&](int bb) __attribute__((always_inline)) {
+    auto convert = [&](int bb, int wave) __attribute__((always_inline)) {
         char* base = lds + bb * BUF;
         const int lane = fresh_lane();
         u32x4 v[6];
@@ -2871,9 +2870,9 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
     };
 
     if (t_beg < t_end) {
-        stage(t_beg, 0);
+        stage(t_beg, 0, wave);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        convert(0);
+        convert(0, wave);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();
         // per iteration: the DMA of tile t + 1, the sigma' MFMAs of tile t, its epilogue, its TN MFMAs, then tile t + 1's
@@ -2883,16 +2882,29 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
         // (5.25-5.32); waves 4-7 running TN before sigma' (profiles/r06/ab_sigma_tn_b3_r06a.txt: 4.99-5.02 vs 4.78-4.89)
         {
             int b = 0;
+            // ROLES: waves 0-3 stage and convert the rows of their SIMD's partner wave (w + 4) too, so waves 4-7 run
+            // only MFMAs and their epilogue: they start the tile's MFMAs at once and finish with no conversion
+            // (1: the conversions after the TN MFMAs, 2: between the epilogue and the TN MFMAs)
+            const bool stager = ROLES == 0 || wave < 4;
             for (long long t = t_beg; t < t_end; ++t) {
                 const bool more = t + 1 < t_end;
-                if (more) stage(t + 1, b ^ 1);
+                if (more && stager) {
+                    stage(t + 1, b ^ 1, wave);
+                    if (ROLES != 0) stage(t + 1, b ^ 1, wave + 4);
+                }
                 f32x4 acc[2];
                 mfma_sigma(b, acc);
                 const int ns = epilogue(t, b, acc);
-                mfma_tn(b);
-                if (more) {
+                if (ROLES == 2 && more && stager) {
                     wait_vm(ns);
-                    convert(b ^ 1);
+                    convert(b ^ 1, wave);
+                    convert(b ^ 1, wave + 4);
+                }
+                mfma_tn(b);
+                if (ROLES != 2 && more && stager) {
+                    wait_vm(ns);
+                    convert(b ^ 1, wave);
+                    if (ROLES != 0) convert(b ^ 1, wave + 4);
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
