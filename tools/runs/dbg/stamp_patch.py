@@ -7,7 +7,7 @@ Writes <out>/iddgcn_amd/csrc/iddgcn_hip.hip (+ include/) with s_memtime stamps a
 plus s_memrealtime (100 MHz) beside stamps 0 and 4, and an exported iddgcn_dbg_stamps(dst, bytes) that copies the
 table to the host.  Vector stores from lane 0 only.  Not product code: tools/runs/dbg/stamp_fwd.py drives it.
 
-usage: python tools/runs/dbg/stamp_patch.py OUTDIR [rowgemm|sigma_tn]
+usage: python tools/runs/dbg/stamp_patch.py OUTDIR [rowgemm|rowgemm_fine|sigma_tn]
 """
 import os
 import shutil
@@ -54,6 +54,60 @@ def patch_sigma_tn(src):
     return src
 
 
+FINE_LOOP = r"""        f32x4 acc[2];                                                                                \
+        int b = 0;                                                                                   \
+        for (long long t = t_beg; t < t_end; ++t) {                                                  \
+            const bool more = t + 1 < t_end; STAMPF(0);                                              \
+            const int nA = dma_A(t + 1, b ^ 1); STAMPF(1);                                           \
+            int after_A = 0;                                                                         \
+            if (LATE && t > t_beg) {                                                                 \
+                wait_vm(nA); STAMPF(2);                                                              \
+                after_A += epilogue(t - 1, acc); STAMPF(3);                                          \
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
+                after_A += dma_slabs(t); STAMPF(4);                                                  \
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
+                after_A += dma_idx(t + 1); STAMPF(5);                                                \
+            }                                                                                        \
+            STAMPF(6); mfma_tile(b, acc); asm volatile("" :: "v"(acc[0]), "v"(acc[1]) : "memory"); STAMPF(7); \
+            if (LATE) {                                                                              \
+                if (more) {                                                                          \
+                    wait_vm(after_A); STAMPF(8);                                                     \
+                    convert(b ^ 1); STAMPF(9);                                                       \
+                }                                                                                    \
+            } else {                                                                                 \
+                wait_vm(nA); STAMPF(8);                                                              \
+                after_A += epilogue(t, acc); STAMPF(9);                                              \
+                if (more) {                                                                          \
+                    wait_vm(after_A); STAMPF(10);                                                    \
+                    convert(b ^ 1); STAMPF(11);                                                      \
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                               \
+                    dma_slabs(t + 1); STAMPF(12);                                                    \
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                               \
+                    dma_idx(t + 2); STAMPF(13);                                                      \
+                }                                                                                    \
+            }                                                                                        \
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); STAMPF(14);                           \
+            __builtin_amdgcn_s_barrier();                                                            \
+            asm volatile("" ::: "memory"); STAMPF(15);                                               \
+            b ^= 1;                                                                                  \
+        }                                                                                            \
+"""
+
+
+def patch_rowgemm_fine(src):
+    """16 stamps per tile in rowgemm256_b3_kernel's loop (see FINE_LOOP); table [32][16][16]."""
+    i0 = src.index("#define B3_MAIN_LOOP(LATE)")
+    i1 = src.index("        if (LATE) {                                                                                  \\\n"
+                   "            asm volatile(\"s_waitcnt vmcnt(0)\"", i0)
+    head = src[i0:src.index("\n", i0) + 1] + "    {                                                                                                \\\n"
+    src = src[:i0] + ("    const bool stamp_on = bx < 16 && (wave == 0 || wave == 4);\n"
+                      "    const int sidx = bx * 2 + (wave >= 4 ? 1 : 0);\n"
+                      "#define STAMPF(k) do { if (stamp_on && (t - t_beg) < 16) { const unsigned long long ts_ = "
+                      "__builtin_amdgcn_s_memtime(); if (lane == 0) g_stampf[(sidx * 16 + (int)(t - t_beg)) * 16 + (k)] = ts_; } } "
+                      "while (0)\n") + head + FINE_LOOP + src[i1:]
+    return src
+
+
 def main(out, kernel="rowgemm"):
     os.makedirs(os.path.join(out, "iddgcn_amd", "csrc"), exist_ok=True)
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(out, "include"), dirs_exist_ok=True)
@@ -61,6 +115,15 @@ def main(out, kernel="rowgemm"):
     src = rep(src, "}  // namespace rb3\n",
               "}  // namespace rb3\n"
               "__device__ unsigned long long g_stamp[32 * 16 * 8];\n")
+    if kernel == "rowgemm_fine":
+        src = rep(src, "__device__ unsigned long long g_stamp[32 * 16 * 8];\n",
+                  "__device__ unsigned long long g_stamp[32 * 16 * 8];\n__device__ unsigned long long g_stampf[32 * 16 * 16];\n")
+        src = patch_rowgemm_fine(src)
+        src += ('\nextern "C" int iddgcn_dbg_stamps(void* dst, long long bytes) {\n'
+                '    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stampf), (size_t)bytes, 0, hipMemcpyDeviceToHost);\n'
+                '}\n')
+        open(os.path.join(out, "iddgcn_amd", "csrc", "iddgcn_hip.hip"), "w").write(src)
+        return
     if kernel == "sigma_tn":
         src = patch_sigma_tn(src)
         src += ('\nextern "C" int iddgcn_dbg_stamps(void* dst, long long bytes) {\n'
