@@ -45,6 +45,16 @@ def main():
                     if s[wg * 2, t, 0] and s[wg * 2 + w, t, k]]
             meds.append(f"{k}:{statistics.median(vals):.0f}" if vals else f"{k}:-")
         print(f"  {label}: " + " ".join(meds))
+    if hasattr(lib, "iddgcn_dbg_stampx"):
+        bx = np.zeros(32 * 16 * 4, dtype=np.uint64)
+        assert lib.iddgcn_dbg_stampx(ctypes.c_void_p(bx.ctypes.data), ctypes.c_longlong(bx.nbytes)) == 0
+        x = bx.reshape(32, 16, 4).astype(np.int64)
+        # the slab wait split: done when only (A, idx, slabs) / (A, idx) are younger
+        for w, ks, label in ((1, (0, 1), "late: older-than-slabs done, slabs done"),
+                             (0, (2, 3), "early: older-than-slabs done, slabs done")):
+            vals = [[x[wg * 2 + w, t, k] - s[wg * 2, t, 0] for wg in range(16) for t in range(2, 15)
+                     if s[wg * 2, t, 0] and x[wg * 2 + w, t, k]] for k in ks]
+            print(f"  {label}: " + " ".join(f"{statistics.median(v):.0f}" if v else "-" for v in vals))
 
 
 if __name__ == "__main__":

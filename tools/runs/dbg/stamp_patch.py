@@ -61,7 +61,7 @@ FINE_LOOP = r"""        f32x4 acc[2];                                           
             const int nA = dma_A(t + 1, b ^ 1); STAMPF(1);                                           \
             int after_A = 0;                                                                         \
             if (LATE && t > t_beg) {                                                                 \
-                wait_vm(nA); STAMPF(2);                                                              \
+                wait_vm(nA + 4); STAMPX(0); wait_vm(nA + 1); STAMPX(1); wait_vm(nA); STAMPF(2);                                                              \
                 after_A += epilogue(t - 1, acc); STAMPF(3);                                          \
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                   \
                 after_A += dma_slabs(t); STAMPF(4);                                                  \
@@ -75,7 +75,7 @@ FINE_LOOP = r"""        f32x4 acc[2];                                           
                     convert(b ^ 1); STAMPF(9);                                                       \
                 }                                                                                    \
             } else {                                                                                 \
-                wait_vm(nA); STAMPF(8);                                                              \
+                wait_vm(nA + 4); STAMPX(2); wait_vm(nA + 1); STAMPX(3); wait_vm(nA); STAMPF(8);                                                              \
                 after_A += epilogue(t, acc); STAMPF(9);                                              \
                 if (more) {                                                                          \
                     wait_vm(after_A); STAMPF(10);                                                    \
@@ -104,6 +104,9 @@ def patch_rowgemm_fine(src):
                       "    const int sidx = bx * 2 + (wave >= 4 ? 1 : 0);\n"
                       "#define STAMPF(k) do { if (stamp_on && (t - t_beg) < 16) { const unsigned long long ts_ = "
                       "__builtin_amdgcn_s_memtime(); if (lane == 0) g_stampf[(sidx * 16 + (int)(t - t_beg)) * 16 + (k)] = ts_; } } "
+                      "while (0)\n"
+                      "#define STAMPX(k) do { if (stamp_on && (t - t_beg) < 16) { const unsigned long long ts_ = "
+                      "__builtin_amdgcn_s_memtime(); if (lane == 0) g_stampx[(sidx * 16 + (int)(t - t_beg)) * 4 + (k)] = ts_; } } "
                       "while (0)\n") + head + FINE_LOOP + src[i1:]
     return src
 
@@ -117,10 +120,14 @@ def main(out, kernel="rowgemm"):
               "__device__ unsigned long long g_stamp[32 * 16 * 8];\n")
     if kernel == "rowgemm_fine":
         src = rep(src, "__device__ unsigned long long g_stamp[32 * 16 * 8];\n",
-                  "__device__ unsigned long long g_stamp[32 * 16 * 8];\n__device__ unsigned long long g_stampf[32 * 16 * 16];\n")
+                  "__device__ unsigned long long g_stamp[32 * 16 * 8];\n__device__ unsigned long long g_stampf[32 * 16 * 16];\n"
+                  "__device__ unsigned long long g_stampx[32 * 16 * 4];\n")
         src = patch_rowgemm_fine(src)
         src += ('\nextern "C" int iddgcn_dbg_stamps(void* dst, long long bytes) {\n'
                 '    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stampf), (size_t)bytes, 0, hipMemcpyDeviceToHost);\n'
+                '}\n'
+                'extern "C" int iddgcn_dbg_stampx(void* dst, long long bytes) {\n'
+                '    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stampx), (size_t)bytes, 0, hipMemcpyDeviceToHost);\n'
                 '}\n')
         open(os.path.join(out, "iddgcn_amd", "csrc", "iddgcn_hip.hip"), "w").write(src)
         return
