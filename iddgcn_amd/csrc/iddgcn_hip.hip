@@ -2560,14 +2560,11 @@ __global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long lo
 // wave that DMA'd them converts them in place (all six reads before any write) to three bf16 planes (plane j at byte
 // 512 j / 256 j of the slot) with 16-B chunk c of row r at c ^ stn_sw(r).  Every slot starts at bank 0, so the
 // conflict analysis of sigma_tn_bf16_kernel's 512 / 256-B slots holds for the ds_read_b128 row fragments and the
-// transposed reads alike.  Tile t + 1 is DMA'd while tile t computes and converted after its MFMAs; one barrier per
-// tile.  Every LDS read of the loop is issued in asm with a tied lgkmcnt wait (no compiler vmcnt drain of the DMAs).
+// transposed reads alike.  Tile t + 1 is DMA'd while tile t computes and converted after its MFMAs, both by waves 0-3
+// for their SIMD's two waves (waves 4-7: MFMAs and epilogue only); one barrier per tile.  Every LDS read of the loop
+// is issued in asm with a tied lgkmcnt wait (no compiler vmcnt drain of the DMAs).
 namespace st3 {
 constexpr int D = 256, TR = 32, DP = 1536, XP = 768, DOB = TR * DP, XB = TR * XP, BUF = DOB + XB, NBUF = 2;
-#ifndef ST3_ROLES
-#define ST3_ROLES 1
-#endif
-constexpr int ROLES = ST3_ROLES;
 }  // namespace st3
 // three transposed reads at a, a + PS, a + 2 PS (the three planes of one 4-row block).  Every multi-instruction asm
 // read here marks its outputs early-clobber ("=&v"): without it the compiler may give an output the input address
@@ -2882,29 +2879,26 @@ __global__ __launch_bounds__(512) void sigma_tn_b3_kernel(long long M, int tiles
         // (5.25-5.32); waves 4-7 running TN before sigma' (profiles/r06/ab_sigma_tn_b3_r06a.txt: 4.99-5.02 vs 4.78-4.89)
         {
             int b = 0;
-            // ROLES: waves 0-3 stage and convert the rows of their SIMD's partner wave (w + 4) too, so waves 4-7 run
-            // only MFMAs and their epilogue: they start the tile's MFMAs at once and finish with no conversion
-            // (1: the conversions after the TN MFMAs, 2: between the epilogue and the TN MFMAs)
-            const bool stager = ROLES == 0 || wave < 4;
+            // Split roles: waves 0-3 stage and convert the rows of their SIMD's partner wave (w + 4) too, so waves 4-7
+            // run only MFMAs and their epilogue: they start the tile's MFMAs at once and end it with no conversion.
+            // 4.83 vs 4.98-5.04 ms per config-3 launch for every wave staging and converting its own rows; the
+            // conversions between the epilogue and the TN MFMAs instead of after them 4.89-4.90
+            // (profiles/r06/ab_sigma_tn_roles_r06l.txt, phase stamps in profiles/r06/stamps)
+            const bool stager = wave < 4;
             for (long long t = t_beg; t < t_end; ++t) {
                 const bool more = t + 1 < t_end;
                 if (more && stager) {
                     stage(t + 1, b ^ 1, wave);
-                    if (ROLES != 0) stage(t + 1, b ^ 1, wave + 4);
+                    stage(t + 1, b ^ 1, wave + 4);
                 }
                 f32x4 acc[2];
                 mfma_sigma(b, acc);
                 const int ns = epilogue(t, b, acc);
-                if (ROLES == 2 && more && stager) {
+                mfma_tn(b);
+                if (more && stager) {
                     wait_vm(ns);
                     convert(b ^ 1, wave);
                     convert(b ^ 1, wave + 4);
-                }
-                mfma_tn(b);
-                if (ROLES != 2 && more && stager) {
-                    wait_vm(ns);
-                    convert(b ^ 1, wave);
-                    if (ROLES != 0) convert(b ^ 1, wave + 4);
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
