@@ -45,6 +45,14 @@ def main():
                     if s[wg * 2, t, 0] and s[wg * 2 + w, t, k]]
             meds.append(f"{k}:{statistics.median(vals):.0f}" if vals else f"{k}:-")
         print(f"  {label}: " + " ".join(meds))
+    if hasattr(lib, "iddgcn_dbg_rt"):      # s_memrealtime (100 MHz) beside stamps 0 and 15: the in-kernel clock
+        br = np.zeros(32 * 16 * 2, dtype=np.uint64)
+        assert lib.iddgcn_dbg_rt(ctypes.c_void_p(br.ctypes.data), ctypes.c_longlong(br.nbytes)) == 0
+        rt = br.reshape(32, 16, 2).astype(np.int64)
+        clk = [(s[j, t, 15] - s[j, t, 0]) / (rt[j, t, 1] - rt[j, t, 0]) * 0.1 for j in range(32) for t in range(2, 15)
+               if rt[j, t, 1] > rt[j, t, 0] and s[j, t, 15] and s[j, t, 0]]
+        if clk:
+            print(f"  in-kernel clock {statistics.median(clk):.3f} GHz (n={len(clk)})")
     if hasattr(lib, "iddgcn_dbg_stampx"):
         bx = np.zeros(32 * 16 * 4, dtype=np.uint64)
         assert lib.iddgcn_dbg_stampx(ctypes.c_void_p(bx.ctypes.data), ctypes.c_longlong(bx.nbytes)) == 0
