@@ -2379,10 +2379,21 @@ __device__ __forceinline__ bf16x8 tr_frag_b3(const char* p0) {
     const v4s16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((l4p)(p0 + 4 * tb3::PT));
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
-__global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M, long long rows_per_block,
-                                                            const float* __restrict__ A, const float* __restrict__ B,
-                                                            float* __restrict__ slab) {
+// Batched (TnBatch.n > 0, as gemm_tn256_x3_kernel): blockIdx.y = entry, each entry its own operands, row split and
+// slab region — a layer's node-level TNs (dS head part, dK_r) in one launch of ~256 workgroups instead of one launch
+// of 256 per entry, each with its prologue, its drain and 256 partial slabs to sum.
+__global__ __launch_bounds__(512) void gemm_tn256_b3_kernel(long long M_, long long rpb_, const float* __restrict__ A_,
+                                                            const float* __restrict__ B_, float* __restrict__ slab_,
+                                                            TnBatch tb) {
     using namespace tb3;
+    const bool bat = tb.n > 0;
+    const int ent = bat ? (int)blockIdx.y : 0;
+    if (bat && (int)blockIdx.x >= tb.nb[ent]) return;     // past this entry's slabs (whole workgroup)
+    const long long M = bat ? tb.M[ent] : M_;
+    const long long rows_per_block = bat ? tb.rpb[ent] : rpb_;
+    const float* __restrict__ A = bat ? tb.A[ent] : A_;
+    const float* __restrict__ B = bat ? tb.B[ent] : B_;
+    float* __restrict__ slab = bat ? tb.slab[ent] : slab_;
     static_assert(NBUF * BUF <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(16))) char lds[NBUF * BUF];     // [buf][A | B][TK][PT]
     const int lane = threadIdx.x & 63;
@@ -4998,7 +5009,7 @@ int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const f
     if (rpb < 32) rpb = 32;
 #define TNK(DD) hipLaunchKernelGGL(gemm_tn_kernel<DD>, dim3(n_blocks), dim3(TN<DD>::NW * 64), 0, st, M, rpb, A, B, slab)
     if (d == 256 && precision == IDDGCN_GEMM_BF16X3) {
-        hipLaunchKernelGGL(gemm_tn256_b3_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab);
+        hipLaunchKernelGGL(gemm_tn256_b3_kernel, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab, TnBatch{});
     } else if (d == 256 && precision == IDDGCN_GEMM_SPLIT_F16) {
         hipLaunchKernelGGL(gemm_tn256_x3_kernel<>, dim3(n_blocks), dim3(512), 0, st, M, rpb, A, B, slab, TnBatch{});
     } else if (d == 256) {
@@ -5026,7 +5037,8 @@ int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n,
         if (e[k].M < 0 || (e[k].M > 0 && (!e[k].A || !e[k].B)) || !e[k].C) return IDDGCN_E_BAD_ARG;
     hipStream_t st = (hipStream_t)stream;
     const long long dd = (long long)d * d;
-    if (!(d == 256 && precision == IDDGCN_GEMM_SPLIT_F16)) {
+    const bool b3 = d == 256 && precision == IDDGCN_GEMM_BF16X3;
+    if (!(d == 256 && (precision == IDDGCN_GEMM_SPLIT_F16 || b3))) {
         // other widths and the exact mode: the single-call kernels one after another (slab reused in order)
         for (int k = 0; k < n; ++k) {
             if (e[k].M == 0) {                     // no rows: C = 0, or C unchanged when accumulating
@@ -5068,8 +5080,12 @@ int iddgcn_gemm_tn_batched_f32(void* stream, int d, const iddgcn_tn_t* e, int n,
     }
     if (off > slab_floats) return IDDGCN_E_BAD_ARG;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(gemm_tn256_x3_kernel<>, dim3(nbmax, (unsigned)n), dim3(512), 0, st, 0LL, 0LL, nullptr, nullptr,
-                       nullptr, tb);
+    if (b3)
+        hipLaunchKernelGGL(gemm_tn256_b3_kernel, dim3(nbmax, (unsigned)n), dim3(512), 0, st, 0LL, 0LL, nullptr, nullptr,
+                           nullptr, tb);
+    else
+        hipLaunchKernelGGL(gemm_tn256_x3_kernel<>, dim3(nbmax, (unsigned)n), dim3(512), 0, st, 0LL, 0LL, nullptr,
+                           nullptr, nullptr, tb);
     int rc = launch_status();
     if (rc) return rc;
     for (int k = 0; k < n; ++k) launch_reduce_slabs(st, nbk[k], dd, tb.slab[k], e[k].C, e[k].accumulate, 1.0f);

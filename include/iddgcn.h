@@ -155,7 +155,7 @@ int iddgcn_gemm_tn_blocks(long long M, int d);
 int iddgcn_gemm_tn_f32(void* stream, long long M, int d, const float* A, const float* B,
                        float* slab, int n_blocks, float* C, int accumulate, int precision);
 /* Up to IDDGCN_TN_BATCH independent C_k (+)= A_k^T B_k (fp32, same D) in one launch (ABI 5): at D = 256 in the
- * split-fp16 mode one launch of ~256 workgroups shared out over the entries (blockIdx.y = entry), then each
+ * split-fp16 and (round 6) bf16x3 modes one launch of ~256 workgroups shared out over the entries (blockIdx.y = entry), then each
  * entry's partials summed in block order; otherwise the single-call kernels in turn.  slab: slab_floats floats,
  * at least sum_k min(256 / n, ceil(M_k / 32)) * D * D (the single-call fallback uses up to
  * iddgcn_gemm_tn_blocks(M_k, D) partials, fewer when the slab is smaller, at least one D * D).  The node-level weight gradients of one layer: dK_r = AE_r^T dP_r
