@@ -477,6 +477,7 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
         from iddgcn_amd.parallel import NodeShard
         eng.row_shard = NodeShard(cuts)          # node rows split over the ranks, scored edges by tail
         eng.overlap_e_gather = True              # the E all-gather travels into the next step (finished below)
+        eng.split_e_collectives = bool(getattr(args, "split_e", False))   # opt-in: per-owner E pieces (round 6)
     elif shard == "relation" and world > 1:
         eng.node_shard = RelationShard(R, N)     # SURVEY §8(e) alternative: node tables split by relation
     elif shard == "spmm" and world > 1:
@@ -519,7 +520,8 @@ def run_workload(cid, args, world, rank, dev, gemm, other_mode, probe_kernels=Tr
                                                if feat == "bf16" else ""),
            "config": {"workload": cfg["name"], "num_nodes": N, "num_relations": R, "adjacency_edges": M,
                       "scored_edges": T, "scored_edges_per_gpu": ed.T, "feat_dim": D,
-                      "parallelism": (f"node-rows{world}" if eng.row_shard else f"edge-dp{world}")
+                      "parallelism": (f"node-rows{world}" + ("+split-e" if eng.split_e_collectives else "")
+                                      if eng.row_shard else f"edge-dp{world}")
                       + ("+relation-sharded-nodes" if eng.node_shard else "")
                       + ("+row-partitioned-spmm" if eng.spmm_shard else ""),
                       "gemm": gemm, "features": feat, **({"edge_mfma": emfma} if feat == "bf16" else {})},
@@ -591,6 +593,9 @@ def main():
                          "row range, scored edges by tail, parallel.NodeShard), edge partitioning only (node work "
                          "replicated), also relation-sharded node tables, or also row-partitioned SpMMs (A_r E "
                          "all-gathered, dAE reduce-scattered; node GEMMs replicated)")
+    ap.add_argument("--split-e", action="store_true",
+                    help="node rows: E as one broadcast per owner and A_r E as one SpMM per source owner, dE reduced "
+                         "to each owner as the transposed SpMM writes it (Engine.split_e_collectives; opt-in)")
     ap.add_argument("--features", default=None, choices=["f32", "bf16"],
                     help="edge-table storage (default: the config's; bf16 = config 5's perf-only mode)")
     ap.add_argument("--gemm", default="bf16x3", choices=["exact", "bf16x3", "split"],

@@ -651,6 +651,13 @@ class Engine:
     # flight for the next forward to complete after its owner-local work (bench.py's timed loop) — until then the other
     # ranks' rows of params["E"] are stale and must be neither read nor written (finish_pending() completes it)
     overlap_e_gather = False
+    # split E collectives (opt-in, round 6): with owner_e, E travels as one broadcast per owner
+    # instead of one all-gather, and the next forward's A_r E runs as one SpMM per source owner, each after its piece
+    # has landed (the own rows' first); dE is reduced to each owner as soon as the transposed SpMM has written that
+    # owner's rows.  Results within fp32 reordering of the unsplit step (the per-row sums add the owners' partial
+    # sums); bounded to ~2 ms per config-5 rank step by the SpMMs it can hide behind (Multi-GPU)
+    split_e_collectives = False
+    _e_parts = None
 
     def finish_pending(self):
         """Complete the all-gather of E a node-partitioned train_step left in flight (the next forward does it
@@ -658,6 +665,37 @@ class Engine:
         pend, self._e_pending = self._e_pending, None
         if pend is not None:
             pend.wait()
+        parts, self._e_parts = self._e_parts, None
+        if parts is not None:
+            for h in parts.values():
+                h.wait()
+
+    def _owner_csr(self, adj, sh):
+        """The owned rows' forward CSR of every relation cut by the owner of the column (split E collectives): {(r, k):
+        (row_ptr, col, val)} over rows [a, b), each row's entries of owner k in their original order."""
+        key = (id(adj), sh.a, sh.b, tuple(sh.cuts))
+        if getattr(self, "_ocsr_key", None) == key:
+            return self._ocsr
+        N, R = self.N, self.R
+        a, b = sh.a, sh.b
+        dev = adj.fwd_col.device
+        inner = torch.tensor(sh.cuts[1:-1], dtype=torch.int64, device=dev)
+        out = {}
+        for r in range(R):
+            ptr = adj.fwd_ptr[r * (N + 1) + a:r * (N + 1) + b + 1].long()
+            p0, p1 = int(ptr[0]), int(ptr[-1])
+            col = adj.fwd_col[p0:p1]
+            val = adj.fwd_val[p0:p1] if adj.fwd_val is not None else None      # (None: every value 1)
+            rows = torch.repeat_interleave(torch.arange(b - a, device=dev), ptr[1:] - ptr[:-1])
+            own = torch.bucketize(col.long(), inner, right=True)
+            for k in range(sh.world):
+                m = own == k
+                cnt = torch.bincount(rows[m], minlength=b - a)
+                kp = torch.zeros(b - a + 1, dtype=torch.int64, device=dev)
+                kp[1:] = torch.cumsum(cnt, 0)
+                out[(r, k)] = (kp.int().contiguous(), col[m].contiguous(), None if val is None else val[m].contiguous())
+        self._ocsr_key, self._ocsr = key, out
+        return out
 
     def _forward_rows(self, P, adj, ed, ws, train):
         """The forward with the node tables computed for the owned rows [a, b) only (parallel.NodeShard): the
@@ -674,11 +712,27 @@ class Engine:
         if b > a:
             ops.rowgemm(E[a:b], P["S1"], ws.ES1[a:b], **pn)
             ops.alpha_fwd(E[a:b], P["Wa1"], P["ba1"], ws.Ssm[0][a:b], ws.W[0][a:b])
+        parts, self._e_parts = self._e_parts, None
         self.finish_pending()
-        if b > a:
+        if b > a and parts is not None:
+            # split E collectives: A_r E as one SpMM per source owner, the own rows first, each other owner's after
+            # its broadcast has landed; the pieces add into the rows in that order
+            ocsr = self._owner_csr(adj, sh)
+            order = [sh.rank] + [k for k in range(sh.world) if k != sh.rank]
+            for i, k in enumerate(order):
+                if k != sh.rank:
+                    parts[k].wait()
+                for r in range(R):
+                    kp, kc, kv = ocsr[(r, k)]
+                    ops.spmm_csr(kp, kc, kv, E, ws.AE[r][a:b].view(1, b - a, D), 1, b - a, accumulate=i > 0)
+        elif b > a:
             for r in range(R):              # A_r E over the owned rows (IDDGCN.py:69-70)
                 ops.spmm_csr(adj.fwd_ptr[r * (N + 1) + a:r * (N + 1) + b + 1], adj.fwd_col, adj.fwd_val, E,
                              ws.AE[r][a:b].view(1, b - a, D), 1, b - a)
+        if parts is not None:
+            for h in parts.values():
+                h.wait()
+        if b > a:
             proj = [(ws.AE[r][a:b], P[f"K{l + 1}"][r], ws.P[l, r][a:b], pn) for l in range(NUM_LAYERS)
                     for r in range(R)]
             nb = L.ROWGEMM_BATCH
@@ -804,6 +858,18 @@ class Engine:
         G["E"][:a].zero_()
         G["E"][b:].zero_()
         bptr, bcol, bval = adj.bwd_node_rows(a, b)
+        if e_owner and self.split_e_collectives:
+            # split E collectives: the transposed SpMM by destination owner, each owner's dE rows reduced to it as soon
+            # as they are written (owner order on every rank)
+            hs = []
+            for k in range(sh.world):
+                n0, n1 = sh.cuts[k], sh.cuts[k + 1]
+                if n1 > n0:
+                    ops.spmm_csr(bptr[n0:n1 + 1], bcol, bval, ws.dAE.view(R * N, D),
+                                 G["E"][n0:n1].view(1, n1 - n0, D), 1, n1 - n0, accumulate=True)
+                hs.append(sh.reduce_rows(G["E"], k))
+            from .parallel import _All
+            return _All(hs)
         if e_owner:
             ops.spmm_csr(bptr, bcol, bval, ws.dAE.view(R * N, D), G["E"].view(1, N, D), 1, N, accumulate=True)
             return sh.reduce_scatter(G["E"], async_op=True)
@@ -830,7 +896,10 @@ class Engine:
             rs = self.backward(params, grads, adj, ed, ws, comm, e_owner=True)
             D = self.D
             opt.apply_owned(params, grads, comm, rs, sh.a * D, sh.b * D)
-            self._e_pending = sh.all_gather(params["E"], async_op=True)
+            if self.split_e_collectives:
+                self._e_parts = sh.broadcast_rows(params["E"])
+            else:
+                self._e_pending = sh.all_gather(params["E"], async_op=True)
             if not self.overlap_e_gather:
                 self.finish_pending()
             return grads.loss

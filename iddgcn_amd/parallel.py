@@ -326,9 +326,63 @@ class NodeShard:
         return h
 
 
+    def broadcast_rows(self, table):
+        """Every owner's rows [cuts[k], cuts[k+1]) of ``table`` to every rank, one broadcast per owner (split E
+        collectives, round 6: the all-gather of E cut by source owner, so that the next forward's A_r E can start on
+        the pieces already here).  Issued in owner order on every rank; returns {k: handle}.  Until handle k's
+        ``wait()``, kernels must not write rows [cuts[k], cuts[k+1]) nor, for k other than this rank, read them."""
+        hs = {}
+        for k in range(self.world):
+            a, b = self.cuts[k], self.cuts[k + 1]
+            if b <= a:
+                hs[k] = _Done()
+                continue
+            if self._gloo:
+                host = table[a:b].to("cpu", copy=True)
+                dist.broadcast(host, src=k, group=self.group)
+                if k != self.rank:
+                    table[a:b].copy_(host)
+                hs[k] = _Done()
+            else:
+                work = dist.broadcast(table[a:b], src=k, group=self.group, async_op=True)
+                hs[k] = _Pending(work.wait)     # (the own rows: readable at once, writable after wait())
+        return hs
+
+    def reduce_rows(self, table, k):
+        """Rows [cuts[k], cuts[k+1]) of ``table`` summed over the ranks into rank k's table (split E collectives: the
+        reduce-scatter of dE cut by destination owner, each piece issued as soon as the transposed SpMM has written
+        it).  Asynchronous on the device path; other ranks' rows of the piece are left undefined for the caller."""
+        a, b = self.cuts[k], self.cuts[k + 1]
+        if b <= a:
+            return _Done()
+        if self._gloo:
+            host = table[a:b].to("cpu", copy=True)
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+            if k == self.rank:
+                table[a:b].copy_(host)
+            return _Done()
+        if dist.get_backend(self.group) == "gloo":       # (gloo's reduce takes host tensors only)
+            work = dist.all_reduce(table[a:b], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        else:
+            work = dist.reduce(table[a:b], dst=k, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        return _Pending(work.wait)
+
+
 class _Done:
     def wait(self):
         pass
+
+
+class _All:
+    """Handle over several collective handles: wait() completes them all (idempotent)."""
+
+    def __init__(self, hs):
+        self._hs = list(hs)
+
+    def wait(self):
+        hs, self._hs = self._hs, []
+        for h in hs:
+            h.wait()
 
 
 class _Pending:

@@ -10,6 +10,7 @@
   every rank the full-batch gradients, loss and — Adam being replicated — identical weights.
 """
 import os
+import sys
 import socket
 
 import numpy as np
@@ -474,3 +475,82 @@ def test_node_sharded_owner_e_adam(world, staged, cuda):
     full = G["E"].cpu().numpy()
     dE = np.concatenate([res[True][3] for _, res in out])
     assert np.abs(dE - full).max() <= 1e-5 * np.abs(full).max()
+
+
+def _split_worker(rank, world, port, q, staged, N, R, D, gemm):
+    """Two node-partitioned, E-owning training steps with and without the split E collectives (round 6,
+    Engine.split_e_collectives): the parameters after each step, the second step's dE of the owned rows."""
+    import torch.distributed as dist
+    from iddgcn_amd.engine import KerasAdam
+    from iddgcn_amd.parallel import BucketedAllReduce, NodeShard, node_ranges, node_shard_triples
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        pos, neg = synthetic_graph(N, R, 9000, seed=77)
+        tri = np.concatenate([pos, neg])
+        lab = np.concatenate([np.ones(len(pos)), np.zeros(len(neg))])
+        cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), world)
+        mine, mlab = node_shard_triples(tri, lab, cuts, rank)
+        eng = Engine(N, R, D, dev, gemm=gemm)
+        adj = eng.adjacency(get_adj_mats(pos, N, R))
+        ed = eng.edges(mine, mlab)
+        a, b = cuts[rank], cuts[rank + 1]
+        res = {}
+        for split in (False, True):
+            eng.split_e_collectives = split
+            eng.overlap_e_gather = True            # the pieces travel into the next forward, as bench.py runs it
+            eng.row_shard = NodeShard(cuts, staged=staged, owner_e=True)
+            after = []
+            for steps in (1, 2):                   # (two steps back to back: the second forward takes the pieces)
+                print(f"split worker rank {rank}: split {split}, {steps} step(s)", file=sys.stderr, flush=True)
+                P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
+                P.load(_mild(N, R, D, 9))
+                opt = KerasAdam(P)
+                comm = BucketedAllReduce(min_bucket_rows=64, host_staged=staged)
+                for _ in range(steps):
+                    eng.train_step(P, G, opt, adj, ed, t_global=len(tri), comm=comm)
+                dE = G["E"][a:b].cpu().numpy()
+                eng.finish_pending()
+                after.append(P.buf.cpu().numpy())
+            torch.cuda.synchronize()
+            res[split] = (after, dE)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,staged", [(2, None), (2, False), (3, False)])
+def test_node_sharded_split_e_collectives(world, staged, cuda):
+    """VERDICT r05 item 3 (opt-in, round 6): E as one broadcast per owner with the next forward's A_r E as one SpMM per
+    source owner (own rows first), dE reduced to each owner as the transposed SpMM writes its rows.  world 2 / 3 ranks
+    on one GPU over gloo, host-staged (None) and device (False) collectives, two steps: every rank's parameters bitwise
+    equal after each step; against the same steps with the one all-gather / reduce-scatter: the first step's
+    parameters bitwise at world 2 (a + b either way) and within 1e-6 of max|E| at world 3 (another order of the three
+    partials); the second step (its forward takes the pieces: per-row sums added owner by owner) the owned rows' dE
+    within 1e-5 of max|dE| and the parameters within 1e-5 of max|P|."""
+    N, R, D, gemm = 700, 2, 256, "bf16x3"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q, staged, N, R, D, gemm)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, res in out[1:]:
+        for s in (0, 1):
+            assert np.array_equal(res[True][0][s], out[0][1][True][0][s])
+    nE = N * D
+    for _, res in out:
+        (sp, sdE), (un, udE) = res[True], res[False]
+        if world == 2:
+            assert np.array_equal(sp[0], un[0])
+        else:
+            assert np.array_equal(sp[0][nE:], un[0][nE:])
+            assert np.abs(sp[0][:nE] - un[0][:nE]).max() <= 1e-6 * np.abs(un[0][:nE]).max()
+        assert np.abs(sdE - udE).max() <= 1e-5 * np.abs(udE).max()
+        assert np.abs(sp[1] - un[1]).max() <= 1e-5 * np.abs(un[1]).max()

@@ -11,6 +11,8 @@ calls through RCCL on the box's GPU:
   * the node-row step's E ownership (round 5, NodeShard owner_e): dE ``reduce_scatter_tensor`` to the row owners,
     ``KerasAdam.apply_owned``, then the asynchronous ``all_gather_into_tensor`` of E (Engine.finish_pending);
   * ``RelationShard``'s ``all_gather_into_tensor`` / ``reduce_scatter_tensor`` (``--shard relation``);
+  * the split E collectives (round 6, ``Engine.split_e_collectives``): per-owner ``broadcast`` of E and ``reduce`` of
+    dE, the forward's A_r E as one SpMM per source owner (two steps: the second forward takes the broadcast pieces);
   * bench.py's ``rank_consistency`` (broadcast + MAX all-reduce on the device).
 
 With one rank every collective is the identity, so each RCCL step must be BITWISE the same step on a gloo group
@@ -73,8 +75,10 @@ def _child(port, q, N, R, D, gemm, features):
         cuts = node_ranges(np.bincount(tri[:, 2], minlength=N), 1)
         mine, mlab = node_shard_triples(tri, lab, cuts, 0)
 
-        def step(shard, comm):
+        def step(shard, comm, split=False, steps=1):
             eng = Engine(N, R, D, dev, gemm=gemm, features=features)
+            eng.split_e_collectives = split
+            eng.overlap_e_gather = steps > 1    # E's collectives in flight into the next forward (split: its pieces)
             if shard == "node_rccl":
                 eng.row_shard = NodeShard(cuts, staged=False)              # the RCCL ranks' branch
             elif shard == "node_gloo":
@@ -87,7 +91,8 @@ def _child(port, q, N, R, D, gemm, features):
             P, G = FlatParams(N, R, D, dev), FlatParams(N, R, D, dev)
             P.load(_mild(N, R, D, 9))
             opt = KerasAdam(P)
-            loss = eng.train_step(P, G, opt, adj, ed, t_global=len(tri), comm=comm)
+            for _ in range(steps):
+                loss = eng.train_step(P, G, opt, adj, ed, t_global=len(tri), comm=comm)
             eng.finish_pending()        # node rows (owner_e): the all-gather of E the step left in flight
             torch.cuda.synchronize()
             return float(loss.item()), G.buf.cpu().numpy(), P.buf.cpu().numpy(), P.buf
@@ -99,6 +104,8 @@ def _child(port, q, N, R, D, gemm, features):
         res["node_gloo"] = step("node_gloo", BucketedAllReduce(group=gloo, min_bucket_rows=64))
         res["relation_rccl"] = step("relation_rccl", BucketedAllReduce(min_bucket_rows=64))
         res["relation_gloo"] = step("relation_gloo", BucketedAllReduce(group=gloo, min_bucket_rows=64))
+        res["node_rccl_2"] = step("node_rccl", BucketedAllReduce(min_bucket_rows=64), steps=2)
+        res["node_rccl_split_2"] = step("node_rccl", BucketedAllReduce(min_bucket_rows=64), split=True, steps=2)
         consist = rank_consistency(res["node_rccl"][3])
         q.put(("ok", {k: v[:3] for k, v in res.items()}, consist))
     except BaseException as e:                      # report, then let the process exit non-zero
@@ -120,7 +127,8 @@ def test_rccl_world1_collectives_bitwise(N, R, D, gemm, features, cuda):
     assert p.exitcode == 0
     # one rank: every collective is the identity -> bitwise the gloo (host-staged) step, and the edge-partitioned
     # RCCL step (async in-place buckets + bucket-wise Adam) bitwise the step without a communicator
-    for a, b in (("edge_rccl", "plain"), ("node_rccl", "node_gloo"), ("relation_rccl", "relation_gloo")):
+    for a, b in (("edge_rccl", "plain"), ("node_rccl", "node_gloo"), ("relation_rccl", "relation_gloo"),
+                 ("node_rccl_split_2", "node_rccl_2")):
         la, ga, pa = res[a]
         lb, gb, pb = res[b]
         assert la == lb, (a, b, la, lb)
