@@ -673,8 +673,9 @@ class Engine:
     def _owner_csr(self, adj, sh):
         """The owned rows' forward CSR of every relation cut by the owner of the column (split E collectives): {(r, k):
         (row_ptr, col, val)} over rows [a, b), each row's entries of owner k in their original order."""
-        key = (id(adj), sh.a, sh.b, tuple(sh.cuts))
-        if getattr(self, "_ocsr_key", None) == key:
+        # the adjacency itself is held beside the key (an id() could be reused by a later graph)
+        key = (sh.a, sh.b, tuple(sh.cuts))
+        if getattr(self, "_ocsr_adj", None) is adj and self._ocsr_key == key:
             return self._ocsr
         N, R = self.N, self.R
         a, b = sh.a, sh.b
@@ -694,7 +695,7 @@ class Engine:
                 kp = torch.zeros(b - a + 1, dtype=torch.int64, device=dev)
                 kp[1:] = torch.cumsum(cnt, 0)
                 out[(r, k)] = (kp.int().contiguous(), col[m].contiguous(), None if val is None else val[m].contiguous())
-        self._ocsr_key, self._ocsr = key, out
+        self._ocsr_adj, self._ocsr_key, self._ocsr = adj, key, out
         return out
 
     def _forward_rows(self, P, adj, ed, ws, train):
