@@ -179,7 +179,19 @@ def _node_shard_worker(rank, world, port, q, staged):
         # reduce-scatter: every rank holds partials (rank + 1) * row index; owners get the sums
         part = (rank + 1) * torch.arange(N, dtype=torch.float32)[:, None].repeat(1, C)
         sh.reduce_scatter(part)
-        q.put((rank, tab.numpy(), part[sh.a:sh.b].numpy(), (sh.a, sh.b), part.numpy()))
+        # split E collectives: one broadcast per owner, then one reduce per destination owner (owner rows checked only)
+        tb = torch.full((N, C), -1.0)
+        tb[sh.a:sh.b] = torch.arange(sh.a, sh.b, dtype=torch.float32)[:, None] * 10 + torch.arange(C)
+        hs = sh.broadcast_rows(tb)
+        assert sorted(hs) == list(range(world))
+        for k in range(world):
+            hs[k].wait()
+            hs[k].wait()                            # idempotent
+        pr = (rank + 1) * torch.arange(N, dtype=torch.float32)[:, None].repeat(1, C)
+        for k in range(world):
+            sh.reduce_rows(pr, k).wait()
+        q.put((rank, tab.numpy(), part[sh.a:sh.b].numpy(), (sh.a, sh.b), part.numpy(), tb.numpy(),
+               pr[sh.a:sh.b].numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -191,7 +203,9 @@ def test_node_shard_collectives_gloo(world, staged):
     after the all-gather every rank holds every rank's rows; after the reduce-scatter each owner holds the sums
     of the ranks' partials for its rows and the other rows are untouched.  staged=None: the host-staged gloo
     branch; staged=False: the device branch the RCCL ranks take (padded all_gather_into_tensor with the rank's
-    chunk aliased in the output, reduce_scatter_tensor with zeroed padding rows), run here on CPU tensors."""
+    chunk aliased in the output, reduce_scatter_tensor with zeroed padding rows), run here on CPU tensors.  The same
+    for the split E collectives (broadcast_rows: every owner's rows to every rank; reduce_rows: each owner's rows
+    summed into it)."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -205,8 +219,10 @@ def test_node_shard_collectives_gloo(world, staged):
     N = 12
     want = np.arange(N, dtype=np.float32)[:, None] * 10 + np.arange(3)
     tot = sum(range(1, world + 1))
-    for rank, tab, mine, (a, b), part in res:
+    for rank, tab, mine, (a, b), part, tb, pr in res:
         assert np.array_equal(tab, want)
+        assert np.array_equal(tb, want)
+        assert np.array_equal(pr, tot * np.arange(a, b, dtype=np.float32)[:, None].repeat(3, 1))
         assert np.array_equal(mine, tot * np.arange(a, b, dtype=np.float32)[:, None].repeat(3, 1))
         other = np.ones(N, bool)
         other[a:b] = False
